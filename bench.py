@@ -1,0 +1,268 @@
+"""Benchmark: DCF batch eval on MI355X (BASELINE.json metric).
+
+Workload (default, BASELINE.json configs[2] = SURVEY.md §8 C3): N = 16 (128-bit
+x), LAMBDA = 16, Aes256HirosePrg, one key, 2^28 uniformly random points per GPU
+resident in HBM, party 0 (the reference bench's shape, benches/dcf_batch_eval.rs:
+25-30, scaled up).  A step = one `Dcf::eval` pass over the rank's points.  Ranks
+hold disjoint contiguous slices of the global point space (weak scaling); the
+key is generated once on rank 0 and broadcast over RCCL before timing; there is
+no collective inside the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c5]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement" for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import dcf_amd  # noqa: E402
+
+METRIC = "DCF evals/sec (node) at 128-bit input, λ=16B; AES blocks/s vs INT roofline"
+
+# ---- roofline constants (MI355X_MICROARCH.md) ----
+CUS, CLK_HZ = 256, 2.4e9
+LDS_B32_LOOKUPS_PER_CLK_CU = 32          # ds_read_b32: 64 lanes / 2 LDS cycles (§LDS table)
+AES256_LOOKUPS_PER_BLOCK = 14 * 16       # T-table AES-256: 16 table reads per round
+PEAK_LDS_LOOKUPS = CUS * LDS_B32_LOOKUPS_PER_CLK_CU * CLK_HZ
+PEAK_AES_BLOCKS = PEAK_LDS_LOOKUPS / AES256_LOOKUPS_PER_BLOCK  # ~87.8 G blocks/s per GPU
+
+
+def blocks_per_eval(n_bytes: int, lam: int) -> int:
+    """The reference's AES-256 block count per eval: 2 per level at LAMBDA = 16,
+    4 per level at LAMBDA >= 32 (prg.rs:48-53 called once per level, lib.rs:176)."""
+    return (2 if lam == 16 else 4) * 8 * n_bytes
+
+
+def dist_setup(n_gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    if world != n_gpus:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    return world, rank, local
+
+
+def bcast(t: torch.Tensor, world: int):
+    if world > 1:
+        dist.broadcast(t, src=0)
+    return t
+
+
+def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int):
+    """Rank 0 runs gen on its GPU; the CWB and both seeds go to every rank by RCCL broadcast."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    rng = np.random.default_rng(seed)
+    alpha, beta, s0, s1 = rng.bytes(n_bytes), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+    cwb = torch.empty(dcf_amd.cwb_bytes(n_bytes, lam, 1), dtype=torch.uint8, device=dev)
+    seeds = torch.empty((2, lam), dtype=torch.uint8, device=dev)
+    if not world > 1 or dist.get_rank() == 0:
+        k = d.gen(dcf_amd.CmpFn(alpha, beta), [s0, s1], dcf_amd.BoundState.LtBeta)
+        cwb.copy_(torch.from_numpy(np.frombuffer(dcf_amd.share_to_cwb(k, n_bytes, lam), np.uint8).copy()))
+        seeds.copy_(torch.from_numpy(np.frombuffer(s0 + s1, np.uint8).reshape(2, lam).copy()))
+    bcast(cwb, world)
+    bcast(seeds, world)
+    return cwb, seeds, alpha, beta
+
+
+def gen_points(m: int, n_bytes: int, rank: int, seed: int) -> torch.Tensor:
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed * 1000003 + rank)
+    return torch.randint(0, 256, (m, n_bytes), dtype=torch.uint8, device="cuda", generator=g)
+
+
+def cpu_baseline(keys, n_bytes, lam, cwb_h: bytes, s0: bytes, xs_sample: np.ndarray, ys_gpu: np.ndarray,
+                 target_s: float):
+    """Time the C++-free C restatement of the reference eval (oracle, AES-NI,
+    one pthread per core over contiguous point chunks like rayon) on this host.
+    Bounded: calibrate on a small slice, then run ~target_s of CPU work."""
+    from oracle import oracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    P = O.OraclePrg(keys, lam)
+    k = O.OracleKey(n_bytes, lam)
+    n = 8 * n_bytes
+    k.cw_s[:] = np.frombuffer(cwb_h[:n * lam], np.uint8).reshape(n, lam)
+    k.cw_v[:] = np.frombuffer(cwb_h[n * lam:2 * n * lam], np.uint8).reshape(n, lam)
+    k.cw_t[:] = np.frombuffer(cwb_h[2 * n * lam:2 * n * lam + n], np.uint8)
+    off = dcf_amd.cwb_np1_offset(n_bytes, lam, 1)
+    k.cw_np1[:] = np.frombuffer(cwb_h[off:off + lam], np.uint8)
+    cal = xs_sample[: min(len(xs_sample), 8192 * threads)]
+    t0 = time.perf_counter()
+    y = O.eval_(P, 0, k, s0, cal, nthreads=threads)
+    dt = time.perf_counter() - t0
+    matches = bool(np.array_equal(y, ys_gpu[: len(cal)]))
+    rate = len(cal) / dt
+    m = int(min(len(xs_sample), max(len(cal), rate * target_s)))
+    t0 = time.perf_counter()
+    y = O.eval_(P, 0, k, s0, xs_sample[:m], nthreads=threads)
+    dt = time.perf_counter() - t0
+    matches = matches and bool(np.array_equal(y, ys_gpu[:m]))
+    return {
+        "value": m / dt, "unit": "evals/s", "cores": threads, "kind": "port",
+        "sample": f"{m} of the GPU's points (first rows of rank 0's slice), party 0, same key; "
+                  f"C restatement of lib.rs:163-204 + prg.rs:42-73 with AES-NI, {threads} threads; "
+                  f"{dt:.1f} s",
+        "aesni": P.uses_aesni, "matches_gpu": matches,
+    }
+
+
+def run_eval(args, world, rank):
+    nb, lam = args.n_bytes, 16
+    m = args.points
+    rng = np.random.default_rng(0xDCF0001)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
+    d = dcf_amd.DcfImpl(nb, lam, prg)
+    cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002)
+    s0 = seeds[0].contiguous()
+    xs = gen_points(m, nb, rank, 0xDCF0003)
+    ys = torch.empty((m, lam), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        d.eval_device(False, cwb, s0, xs, ys)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        d.eval_device(False, cwb, s0, xs, ys)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # one k_eval16 launch per step
+    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    total_evals = m * world * args.steps
+    value = total_evals / wall
+    bpe = blocks_per_eval(nb, lam)
+    per_gpu_blocks = m * bpe / kern_s
+    out = {
+        "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"{args.workload.upper()}: N={nb} ({8 * nb}-bit x), lambda={lam}, Aes256HirosePrg, 1 key, "
+                               f"{m} points/GPU in HBM, party 0, eval only",
+                   "n_bytes": nb, "lambda": lam, "points_per_gpu": m, "global_points": m * world,
+                   "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
+        "aes_blocks_per_s": value * bpe,
+        "roofline": {
+            "bound": "lds", "kernel": "k_eval16<0>",
+            "achieved": per_gpu_blocks / 1e9, "peak": PEAK_AES_BLOCKS / 1e9, "unit": "G AES-256 blocks/s",
+            "frac": per_gpu_blocks / PEAK_AES_BLOCKS, "traffic": None,
+            "kernel_ms": kern_s * 1e3,
+            "note": "blocks = reference count (2 per level, 128 levels); peak = 256 CU x 32 ds_read_b32 "
+                    "lookups/clk x 2.4 GHz / 224 lookups per T-table AES-256 block; per GPU",
+            "hbm_GBps": m * (nb + lam) / kern_s / 1e9,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        ns = min(m, 1 << 22)
+        xs_h = xs[:ns].cpu().numpy()
+        ys_h = ys[:ns].cpu().numpy()
+        cwb_h = cwb.cpu().numpy().tobytes()
+        out["cpu_baseline"] = cpu_baseline(keys, nb, lam, cwb_h, seeds[0].cpu().numpy().tobytes(), xs_h, ys_h,
+                                           args.cpu_seconds)
+    return out
+
+
+def run_c5(args, world, rank):
+    """C5: K independent keys x 64 points: batched gen + eval of both parties."""
+    nb, lam, P = args.n_bytes, 16, 64
+    K = args.keys
+    rng = np.random.default_rng(0xDCF0005)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
+    d = dcf_amd.DcfImpl(nb, lam, prg)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5 + rank)
+    rnd = lambda *s: torch.randint(0, 256, s, dtype=torch.uint8, device="cuda", generator=g)  # noqa: E731
+    alpha, beta, s0, s1 = rnd(K, nb), rnd(K, lam), rnd(K, lam), rnd(K, lam)
+    xs = rnd(K * P, nb)
+    cwb = torch.empty(dcf_amd.cwb_bytes(nb, lam, K), dtype=torch.uint8, device="cuda")
+    y0 = torch.empty((K * P, lam), dtype=torch.uint8, device="cuda")
+    y1 = torch.empty_like(y0)
+
+    def step():
+        d.gen_batch_device(alpha, beta, s0, s1, dcf_amd.BoundState.LtBeta, cwb)
+        d.eval_multikey_device(False, cwb, s0, xs, P, y0)
+        d.eval_multikey_device(True, cwb, s1, xs, P, y1)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    evals = 2 * K * P * world * args.steps
+    return {"metric": "C5 batched gen + eval (both parties)", "value": evals / wall, "unit": "evals/s",
+            "keys_per_s": K * world * args.steps / wall, "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"C5: {K} keys x {P} points per GPU, N={nb}, lambda={lam}"}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c5"])
+    ap.add_argument("--points", type=int, default=None)
+    ap.add_argument("--keys", type=int, default=1 << 20)
+    ap.add_argument("--n-bytes", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    if args.workload == "c2":
+        args.n_bytes = args.n_bytes or 4
+        args.points = args.points or (1 << 24)
+    else:
+        args.n_bytes = args.n_bytes or 16
+        args.points = args.points or (1 << 28)
+    world, rank, _ = dist_setup(args.gpus)
+    out = run_c5(args, world, rank) if args.workload == "c5" else run_eval(args, world, rank)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,262 @@
+"""Host-side mirror of the `dcf` crate's operator and plugin interface.
+
+Same names, argument meaning and error behaviour as the Rust crate
+(xymeng16/dcf v0.2.2), with the compute on MI355X through the C ABI:
+
+  Rust (reference)                                   here
+  -------------------------------------------------  ------------------------------
+  trait Dcf<N, LAMBDA> { gen, eval }  lib.rs:24-35   DcfImpl.gen / DcfImpl.eval
+  struct CmpFn { alpha, beta }        lib.rs:41-46   CmpFn
+  trait Prg / Aes256HirosePrg::new    lib.rs:52, prg.rs:27  Aes256HirosePrg(keys, lam)
+  DcfImpl::new(prg)                   lib.rs:74      DcfImpl(n_bytes, lam, prg)
+  struct Cw { s, v, tl, tr }          lib.rs:209     Cw
+  struct Share { s0s, cws, cw_np1 }   lib.rs:275     Share
+  enum BoundState { LtBeta, GtBeta }  lib.rs:342     BoundState
+
+Const generics `N` / `LAMBDA` become constructor arguments.  Panics of the
+reference (`assert_eq!(k.cws.len(), N * 8)`, lib.rs:165; the cipher index at
+prg.rs:51) surface as `DcfError`/`ValueError`; the silent zip truncation of
+lib.rs:196 becomes an error.
+
+Batch entry points (`eval_device`, `eval_multikey_device`, `gen_batch_device`)
+take torch uint8 tensors resident on the prg's device and run on the current
+stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from dataclasses import dataclass, field
+from typing import List, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import DcfError, check
+
+
+class BoundState(enum.IntEnum):
+    """lib.rs:342-349."""
+    LtBeta = 0  # f(x) = beta iff x < alpha
+    GtBeta = 1  # f(x) = beta iff x > alpha
+
+
+@dataclass
+class CmpFn:
+    """lib.rs:41-46: alpha (N bytes), beta (LAMBDA bytes)."""
+    alpha: bytes
+    beta: bytes
+
+
+@dataclass
+class Cw:
+    """lib.rs:209-214."""
+    s: bytes
+    v: bytes
+    tl: bool
+    tr: bool
+
+
+@dataclass
+class Share:
+    """lib.rs:275-283.  gen returns both seeds; eval reads s0s[0] (lib.rs:168)."""
+    s0s: List[bytes]
+    cws: List[Cw] = field(default_factory=list)
+    cw_np1: bytes = b""
+
+
+def cwb_bytes(n_bytes: int, lam: int, num_keys: int = 1) -> int:
+    return int(_lib.load().dcf_cwb_bytes(n_bytes, lam, num_keys))
+
+
+def cwb_np1_offset(n_bytes: int, lam: int, num_keys: int = 1) -> int:
+    return int(_lib.load().dcf_cwb_np1_offset(n_bytes, lam, num_keys))
+
+
+def share_to_cwb(k: Share, n_bytes: int, lam: int) -> bytes:
+    """Pack `Share.cws` / `cw_np1` into the single-key CWB layout (include/dcf_hip.h)."""
+    n = 8 * n_bytes
+    if len(k.cws) != n:  # lib.rs:165
+        raise DcfError(-8, f"k.cws.len() = {len(k.cws)} != N * 8 = {n}")
+    buf = bytearray(cwb_bytes(n_bytes, lam, 1))
+    for i, cw in enumerate(k.cws):
+        if len(cw.s) != lam or len(cw.v) != lam:
+            raise DcfError(-8, "correction word of the wrong length")
+        buf[i * lam:(i + 1) * lam] = cw.s
+        buf[n * lam + i * lam:n * lam + (i + 1) * lam] = cw.v
+        buf[2 * n * lam + i] = int(bool(cw.tl)) | (int(bool(cw.tr)) << 1)
+    off = cwb_np1_offset(n_bytes, lam, 1)
+    buf[off:off + lam] = k.cw_np1
+    return bytes(buf)
+
+
+def cwb_to_share(cwb: bytes, n_bytes: int, lam: int, s0s: Sequence[bytes]) -> Share:
+    n = 8 * n_bytes
+    cws = []
+    for i in range(n):
+        t = cwb[2 * n * lam + i]
+        cws.append(Cw(bytes(cwb[i * lam:(i + 1) * lam]), bytes(cwb[n * lam + i * lam:n * lam + (i + 1) * lam]),
+                      bool(t & 1), bool(t & 2)))
+    off = cwb_np1_offset(n_bytes, lam, 1)
+    return Share([bytes(s) for s in s0s], cws, bytes(cwb[off:off + lam]))
+
+
+def _ptr(b) -> ctypes.c_void_p:
+    if isinstance(b, np.ndarray):
+        assert b.flags["C_CONTIGUOUS"]
+        return ctypes.c_void_p(b.ctypes.data)
+    return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p)
+
+
+def _tptr(t) -> ctypes.c_void_p:
+    """Device pointer of a contiguous torch uint8 tensor."""
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device_index: int):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device_index).cuda_stream)
+
+
+class Aes256HirosePrg:
+    """`Aes256HirosePrg::<LAMBDA, CIPHER_N>::new(keys)` (prg.rs:27-33), resident on one GPU.
+
+    keys: CIPHER_N 32-byte AES-256 keys.  LAMBDA = 16 reads cipher 0 only;
+    LAMBDA >= 32 reads ciphers 0 and 17 (the diagonal zip, prg.rs:48-51), so it
+    needs CIPHER_N >= 18 (the reference panics otherwise).
+    """
+
+    def __init__(self, keys: Sequence[bytes], lam: int = 16, device: int = 0):
+        keys = [bytes(k) for k in keys]
+        if any(len(k) != 32 for k in keys):
+            raise ValueError("AES-256 keys are 32 bytes")
+        L = _lib.load()
+        blob = b"".join(keys)
+        h = ctypes.c_void_p()
+        check(L.dcf_hirose_prg_new(_ptr(blob), len(keys), lam, device, ctypes.byref(h)))
+        self._h = h
+        self.lam = lam
+        self.cipher_n = len(keys)
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib._lib is not None:
+            _lib._lib.dcf_prg_free(h)
+            self._h = None
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def gen(self, seed: bytes):
+        """`Prg::gen` (lib.rs:52-54) for one seed — the GPU PRG kernel, not a CPU path."""
+        return self.gen_many([seed])[0]
+
+    def gen_many(self, seeds: Sequence[bytes]):
+        lam = self.lam
+        m = len(seeds)
+        blob = b"".join(bytes(s) for s in seeds)
+        if len(blob) != m * lam:
+            raise ValueError("seed of the wrong length")
+        out = np.zeros((m, 4 * lam + 2), np.uint8)
+        check(_lib.load().dcf_prg_gen(self._h, _ptr(blob), m, _ptr(out)))
+        res = []
+        for r in out:
+            b = r.tobytes()
+            res.append([(b[0:lam], b[lam:2 * lam], bool(b[4 * lam])),
+                        (b[2 * lam:3 * lam], b[3 * lam:4 * lam], bool(b[4 * lam + 1]))])
+        return res
+
+
+class DcfImpl:
+    """`DcfImpl<N, LAMBDA, Aes256HirosePrg>` (lib.rs:63-205) on MI355X."""
+
+    def __init__(self, n_bytes: int, lam: int, prg: Aes256HirosePrg):
+        if prg.lam != lam:
+            raise ValueError("prg LAMBDA mismatch")
+        if n_bytes <= 0:
+            raise ValueError("N must be positive")
+        self.n_bytes = n_bytes
+        self.lam = lam
+        self.prg = prg
+
+    # ---- Dcf trait (lib.rs:24-35), host buffers ----
+    def gen(self, f: CmpFn, s0s: Sequence[bytes], bound: BoundState) -> Share:
+        """`Dcf::gen` (lib.rs:86-161)."""
+        lam, nb = self.lam, self.n_bytes
+        if len(f.alpha) != nb or len(f.beta) != lam or len(s0s) != 2 or any(len(s) != lam for s in s0s):
+            raise ValueError("argument lengths do not match N / LAMBDA")
+        out = np.zeros(cwb_bytes(nb, lam, 1), np.uint8)
+        check(_lib.load().dcf_gen(self.prg.handle, nb, _ptr(bytes(f.alpha)), _ptr(bytes(f.beta)),
+                                  _ptr(bytes(s0s[0])), _ptr(bytes(s0s[1])), int(bound), _ptr(out)))
+        return cwb_to_share(out.tobytes(), nb, lam, [bytes(s0s[0]), bytes(s0s[1])])
+
+    def eval(self, b: bool, k: Share, xs, ys=None):
+        """`Dcf::eval` (lib.rs:163-204).  xs: sequence of N-byte strings or an (m, N)
+        uint8 array; ys (optional, (m, LAMBDA) uint8 array) is overwritten in place.
+        Returns ys."""
+        lam, nb = self.lam, self.n_bytes
+        cwb = share_to_cwb(k, nb, lam)
+        xa = self._as_points(xs)
+        m = xa.shape[0]
+        if ys is None:
+            ys = np.zeros((m, lam), np.uint8)
+        if not (isinstance(ys, np.ndarray) and ys.dtype == np.uint8 and ys.flags["C_CONTIGUOUS"]):
+            raise TypeError("ys must be a contiguous uint8 numpy array")
+        if ys.size != m * lam:
+            raise DcfError(-5, f"xs.len() = {m} does not match ys")
+        check(_lib.load().dcf_eval(self.prg.handle, nb, int(bool(b)), _ptr(cwb), len(cwb), _ptr(bytes(k.s0s[0])),
+                                   _ptr(xa), m, _ptr(ys), ys.size))
+        return ys
+
+    def _as_points(self, xs) -> np.ndarray:
+        nb = self.n_bytes
+        if isinstance(xs, np.ndarray):
+            xa = np.ascontiguousarray(xs, dtype=np.uint8).reshape(-1, nb) if xs.size else np.zeros((0, nb), np.uint8)
+        else:
+            blob = b"".join(bytes(x) for x in xs)
+            if len(blob) != len(xs) * nb:
+                raise ValueError("point of the wrong length")
+            xa = np.frombuffer(blob, np.uint8).reshape(-1, nb).copy() if xs else np.zeros((0, nb), np.uint8)
+        return xa
+
+    # ---- batch / device entry points (torch uint8 tensors on self.prg.device) ----
+    def gen_batch_device(self, alpha, beta, s0_0, s0_1, bound: BoundState, cwb_out=None):
+        """K independent `Dcf::gen` calls in one launch.  alpha: (K, N), beta/s0_0/s0_1: (K, LAMBDA).
+        Returns the K-key CWB tensor (include/dcf_hip.h layout)."""
+        import torch
+        K = alpha.shape[0]
+        if cwb_out is None:
+            cwb_out = torch.empty(cwb_bytes(self.n_bytes, self.lam, K), dtype=torch.uint8, device=alpha.device)
+        check(_lib.load().dcf_gen_batch_device(self.prg.handle, self.n_bytes, K, _tptr(alpha), _tptr(beta),
+                                               _tptr(s0_0), _tptr(s0_1), int(bound), _tptr(cwb_out),
+                                               _stream(self.prg.device)))
+        return cwb_out
+
+    def eval_device(self, b: bool, cwb, s0, xs, ys=None):
+        """One key over m points: xs (m, N) -> ys (m, LAMBDA), device tensors."""
+        import torch
+        m = xs.shape[0]
+        if ys is None:
+            ys = torch.empty((m, self.lam), dtype=torch.uint8, device=xs.device)
+        if ys.numel() != m * self.lam:
+            raise DcfError(-5, "xs / ys length mismatch")
+        check(_lib.load().dcf_eval_device(self.prg.handle, self.n_bytes, int(bool(b)), _tptr(cwb), _tptr(s0),
+                                          _tptr(xs), m, _tptr(ys), _stream(self.prg.device)))
+        return ys
+
+    def eval_multikey_device(self, b: bool, cwb, s0s, xs, points_per_key: int, ys=None):
+        """K keys x P points: xs (K*P, N), s0s (K, LAMBDA) -> ys (K*P, LAMBDA)."""
+        import torch
+        K = s0s.shape[0]
+        if xs.shape[0] != K * points_per_key:
+            raise DcfError(-5, "xs rows != num_keys * points_per_key")
+        if ys is None:
+            ys = torch.empty((xs.shape[0], self.lam), dtype=torch.uint8, device=xs.device)
+        check(_lib.load().dcf_eval_multikey_device(self.prg.handle, self.n_bytes, K, points_per_key, int(bool(b)),
+                                                   _tptr(cwb), _tptr(s0s), _tptr(xs), _tptr(ys),
+                                                   _stream(self.prg.device)))
+        return ys

@@ -1,0 +1,128 @@
+/*
+ * dcf_hip.h — C ABI of the MI355X (gfx950) DCF evaluator.
+ *
+ * Drop-in boundary for the hot path of the `dcf` crate (xymeng16/dcf v0.2.2):
+ * the `Dcf<N, LAMBDA>` operator (lib.rs:24-35) implemented by `DcfImpl`
+ * (lib.rs:63-205) over the `Aes256HirosePrg` plugin (prg.rs:22-74).  Every
+ * entry point is plain C: pointers, sizes, int status codes.  A Rust crate binds
+ * it with `extern "C"` declarations (INTEGRATION.md shows the stub).
+ *
+ * Conventions
+ *   n_bytes   `N` of `Dcf<N, LAMBDA>` / `CmpFn<N, LAMBDA>` (lib.rs:39): domain
+ *             size in bytes; the tree has n = 8 * n_bytes levels (lib.rs:93).
+ *   lambda    `LAMBDA` (lib.rs:40): seed and output size in bytes; must be a
+ *             multiple of 16 (prg.rs:17-18).
+ *   party     `b` of `Dcf::eval` (lib.rs:34): 0 = false, 1 = true.
+ *   bound     `BoundState` (lib.rs:342-349): 0 = LtBeta, 1 = GtBeta.
+ *   seeds     `Share::s0s` (lib.rs:278).  gen takes both; eval takes the one the
+ *             reference reads, `k.s0s[0]` (lib.rs:168), as `s0`.
+ *
+ * Key layout ("correction-word block", CWB) for K keys, n = 8 * n_bytes
+ * (replaces `Share { cws: Vec<Cw>, cw_np1 }`, lib.rs:208-214 and 275-283),
+ * structure-of-arrays so a wave reads one level of 64 keys coalesced:
+ *   offset 0                 cw_s  [n][K][lambda]   Cw::s
+ *   offset n*K*lambda        cw_v  [n][K][lambda]   Cw::v
+ *   offset 2*n*K*lambda      cw_t  [n][K]  u8       bit0 = Cw::tl, bit1 = Cw::tr
+ *   offset dcf_cwb_np1_offset cw_np1[K][lambda]     Share::cw_np1
+ * (the cw_np1 offset is 2*n*K*lambda + n*K rounded up to 16).  K = 1 is the
+ * single-key layout.  Size: dcf_cwb_bytes().
+ *
+ * Errors: the reference panics where this ABI returns a code —
+ *   DCF_ERR_KEY      assert_eq!(k.cws.len(), N * 8)           lib.rs:165
+ *   DCF_ERR_CIPHER_N self.ciphers[i * 16 + j] out of range     prg.rs:51
+ *   DCF_ERR_LEN      xs.len() != ys.len() (the reference silently truncates
+ *                    via zip, lib.rs:196-198)
+ * Nothing aborts the process.
+ *
+ * Memory: `*_device` entry points take device pointers and a hipStream_t (as
+ * void*, NULL = the legacy default stream) and are asynchronous; the library
+ * keeps no reference to caller buffers once the stream has passed the call.
+ * Host entry points take host pointers and are synchronous.
+ *
+ * Threading: one dcf_prg may be used by one host thread at a time; distinct
+ * dcf_prg objects are independent.  Multi-GPU = one process (or one dcf_prg)
+ * per device; the path shards by points/keys with no collective.
+ */
+#ifndef DCF_HIP_H
+#define DCF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCF_OK 0
+#define DCF_ERR_ARG -1        /* null pointer, bad enum */
+#define DCF_ERR_LAMBDA -2     /* lambda == 0 or lambda % 16 != 0 (prg.rs:17-18) */
+#define DCF_ERR_CIPHER_N -3   /* too few ciphers for lambda (reference panics, prg.rs:51) */
+#define DCF_ERR_N -4          /* n_bytes == 0 */
+#define DCF_ERR_LEN -5        /* length mismatch (reference truncates, lib.rs:196) */
+#define DCF_ERR_HIP -6        /* HIP runtime error; see dcf_last_error() */
+#define DCF_ERR_UNSUPPORTED -7 /* shape not implemented by any kernel */
+#define DCF_ERR_KEY -8        /* malformed key (lib.rs:165) */
+
+#define DCF_BOUND_LT_BETA 0
+#define DCF_BOUND_GT_BETA 1
+
+/* Opaque: an Aes256HirosePrg (prg.rs:22-24) whose AES-256 schedules live on one
+ * device, i.e. `DcfImpl::new(Aes256HirosePrg::new(keys))` (lib.rs:74, prg.rs:27). */
+typedef struct dcf_prg dcf_prg;
+
+/* Version string of this library. */
+const char* dcf_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* dcf_last_error(void);
+
+/* Aes256HirosePrg::<LAMBDA, CIPHER_N>::new(keys) (prg.rs:27-33) on `device`.
+ * keys: cipher_n * 32 bytes.  Needs cipher_n >= 1 for lambda == 16 and
+ * cipher_n >= 18 for lambda >= 32 (the diagonal zip reads ciphers 0 and 17,
+ * prg.rs:48-51). */
+int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int device, dcf_prg** out);
+void dcf_prg_free(dcf_prg* prg);
+size_t dcf_prg_lambda(const dcf_prg* prg);
+
+/* CWB layout helpers (see above). */
+size_t dcf_cwb_bytes(size_t n_bytes, size_t lambda, size_t num_keys);
+size_t dcf_cwb_np1_offset(size_t n_bytes, size_t lambda, size_t num_keys);
+
+/* ---- host-pointer, synchronous (mirror Dcf::gen / Dcf::eval) ---- */
+
+/* Dcf::gen (lib.rs:26-31, impl lib.rs:86-161) for one key.
+ * alpha: n_bytes, beta / s0_0 / s0_1: lambda, cwb_out: dcf_cwb_bytes(n_bytes, lambda, 1). */
+int dcf_gen(dcf_prg* prg, size_t n_bytes, const uint8_t* alpha, const uint8_t* beta, const uint8_t* s0_0,
+            const uint8_t* s0_1, int bound, uint8_t* cwb_out);
+
+/* Dcf::eval (lib.rs:34, impl lib.rs:163-204).  xs: m * n_bytes (x_i contiguous),
+ * ys: m * lambda (overwritten, lib.rs:171).  cwb: one key, s0: k.s0s[0]. */
+int dcf_eval(dcf_prg* prg, size_t n_bytes, int party, const uint8_t* cwb, size_t cwb_len, const uint8_t* s0,
+             const uint8_t* xs, size_t m, uint8_t* ys, size_t ys_len);
+
+/* Aes256HirosePrg::gen (prg.rs:42-73) for m seeds (test hook for PRG vectors).
+ * seeds: m * lambda; out: m * (4 * lambda + 2) = s_l | v_l | s_r | v_r | t_l | t_r. */
+int dcf_prg_gen(dcf_prg* prg, const uint8_t* seeds, size_t m, uint8_t* out);
+
+/* ---- device-pointer, asynchronous on `stream` ---- */
+
+/* Batched Dcf::gen: K independent keys, one GPU lane per key.
+ * alpha: K * n_bytes, beta / s0_0 / s0_1: K * lambda (row k = key k),
+ * cwb_out: dcf_cwb_bytes(n_bytes, lambda, K). */
+int dcf_gen_batch_device(dcf_prg* prg, size_t n_bytes, size_t num_keys, const uint8_t* alpha, const uint8_t* beta,
+                         const uint8_t* s0_0, const uint8_t* s0_1, int bound, uint8_t* cwb_out, void* stream);
+
+/* Dcf::eval of one key over m points (x_i contiguous, n_bytes each). */
+int dcf_eval_device(dcf_prg* prg, size_t n_bytes, int party, const uint8_t* cwb, const uint8_t* s0,
+                    const uint8_t* xs, size_t m, uint8_t* ys, void* stream);
+
+/* Dcf::eval for K keys x P points each: point j of key k is xs[k*P + j],
+ * its output ys[k*P + j]; s0s: K * lambda (k.s0s[0] of each key). */
+int dcf_eval_multikey_device(dcf_prg* prg, size_t n_bytes, size_t num_keys, size_t points_per_key, int party,
+                             const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DCF_HIP_H */

@@ -1,0 +1,422 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the xymeng16/dcf reference (Rust crate `dcf` v0.2.2) for
+ * the hot path: `Aes256HirosePrg::gen`, `DcfImpl::gen`, `DcfImpl::eval`.
+ * It exists to check the HIP product path (dcf_amd/csrc) bit for bit and to be
+ * timed as the host-CPU baseline (`cpu_baseline.kind = "port"` in bench.py).
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it; the product library never links or calls it.
+ *
+ * Parity anchors (the Rust crate cannot be built here: no cargo/rustc, nightly
+ * features, un-vendored deps — see DESIGN.md "Oracle"):
+ *   - AES-256 arithmetic: third-party crate `aes` ^0.8.3 (Cargo.toml:36, version
+ *     unpinned, not vendored).  Restated from FIPS-197; pinned by the FIPS-197
+ *     C.3 known-answer vector and cross-checked against OpenSSL libcrypto and an
+ *     independent Python restatement (oracle/pyref.py) in tests/.
+ *   - PRG / gen / eval: restated line by line, citations inline.
+ *   - Reference tests: reconstruction KATs lib.rs:372-420, non-zero tests
+ *     lib.rs:422-442 and prg.rs:86-96 (re-run by tests/test_oracle.py).
+ *
+ * Byte conventions follow the crate:
+ *   - x / alpha bits are read Msb0 (lib.rs:106,181): level i uses byte i/8,
+ *     bit 7 - i%8.
+ *   - t bits and the cleared bit are Lsb0 (prg.rs:63-68).
+ *
+ * Key layout used by the oracle and by the C ABI (include/dcf_hip.h), for one
+ * key with n = 8*N levels:
+ *   cw_s[n][lambda], cw_v[n][lambda], cw_t[n] (bit0 = tl, bit1 = tr),
+ *   cw_np1[lambda]; the party seed s0s[0] is passed separately.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+#define ORC_OK 0
+#define ORC_ERR_ARG -1
+#define ORC_ERR_LAMBDA -2
+#define ORC_ERR_CIPHER_N -3
+#define ORC_ERR_N -4
+
+/* ------------------------------------------------------------------ */
+/* AES-256 (FIPS-197), byte oriented.  S-box derived from GF(2^8)      */
+/* inversion + affine map, not from a copied table.                    */
+/* ------------------------------------------------------------------ */
+static uint8_t SBOX[256];
+static int sbox_ready = 0;
+static pthread_once_t sbox_once = PTHREAD_ONCE_INIT;
+
+static uint8_t gf_mul(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  while (b) {
+    if (b & 1) r ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+    b >>= 1;
+  }
+  return r;
+}
+
+static uint8_t rotl8(uint8_t x, int k) { return (uint8_t)((x << k) | (x >> (8 - k))); }
+
+static void sbox_build(void) {
+  for (int x = 0; x < 256; x++) {
+    uint8_t inv = 0;
+    if (x) { /* x^254 = x^-1 */
+      uint8_t p = (uint8_t)x, acc = 1;
+      int e = 254;
+      while (e) {
+        if (e & 1) acc = gf_mul(acc, p);
+        p = gf_mul(p, p);
+        e >>= 1;
+      }
+      inv = acc;
+    }
+    SBOX[x] = (uint8_t)(inv ^ rotl8(inv, 1) ^ rotl8(inv, 2) ^ rotl8(inv, 3) ^ rotl8(inv, 4) ^ 0x63);
+  }
+  sbox_ready = 1;
+}
+
+static void ensure_sbox(void) { pthread_once(&sbox_once, sbox_build); }
+
+/* AES-256 key expansion: 60 words = 15 round keys, stored as 240 bytes. */
+void orc_aes256_expand(const uint8_t key[32], uint8_t rk[240]) {
+  ensure_sbox();
+  memcpy(rk, key, 32);
+  uint8_t rcon = 1;
+  for (int i = 8; i < 60; i++) {
+    uint8_t t[4];
+    memcpy(t, rk + 4 * (i - 1), 4);
+    if (i % 8 == 0) {
+      uint8_t t0 = t[0];
+      t[0] = (uint8_t)(SBOX[t[1]] ^ rcon);
+      t[1] = SBOX[t[2]];
+      t[2] = SBOX[t[3]];
+      t[3] = SBOX[t0];
+      rcon = gf_mul(rcon, 2);
+    } else if (i % 8 == 4) {
+      for (int k = 0; k < 4; k++) t[k] = SBOX[t[k]];
+    }
+    for (int k = 0; k < 4; k++) rk[4 * i + k] = (uint8_t)(rk[4 * (i - 8) + k] ^ t[k]);
+  }
+}
+
+static void aes_mix_column(uint8_t* c) {
+  uint8_t a0 = c[0], a1 = c[1], a2 = c[2], a3 = c[3];
+  c[0] = (uint8_t)(gf_mul(a0, 2) ^ gf_mul(a1, 3) ^ a2 ^ a3);
+  c[1] = (uint8_t)(a0 ^ gf_mul(a1, 2) ^ gf_mul(a2, 3) ^ a3);
+  c[2] = (uint8_t)(a0 ^ a1 ^ gf_mul(a2, 2) ^ gf_mul(a3, 3));
+  c[3] = (uint8_t)(gf_mul(a0, 3) ^ a1 ^ a2 ^ gf_mul(a3, 2));
+}
+
+/* Portable AES-256 block encryption (FIPS-197 §5.1). */
+void orc_aes256_encrypt_portable(const uint8_t rk[240], const uint8_t in[16], uint8_t out[16]) {
+  uint8_t s[16], t[16];
+  for (int i = 0; i < 16; i++) s[i] = (uint8_t)(in[i] ^ rk[i]);
+  for (int round = 1; round <= 14; round++) {
+    for (int i = 0; i < 16; i++) s[i] = SBOX[s[i]];
+    /* ShiftRows: state byte (r, c) lives at index r + 4c. */
+    for (int c = 0; c < 4; c++)
+      for (int r = 0; r < 4; r++) t[r + 4 * c] = s[r + 4 * ((c + r) & 3)];
+    memcpy(s, t, 16);
+    if (round != 14)
+      for (int c = 0; c < 4; c++) aes_mix_column(s + 4 * c);
+    for (int i = 0; i < 16; i++) s[i] ^= rk[16 * round + i];
+  }
+  memcpy(out, s, 16);
+}
+
+#if defined(__x86_64__)
+__attribute__((target("aes,sse2"))) static void aes256_encrypt2_ni(const uint8_t rk[240], const uint8_t* in0,
+                                                                    const uint8_t* in1, uint8_t* out0,
+                                                                    uint8_t* out1) {
+  __m128i k = _mm_loadu_si128((const __m128i*)rk);
+  __m128i a = _mm_xor_si128(_mm_loadu_si128((const __m128i*)in0), k);
+  __m128i b = _mm_xor_si128(_mm_loadu_si128((const __m128i*)in1), k);
+  for (int r = 1; r < 14; r++) {
+    k = _mm_loadu_si128((const __m128i*)(rk + 16 * r));
+    a = _mm_aesenc_si128(a, k);
+    b = _mm_aesenc_si128(b, k);
+  }
+  k = _mm_loadu_si128((const __m128i*)(rk + 224));
+  a = _mm_aesenclast_si128(a, k);
+  b = _mm_aesenclast_si128(b, k);
+  _mm_storeu_si128((__m128i*)out0, a);
+  _mm_storeu_si128((__m128i*)out1, b);
+}
+static int cpu_has_aesni(void) {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("aes");
+}
+#else
+static int cpu_has_aesni(void) { return 0; }
+#endif
+
+/* ------------------------------------------------------------------ */
+/* Aes256HirosePrg (prg.rs:14-74)                                      */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  size_t lambda;
+  size_t cipher_n;
+  uint8_t* rk; /* cipher_n * 240 bytes: Aes256::new per key, prg.rs:27-33 */
+  int use_ni;
+} orc_prg;
+
+/* Aes256HirosePrg::new (prg.rs:27-33).  The reference panics on
+ * `self.ciphers[i * 16 + j]` (prg.rs:51) when cipher_n is too small; that
+ * condition is reported up front as ORC_ERR_CIPHER_N. */
+int orc_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int allow_ni, orc_prg** out) {
+  if (!keys || !out) return ORC_ERR_ARG;
+  if (lambda == 0 || lambda % 16 != 0) return ORC_ERR_LAMBDA;
+  /* Ciphers touched by the diagonal zip (prg.rs:48): index k*16+k for
+   * k < min(2, lambda/16). */
+  size_t need = (lambda / 16 >= 2) ? 18 : 1;
+  if (cipher_n < need) return ORC_ERR_CIPHER_N;
+  ensure_sbox();
+  orc_prg* p = (orc_prg*)calloc(1, sizeof(orc_prg));
+  if (!p) return ORC_ERR_ARG;
+  p->lambda = lambda;
+  p->cipher_n = cipher_n;
+  p->rk = (uint8_t*)malloc(cipher_n * 240);
+  if (!p->rk) {
+    free(p);
+    return ORC_ERR_ARG;
+  }
+  for (size_t i = 0; i < cipher_n; i++) orc_aes256_expand(keys + 32 * i, p->rk + 240 * i);
+  p->use_ni = allow_ni && cpu_has_aesni();
+  *out = p;
+  return ORC_OK;
+}
+
+void orc_prg_free(orc_prg* p) {
+  if (!p) return;
+  free(p->rk);
+  free(p);
+}
+
+int orc_prg_uses_aesni(const orc_prg* p) { return p ? p->use_ni : 0; }
+
+static void enc2(const orc_prg* p, size_t ci, const uint8_t* in0, const uint8_t* in1, uint8_t* out0,
+                 uint8_t* out1) {
+  const uint8_t* rk = p->rk + 240 * ci;
+#if defined(__x86_64__)
+  if (p->use_ni) {
+    aes256_encrypt2_ni(rk, in0, in1, out0, out1);
+    return;
+  }
+#endif
+  orc_aes256_encrypt_portable(rk, in0, out0);
+  orc_aes256_encrypt_portable(rk, in1, out1);
+}
+
+/* Aes256HirosePrg::gen (prg.rs:42-73).
+ * scratch: 5*lambda bytes.  out: sl, vl, sr, vr (lambda bytes each), tl, tr. */
+static void prg_gen(const orc_prg* p, const uint8_t* seed, uint8_t* scratch, uint8_t* sl, uint8_t* vl, int* tl,
+                    uint8_t* sr, uint8_t* vr, int* tr) {
+  const size_t lam = p->lambda;
+  uint8_t* seed_p = scratch; /* prg.rs:44: seed ^ c(), c() = 0xff.. (prg.rs:36-38) */
+  for (size_t i = 0; i < lam; i++) seed_p[i] = (uint8_t)(seed[i] ^ 0xff);
+  /* prg.rs:45-46: result_buf0 = [[0; L]; 2], result_buf1 = [[0; L]; 2]
+   * buf0[0] = sl, buf0[1] = sr, buf1[0] = vl, buf1[1] = vr */
+  uint8_t* buf0[2] = {sl, sr};
+  uint8_t* buf1[2] = {vl, vr};
+  memset(sl, 0, lam);
+  memset(sr, 0, lam);
+  memset(vl, 0, lam);
+  memset(vr, 0, lam);
+  /* prg.rs:48: (0..2).zip(0..LAMBDA/16) walks the diagonal (i, i) only. */
+  for (size_t i = 0, j = 0; i < 2 && j < lam / 16; i++, j++) {
+    size_t ci = i * 16 + j; /* prg.rs:51 */
+    enc2(p, ci, seed + 16 * j, seed_p + 16 * j, buf0[i] + 16 * j, buf1[i] + 16 * j); /* prg.rs:51-55 */
+  }
+  /* prg.rs:57-62 */
+  for (int b = 0; b < 2; b++)
+    for (size_t i = 0; i < lam; i++) {
+      buf0[b][i] ^= seed[i];
+      buf1[b][i] ^= seed_p[i];
+    }
+  /* prg.rs:63-64: Lsb0 bit 0 of byte 0, read before clearing */
+  *tl = buf0[0][0] & 1;
+  *tr = buf1[0][0] & 1;
+  /* prg.rs:65-68: clear Lsb0 bit 0 of the last byte of all four */
+  for (int b = 0; b < 2; b++) {
+    buf0[b][lam - 1] &= 0xfe;
+    buf1[b][lam - 1] &= 0xfe;
+  }
+}
+
+/* Exposed for PRG-level golden vectors. */
+int orc_prg_gen(const orc_prg* p, const uint8_t* seed, uint8_t* sl, uint8_t* vl, uint8_t* sr, uint8_t* vr,
+                uint8_t* t_out) {
+  if (!p || !seed) return ORC_ERR_ARG;
+  uint8_t* scratch = (uint8_t*)malloc(p->lambda);
+  if (!scratch) return ORC_ERR_ARG;
+  int tl, tr;
+  prg_gen(p, seed, scratch, sl, vl, &tl, sr, vr, &tr);
+  t_out[0] = (uint8_t)tl;
+  t_out[1] = (uint8_t)tr;
+  free(scratch);
+  return ORC_OK;
+}
+
+static inline int msb0_bit(const uint8_t* bytes, size_t i) { return (bytes[i >> 3] >> (7 - (i & 7))) & 1; }
+
+/* ------------------------------------------------------------------ */
+/* DcfImpl::gen (lib.rs:86-161)                                        */
+/* bound: 0 = LtBeta, 1 = GtBeta (lib.rs:342-349)                      */
+/* ------------------------------------------------------------------ */
+int orc_gen(const orc_prg* p, size_t n_bytes, const uint8_t* alpha, const uint8_t* beta, const uint8_t* s0_0,
+            const uint8_t* s0_1, int bound, uint8_t* cw_s, uint8_t* cw_v, uint8_t* cw_t, uint8_t* cw_np1) {
+  if (!p || !alpha || !beta || !s0_0 || !s0_1 || !cw_s || !cw_v || !cw_t || !cw_np1) return ORC_ERR_ARG;
+  if (n_bytes == 0) return ORC_ERR_N;
+  if (bound != 0 && bound != 1) return ORC_ERR_ARG;
+  const size_t lam = p->lambda, n = 8 * n_bytes; /* lib.rs:93 */
+  uint8_t* mem = (uint8_t*)calloc(16 * lam, 1);
+  if (!mem) return ORC_ERR_ARG;
+  uint8_t* v_alpha = mem;               /* lib.rs:94 */
+  uint8_t* ss[2] = {mem + lam, mem + 2 * lam}; /* lib.rs:95-97, current level only */
+  uint8_t* out0[4] = {mem + 3 * lam, mem + 4 * lam, mem + 5 * lam, mem + 6 * lam}; /* s0l v0l s0r v0r */
+  uint8_t* out1[4] = {mem + 7 * lam, mem + 8 * lam, mem + 9 * lam, mem + 10 * lam}; /* s1l v1l s1r v1r */
+  uint8_t* scratch = mem + 11 * lam;
+  memcpy(ss[0], s0_0, lam);
+  memcpy(ss[1], s0_1, lam);
+  int ts[2] = {0, 1}; /* lib.rs:100 */
+  for (size_t i = 1; i <= n; i++) {
+    int t0l, t0r, t1l, t1r;
+    prg_gen(p, ss[0], scratch, out0[0], out0[1], &t0l, out0[2], out0[3], &t0r); /* lib.rs:103 */
+    prg_gen(p, ss[1], scratch, out1[0], out1[1], &t1l, out1[2], out1[3], &t1r); /* lib.rs:104 */
+    int alpha_i = msb0_bit(alpha, i - 1);                                       /* lib.rs:106 */
+    int keep = alpha_i ? 1 : 0, lose = alpha_i ? 0 : 1;                         /* lib.rs:107-111 */
+    uint8_t* s_cw = cw_s + (i - 1) * lam;
+    uint8_t* v_cw = cw_v + (i - 1) * lam;
+    for (size_t k = 0; k < lam; k++) {
+      s_cw[k] = (uint8_t)(out0[2 * lose][k] ^ out1[2 * lose][k]);                    /* lib.rs:112 */
+      v_cw[k] = (uint8_t)(out0[2 * lose + 1][k] ^ out1[2 * lose + 1][k] ^ v_alpha[k]); /* lib.rs:113 */
+    }
+    /* lib.rs:114-125: LtBeta adds beta when lose == L, GtBeta when lose == R */
+    if ((bound == 0 && lose == 0) || (bound == 1 && lose == 1))
+      for (size_t k = 0; k < lam; k++) v_cw[k] ^= beta[k];
+    for (size_t k = 0; k < lam; k++) /* lib.rs:126-129 */
+      v_alpha[k] ^= (uint8_t)(out0[2 * keep + 1][k] ^ out1[2 * keep + 1][k] ^ v_cw[k]);
+    int tl_cw = t0l ^ t1l ^ alpha_i ^ 1; /* lib.rs:130 */
+    int tr_cw = t0r ^ t1r ^ alpha_i;     /* lib.rs:131 */
+    cw_t[i - 1] = (uint8_t)(tl_cw | (tr_cw << 1));
+    int t_keep = keep ? tr_cw : tl_cw;
+    int t0k = keep ? t0r : t0l, t1k = keep ? t1r : t1l;
+    for (size_t k = 0; k < lam; k++) { /* lib.rs:139-148 */
+      ss[0][k] = (uint8_t)(out0[2 * keep][k] ^ (ts[0] ? s_cw[k] : 0));
+      ss[1][k] = (uint8_t)(out1[2 * keep][k] ^ (ts[1] ? s_cw[k] : 0));
+    }
+    int nt0 = t0k ^ (ts[0] & t_keep); /* lib.rs:149-152 */
+    int nt1 = t1k ^ (ts[1] & t_keep);
+    ts[0] = nt0;
+    ts[1] = nt1;
+  }
+  for (size_t k = 0; k < lam; k++) cw_np1[k] = (uint8_t)(ss[0][k] ^ ss[1][k] ^ v_alpha[k]); /* lib.rs:155 */
+  free(mem);
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* DcfImpl::eval (lib.rs:163-204)                                      */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  const orc_prg* p;
+  size_t n_bytes;
+  int party;
+  const uint8_t *s0, *cw_s, *cw_v, *cw_t, *cw_np1, *xs;
+  uint8_t* ys;
+  size_t begin, end;
+  int rc;
+} eval_job;
+
+static void eval_points(eval_job* j) {
+  const size_t lam = j->p->lambda, n = 8 * j->n_bytes;
+  uint8_t* mem = (uint8_t*)malloc(6 * lam);
+  if (!mem) {
+    j->rc = ORC_ERR_ARG;
+    return;
+  }
+  uint8_t *s = mem, *sl = mem + lam, *vl = mem + 2 * lam, *sr = mem + 3 * lam, *vr = mem + 4 * lam,
+          *scratch = mem + 5 * lam;
+  for (size_t pt = j->begin; pt < j->end; pt++) {
+    const uint8_t* x = j->xs + pt * j->n_bytes;
+    uint8_t* v = j->ys + pt * lam;
+    memcpy(s, j->s0, lam); /* lib.rs:168: k.s0s[0] */
+    int t = j->party;      /* lib.rs:170 */
+    memset(v, 0, lam);     /* lib.rs:171 */
+    for (size_t i = 1; i <= n; i++) {
+      const uint8_t* cs = j->cw_s + (i - 1) * lam;
+      const uint8_t* cv = j->cw_v + (i - 1) * lam;
+      int ctl = j->cw_t[i - 1] & 1, ctr = (j->cw_t[i - 1] >> 1) & 1;
+      int tl, tr;
+      prg_gen(j->p, s, scratch, sl, vl, &tl, sr, vr, &tr); /* lib.rs:176 */
+      if (t)
+        for (size_t k = 0; k < lam; k++) { /* lib.rs:177-178 */
+          sl[k] ^= cs[k];
+          sr[k] ^= cs[k];
+        }
+      tl ^= t & ctl; /* lib.rs:179 */
+      tr ^= t & ctr; /* lib.rs:180 */
+      if (msb0_bit(x, i - 1)) { /* lib.rs:181-184 */
+        for (size_t k = 0; k < lam; k++) v[k] ^= (uint8_t)(vr[k] ^ (t ? cv[k] : 0));
+        memcpy(s, sr, lam);
+        t = tr;
+      } else { /* lib.rs:185-189 */
+        for (size_t k = 0; k < lam; k++) v[k] ^= (uint8_t)(vl[k] ^ (t ? cv[k] : 0));
+        memcpy(s, sl, lam);
+        t = tl;
+      }
+    }
+    for (size_t k = 0; k < lam; k++) v[k] ^= (uint8_t)(s[k] ^ (t ? j->cw_np1[k] : 0)); /* lib.rs:192 */
+  }
+  free(mem);
+  j->rc = ORC_OK;
+}
+
+static void* eval_thread(void* arg) {
+  eval_points((eval_job*)arg);
+  return NULL;
+}
+
+/* nthreads <= 1: serial (the crate's --no-default-features path, lib.rs:200-203);
+ * otherwise contiguous chunks over points, like rayon's split (lib.rs:196-198). */
+int orc_eval(const orc_prg* p, size_t n_bytes, int party, const uint8_t* s0, const uint8_t* cw_s, const uint8_t* cw_v,
+             const uint8_t* cw_t, const uint8_t* cw_np1, const uint8_t* xs, size_t m, uint8_t* ys, int nthreads) {
+  if (!p || !s0 || !cw_s || !cw_v || !cw_t || !cw_np1 || (m && (!xs || !ys))) return ORC_ERR_ARG;
+  if (n_bytes == 0) return ORC_ERR_N;
+  if (m == 0) return ORC_OK;
+  if (nthreads < 1) nthreads = 1;
+  if ((size_t)nthreads > m) nthreads = (int)m;
+  eval_job* jobs = (eval_job*)calloc((size_t)nthreads, sizeof(eval_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  if (!jobs || !th) {
+    free(jobs);
+    free(th);
+    return ORC_ERR_ARG;
+  }
+  size_t per = m / (size_t)nthreads, rem = m % (size_t)nthreads, at = 0;
+  for (int k = 0; k < nthreads; k++) {
+    size_t cnt = per + ((size_t)k < rem ? 1 : 0);
+    eval_job j = {p, n_bytes, party ? 1 : 0, s0, cw_s, cw_v, cw_t, cw_np1, xs, ys, at, at + cnt, 0};
+    jobs[k] = j;
+    at += cnt;
+  }
+  int rc = ORC_OK;
+  if (nthreads == 1) {
+    eval_points(&jobs[0]);
+    rc = jobs[0].rc;
+  } else {
+    for (int k = 0; k < nthreads; k++) pthread_create(&th[k], NULL, eval_thread, &jobs[k]);
+    for (int k = 0; k < nthreads; k++) {
+      pthread_join(th[k], NULL);
+      if (jobs[k].rc) rc = jobs[k].rc;
+    }
+  }
+  free(jobs);
+  free(th);
+  return rc;
+}

@@ -1,0 +1,34 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libdcf_hip.so on cuda:0)")
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, f"{name}.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return load_golden
+
+
+@pytest.fixture(scope="session")
+def hip_lib():
+    """The product library, built in-tree; compute tests must not run without it."""
+    from dcf_amd import build
+    build.build()
+    import dcf_amd
+    return dcf_amd.load()

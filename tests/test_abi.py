@@ -1,0 +1,93 @@
+"""C-ABI checks that need no GPU: the library builds for gfx950, loads, exports
+every function include/dcf_hip.h declares, and its pure-host helpers / argument
+validation behave.  No kernel is launched here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.conftest import ROOT
+from tests.golden.make_golden import REF_ALPHAS, REF_BETA, REF_KEYS
+
+HEADER = os.path.join(ROOT, "include", "dcf_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"^[A-Za-z_][\w \*]*?\b(dcf_\w+)\s*\(", src, flags=re.M))
+
+
+def test_header_declares_expected_api():
+    from dcf_amd import _lib
+    assert header_functions() == set(_lib.EXPORTS)
+
+
+def test_library_exports_every_header_symbol(hip_lib):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", hip_lib._name]).decode()
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = header_functions() - syms
+    assert not missing, missing
+    for name in header_functions():
+        assert getattr(hip_lib, name) is not None
+
+
+def test_library_is_gfx950_code_object(hip_lib):
+    out = subprocess.check_output(["/opt/rocm/lib/llvm/bin/clang-offload-bundler", "--list", "--type=o",
+                                   f"--input={hip_lib._name}"], stderr=subprocess.STDOUT).decode() \
+        if os.path.exists("/opt/rocm/lib/llvm/bin/clang-offload-bundler") else ""
+    if out:
+        assert "gfx950" in out
+
+
+def test_version_and_layout_helpers(hip_lib):
+    assert b"gfx950" in hip_lib.dcf_version()
+    for nb, lam, K in ((16, 16, 1), (4, 16, 7), (3, 32, 5), (2, 16384, 1)):
+        n = 8 * nb
+        off = hip_lib.dcf_cwb_np1_offset(nb, lam, K)
+        assert off == (2 * n * K * lam + n * K + 15) // 16 * 16
+        assert hip_lib.dcf_cwb_bytes(nb, lam, K) == off + K * lam
+    assert hip_lib.dcf_cwb_bytes(16, 16, 1) == 4240
+
+
+def test_argument_validation_without_gpu(hip_lib):
+    h = ctypes.c_void_p()
+    keys = b"\x00" * (32 * 18)
+    assert hip_lib.dcf_hirose_prg_new(keys, 18, 24, 0, ctypes.byref(h)) == -2   # lambda % 16
+    assert hip_lib.dcf_hirose_prg_new(keys, 17, 32, 0, ctypes.byref(h)) == -3   # prg.rs:51 panic
+    assert hip_lib.dcf_hirose_prg_new(keys, 0, 16, 0, ctypes.byref(h)) == -3
+    assert hip_lib.dcf_hirose_prg_new(None, 2, 16, 0, ctypes.byref(h)) == -1
+    assert b"cipher" in hip_lib.dcf_last_error() or hip_lib.dcf_last_error() != b""
+    assert hip_lib.dcf_eval(None, 16, 0, None, 0, None, None, 0, None, 0) == -1
+    assert hip_lib.dcf_gen_batch_device(None, 16, 1, None, None, None, None, 0, None, None) == -1
+
+
+def test_share_cwb_roundtrip_matches_oracle_layout(hip_lib):
+    import dcf_amd
+    P = O.OraclePrg(REF_KEYS, 16)
+    s0s = [b"\x11" * 16, b"\x22" * 16]
+    k = O.gen(P, REF_ALPHAS[2], REF_BETA, s0s[0], s0s[1], 0)
+    share = dcf_amd.Share(s0s, [dcf_amd.Cw(k.cw_s[i].tobytes(), k.cw_v[i].tobytes(), bool(k.cw_t[i] & 1),
+                                           bool(k.cw_t[i] & 2)) for i in range(128)], k.cw_np1.tobytes())
+    cwb = dcf_amd.share_to_cwb(share, 16, 16)
+    raw = k.cw_s.tobytes() + k.cw_v.tobytes() + k.cw_t.tobytes()
+    assert cwb == raw + bytes((-len(raw)) % 16) + k.cw_np1.tobytes()
+    back = dcf_amd.cwb_to_share(cwb, 16, 16, s0s)
+    assert back == share
+    bad = dcf_amd.Share(s0s, share.cws[:-1], share.cw_np1)
+    with pytest.raises(dcf_amd.DcfError):  # assert_eq!(k.cws.len(), N * 8), lib.rs:165
+        dcf_amd.share_to_cwb(bad, 16, 16)
+
+
+def test_product_has_no_oracle_dependency():
+    """The product package must not import or link the oracle."""
+    pkg = os.path.join(ROOT, "dcf_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".hpp", ".cpp")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in txt.replace("no CPU fallback", ""), f

@@ -1,0 +1,191 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors and
+the CPU oracle, bit for bit.  Runs on an MI355X only (`-m gpu`)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.golden.make_golden import REF_ALPHAS, REF_BETA, REF_KEYS, detbytes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dcf(hip_lib):
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    import dcf_amd
+    return dcf_amd
+
+
+def _rand(rng, shape):
+    return rng.integers(0, 256, size=shape, dtype=np.uint8)
+
+
+def test_prg16_golden(dcf, golden):
+    g = golden("prg16")
+    prg = dcf.Aes256HirosePrg([bytes.fromhex(k) for k in g["keys"]], 16)
+    outs = prg.gen_many([bytes.fromhex(r["seed"]) for r in g["rows"]])
+    for r, ((sl, vl, tl), (sr, vr, tr)) in zip(g["rows"], outs):
+        assert (sl.hex(), vl.hex(), tl, sr.hex(), vr.hex(), tr) == (r["sl"], r["vl"], r["tl"], r["sr"], r["vr"],
+                                                                      r["tr"])
+
+
+def _lam16_cases(golden):
+    return [c for c in golden("dcf_cases") if c["lambda"] == 16]
+
+
+def test_gen_golden(dcf, golden):
+    for c in _lam16_cases(golden):
+        prg = dcf.Aes256HirosePrg([bytes.fromhex(k) for k in c["keys"]], 16)
+        d = dcf.DcfImpl(c["n_bytes"], 16, prg)
+        s0s = [bytes.fromhex(s) for s in c["s0s"]]
+        k = d.gen(dcf.CmpFn(bytes.fromhex(c["alpha"]), bytes.fromhex(c["beta"])), s0s, dcf.BoundState(c["bound"]))
+        assert dcf.share_to_cwb(k, c["n_bytes"], 16).hex() == c["cwb"], c["name"]
+
+
+def test_eval_golden(dcf, golden):
+    for c in _lam16_cases(golden):
+        prg = dcf.Aes256HirosePrg([bytes.fromhex(k) for k in c["keys"]], 16)
+        nb = c["n_bytes"]
+        d = dcf.DcfImpl(nb, 16, prg)
+        s0s = [bytes.fromhex(s) for s in c["s0s"]]
+        full = dcf.cwb_to_share(bytes.fromhex(c["cwb"]), nb, 16, s0s)
+        xs = [bytes.fromhex(x) for x in c["xs"]]
+        for b, key in ((0, "y0"), (1, "y1")):
+            k = dcf.Share([s0s[b]], full.cws, full.cw_np1)  # lib.rs:382-385: s0s trimmed per party
+            ys = d.eval(bool(b), k, xs)
+            assert [y.tobytes().hex() for y in ys] == c[key], (c["name"], b)
+
+
+@pytest.mark.parametrize("bound", [0, 1])
+def test_reference_reconstruction_kat(dcf, bound):
+    """lib.rs:372-420 and 422-442 on the GPU, seeds fixed."""
+    prg = dcf.Aes256HirosePrg(REF_KEYS, 16)
+    d = dcf.DcfImpl(16, 16, prg)
+    expect = [1, 1, 0, 0, 0] if bound == 0 else [0, 0, 0, 1, 1]
+    for trial in range(3):
+        s0s = [detbytes(f"gkat/{trial}/0", 16), detbytes(f"gkat/{trial}/1", 16)]
+        k = d.gen(dcf.CmpFn(REF_ALPHAS[2], REF_BETA), s0s, dcf.BoundState(bound))
+        y0 = d.eval(False, dcf.Share([s0s[0]], k.cws, k.cw_np1), REF_ALPHAS)
+        y1 = d.eval(True, dcf.Share([s0s[1]], k.cws, k.cw_np1), REF_ALPHAS)
+        for i, e in enumerate(expect):
+            assert (y0[i] ^ y1[i]).tobytes() == (REF_BETA if e else bytes(16))
+        assert y0[2].tobytes() != bytes(16) and y1[2].tobytes() != bytes(16)
+
+
+@pytest.mark.parametrize("nb", [1, 2, 3, 4, 5, 7, 8, 12, 16, 17, 32])
+def test_eval_random_vs_oracle(dcf, nb):
+    rng = np.random.default_rng(100 + nb)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    d = dcf.DcfImpl(nb, 16, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
+    ok = O.gen(P, alpha, beta, s0, s1, int(nb % 2))
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(nb % 2))
+    cwb = dcf.share_to_cwb(k, nb, 16)
+    raw = ok.cw_s.tobytes() + ok.cw_v.tobytes() + ok.cw_t.tobytes()
+    assert cwb == raw + bytes((-len(raw)) % 16) + ok.cw_np1.tobytes()
+    for m in (0, 1, 63, 64, 65, 777):
+        xs = _rand(rng, (m, nb))
+        if m > 3:
+            xs[0] = np.frombuffer(alpha, np.uint8)
+        for b, s in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+            want = O.eval_(P, b, ok, s, xs, nthreads=4)
+            assert np.array_equal(got, want), (nb, m, b)
+
+
+def test_eval_length_mismatch_is_error(dcf):
+    prg = dcf.Aes256HirosePrg(REF_KEYS, 16)
+    d = dcf.DcfImpl(16, 16, prg)
+    k = d.gen(dcf.CmpFn(REF_ALPHAS[0], REF_BETA), [bytes(16), bytes(16)], dcf.BoundState.LtBeta)
+    with pytest.raises(dcf.DcfError):
+        d.eval(False, k, REF_ALPHAS, np.zeros((4, 16), np.uint8))  # reference would silently truncate
+    with pytest.raises(dcf.DcfError):
+        d.eval(False, dcf.Share(k.s0s, k.cws[:127], k.cw_np1), REF_ALPHAS)  # lib.rs:165
+
+
+def _be_int(rows_u8):
+    return [int.from_bytes(r.tobytes(), "big") for r in rows_u8]
+
+
+@pytest.mark.parametrize("nb,m", [(16, 1 << 20), (4, (1 << 20) + 37)])
+def test_eval_device_large_sample_and_reconstruction(dcf, nb, m):
+    """Large batch on device: bit-exact on a sample vs the oracle, and the
+    reconstruction property y0 ^ y1 == beta * [x < alpha] on every point."""
+    import torch
+    rng = np.random.default_rng(nb)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    d = dcf.DcfImpl(nb, 16, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
+    cwb = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, nb, 16), np.uint8).copy()).cuda()
+    xs_h = _rand(rng, (m, nb))
+    xs = torch.from_numpy(xs_h).cuda()
+    y0 = d.eval_device(False, cwb, torch.tensor(list(s0), dtype=torch.uint8).cuda(), xs)
+    y1 = d.eval_device(True, cwb, torch.tensor(list(s1), dtype=torch.uint8).cuda(), xs)
+    torch.cuda.synchronize()
+    y0h, y1h = y0.cpu().numpy(), y1.cpu().numpy()
+    idx = np.unique(np.concatenate([np.arange(64), np.arange(m - 64, m), rng.integers(0, m, 512)]))
+    ok = O.gen(P, alpha, beta, s0, s1, 0)
+    assert np.array_equal(y0h[idx], O.eval_(P, 0, ok, s0, xs_h[idx], nthreads=8))
+    assert np.array_equal(y1h[idx], O.eval_(P, 1, ok, s1, xs_h[idx], nthreads=8))
+    # reconstruction on all points, vectorised: lexicographic x < alpha on big-endian bytes
+    a = np.frombuffer(alpha, np.uint8)
+    diff = xs_h != a
+    first = np.where(diff.any(1), diff.argmax(1), nb)
+    lt = np.zeros(m, bool)
+    has = first < nb
+    lt[has] = xs_h[has, first[has]] < a[first[has]]
+    rec = y0h ^ y1h
+    bt = np.frombuffer(beta, np.uint8)
+    assert np.array_equal(rec[lt], np.broadcast_to(bt, (int(lt.sum()), 16)))
+    assert not rec[~lt].any()
+
+
+@pytest.mark.parametrize("K,P", [(1, 100), (37, 64), (10, 13), (300, 128)])
+def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P):
+    import torch
+    nb = 16
+    rng = np.random.default_rng(K * 1000 + P)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, Po = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    d = dcf.DcfImpl(nb, 16, prg)
+    alpha, beta, s0, s1 = (_rand(rng, (K, nb)), _rand(rng, (K, 16)), _rand(rng, (K, 16)), _rand(rng, (K, 16)))
+    T = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    for bound in (0, 1):
+        cwb = d.gen_batch_device(T(alpha), T(beta), T(s0), T(s1), dcf.BoundState(bound))
+        xs = _rand(rng, (K * P, nb))
+        xs[::P] = alpha  # x == alpha for the first point of each key
+        y0 = d.eval_multikey_device(False, cwb, T(s0), T(xs), P)
+        y1 = d.eval_multikey_device(True, cwb, T(s1), T(xs), P)
+        torch.cuda.synchronize()
+        cw = cwb.cpu().numpy()
+        n = 8 * nb
+        cws = cw[:n * K * 16].reshape(n, K, 16)
+        cwv = cw[n * K * 16:2 * n * K * 16].reshape(n, K, 16)
+        cwt = cw[2 * n * K * 16:2 * n * K * 16 + n * K].reshape(n, K)
+        off = dcf.cwb_np1_offset(nb, 16, K)
+        np1 = cw[off:off + K * 16].reshape(K, 16)
+        y0h, y1h = y0.cpu().numpy(), y1.cpu().numpy()
+        for key in sorted(set([0, K - 1] + list(rng.integers(0, K, 6)))):
+            ok = O.gen(Po, alpha[key].tobytes(), beta[key].tobytes(), s0[key].tobytes(), s1[key].tobytes(), bound)
+            assert np.array_equal(cws[:, key], ok.cw_s) and np.array_equal(cwv[:, key], ok.cw_v)
+            assert np.array_equal(cwt[:, key], ok.cw_t) and np.array_equal(np1[key], ok.cw_np1)
+            sl = slice(key * P, (key + 1) * P)
+            assert np.array_equal(y0h[sl], O.eval_(Po, 0, ok, s0[key].tobytes(), xs[sl]))
+            assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl]))
+        # reconstruction at x == alpha is 0 for both bounds (f(alpha) = 0, lib.rs:62)
+        assert not (y0h[::P] ^ y1h[::P]).any()
+
+
+def test_error_codes_on_device(dcf):
+    with pytest.raises(dcf.DcfError) as e:
+        dcf.Aes256HirosePrg([bytes(32)] * 17, 32)
+    assert e.value.code == -3
+    with pytest.raises(dcf.DcfError) as e:
+        dcf.Aes256HirosePrg([bytes(32)] * 2, 8)
+    assert e.value.code == -2
