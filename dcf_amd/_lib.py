@@ -47,6 +47,14 @@ def load(path: str = LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise ImportError(f"{path} is missing: run `python -m dcf_amd.build` (hipcc, gfx950)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (same soname,
+    # libamdhip64.so.7).  Loading torch first makes the dynamic loader bind this
+    # library to torch's runtime instead of mapping /opt/rocm's as a second one,
+    # which would see no device once torch owns it.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     vp, sz, i, u8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p
     sig = {

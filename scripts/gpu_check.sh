@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+python -c "import torch;print(torch.cuda.get_device_name(0))" > gpurun_out/dev.txt 2>&1
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+timeout -k 10 600 python bench.py --steps 5 --warmup 2 > gpurun_out/bench.log 2>&1

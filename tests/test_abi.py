@@ -91,3 +91,9 @@ def test_product_has_no_oracle_dependency():
             if f.endswith((".py", ".hip", ".h", ".hpp", ".cpp")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in txt.replace("no CPU fallback", ""), f
+
+
+def test_single_hip_runtime_in_process(hip_lib):
+    """torch and libdcf_hip.so must share one libamdhip64 (two runtimes -> 'no device')."""
+    maps = {line.split()[-1] for line in open("/proc/self/maps") if "libamdhip64" in line}
+    assert len(maps) == 1, maps
