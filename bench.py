@@ -182,7 +182,7 @@ def run_eval(args, world, rank):
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        ns = min(m, 1 << 22)
+        ns = min(m, 1 << 26)
         xs_h = xs[:ns].cpu().numpy()
         ys_h = ys[:ns].cpu().numpy()
         cwb_h = cwb.cpu().numpy().tobytes()

@@ -1,0 +1,175 @@
+// aes_lds.h — AES-256 for gfx950: host key schedule / T-tables and the
+// LDS-replicated T-table device rounds.  Included by dcf_hip.hip only.
+#pragma once
+
+namespace {
+
+// ------------------------------------------------------------------------
+// Host-side AES-256 material (key schedule + T-tables), derived from the
+// GF(2^8) definition.  State words are little-endian columns: word j holds
+// bytes 4j..4j+3 = rows 0..3 of column j.
+// ------------------------------------------------------------------------
+uint8_t g_sbox[256];
+uint32_t g_tab[4 * 256];  // T0..T3, LE
+std::once_flag g_aes_once;
+
+uint8_t gmul(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  for (; b; b >>= 1) {
+    if (b & 1) r ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+  }
+  return r;
+}
+
+void aes_init_tables() {
+  // log/antilog over generator 3 gives inverses without exponentiation.
+  uint8_t exp_t[256], log_t[256] = {0};
+  uint8_t x = 1;
+  for (int i = 0; i < 255; i++) {
+    exp_t[i] = x;
+    log_t[x] = (uint8_t)i;
+    x = gmul(x, 3);
+  }
+  for (int v = 0; v < 256; v++) {
+    uint8_t inv = v ? exp_t[(255 - log_t[v]) % 255] : 0;
+    uint8_t s = inv;
+    for (int k = 1; k <= 4; k++) s ^= (uint8_t)((inv << k) | (inv >> (8 - k)));
+    g_sbox[v] = (uint8_t)(s ^ 0x63);
+  }
+  for (int v = 0; v < 256; v++) {
+    uint32_t s = g_sbox[v], s2 = gmul((uint8_t)s, 2), s3 = gmul((uint8_t)s, 3);
+    uint32_t t0 = s2 | (s << 8) | (s << 16) | (s3 << 24);  // MixColumns column (2,1,1,3)
+    for (int t = 0; t < 4; t++) g_tab[t * 256 + v] = t ? ((t0 << (8 * t)) | (t0 >> (32 - 8 * t))) : t0;
+  }
+}
+
+struct RoundKeys {
+  uint32_t w[60];
+};
+
+void aes256_expand_words(const uint8_t key[32], RoundKeys* rk) {
+  uint8_t b[240];
+  memcpy(b, key, 32);
+  uint8_t rcon = 1;
+  for (int i = 8; i < 60; i++) {
+    uint8_t t[4] = {b[4 * i - 4], b[4 * i - 3], b[4 * i - 2], b[4 * i - 1]};
+    if (i % 8 == 0) {
+      uint8_t t0 = t[0];
+      t[0] = (uint8_t)(g_sbox[t[1]] ^ rcon);
+      t[1] = g_sbox[t[2]];
+      t[2] = g_sbox[t[3]];
+      t[3] = g_sbox[t0];
+      rcon = gmul(rcon, 2);
+    } else if (i % 8 == 4) {
+      for (auto& c : t) c = g_sbox[c];
+    }
+    for (int k = 0; k < 4; k++) b[4 * i + k] = (uint8_t)(b[4 * (i - 8) + k] ^ t[k]);
+  }
+  for (int i = 0; i < 60; i++)
+    rk->w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+               ((uint32_t)b[4 * i + 3] << 24);
+}
+
+// ------------------------------------------------------------------------
+// Device: LDS T-tables and AES-256
+// ------------------------------------------------------------------------
+constexpr int kLdsWords = 32768;  // 128 KiB
+constexpr int kBlock = 1024;      // 16 waves; one workgroup per CU (LDS-limited)
+constexpr uint32_t kMaskLast = 0xFEFFFFFFu;  // clear Lsb0 bit 0 of byte 15 (prg.rs:65-68)
+
+__device__ __forceinline__ void lds_fill_tables(uint32_t* lds, const uint32_t* __restrict__ tab) {
+  for (int idx = threadIdx.x; idx < kLdsWords; idx += blockDim.x) {
+    const int half = idx >> 14, rem = idx & 16383;
+    const int b = rem >> 6, slot = rem & 63;
+    lds[idx] = tab[(2 * half + (slot >> 5)) * 256 + b];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t lane_const() {
+  const uint32_t l = (threadIdx.x & 31u) * 4u;
+  return l | ((128u + l) << 8) | (1u << 16);
+}
+
+// perm selector: byte0 <- lane-const byte (T&1), byte1 <- state byte K,
+// byte2 <- half select (T>>1) or zero, byte3 <- zero.
+template <int T, int K>
+struct Sel {
+  static constexpr uint32_t v =
+      ((T & 1) ? 1u : 0u) | ((4u + K) << 8) | (((T >> 1) ? 2u : 0x0cu) << 16) | (0x0cu << 24);
+};
+
+template <int T, int K>
+__device__ __forceinline__ uint32_t lk(const uint32_t* lds, uint32_t w, uint32_t lc) {
+  const uint32_t addr = __builtin_amdgcn_perm(w, lc, Sel<T, K>::v);
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + addr);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// NB independent AES-256 encryptions under one key schedule (FIPS-197),
+// interleaved for ILP.  st holds LE column words.
+template <int NB>
+__device__ __forceinline__ void aes256_tt(uint32_t (&st)[NB][4], const RoundKeys& rk, const uint32_t* lds,
+                                          uint32_t lc) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] ^= rk.w[j];
+#pragma unroll
+  for (int r = 1; r < 14; ++r) {
+    uint32_t o[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+        const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+        const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+        const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+        o[b][j] = xor3(xor3(a, c, d), e, rk.w[4 * r + j]);
+      }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+  // Final round: SubBytes+ShiftRows+AddRoundKey.  S(x) sits in byte r of T_{(r+2)&3}.
+  uint32_t o[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+      const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+      const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+      const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+      const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
+      const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
+      o[b][j] = xor3(lo, hi, rk.w[56 + j]);
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }
+
+// 32 bits of a byte string starting at byte 4c, Msb0 order (lib.rs:106,181),
+// zero-padded past nbytes.
+__device__ __forceinline__ uint32_t load_bits32(const uint8_t* __restrict__ p, uint32_t c, uint32_t nbytes) {
+  if ((nbytes & 3u) == 0) return bswap32(*reinterpret_cast<const uint32_t*>(p + 4 * c));
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t idx = 4 * c + k;
+    w = (w << 8) | (idx < nbytes ? (uint32_t)p[idx] : 0u);
+  }
+  return w;
+}
+
+}  // namespace

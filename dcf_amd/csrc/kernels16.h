@@ -1,0 +1,228 @@
+// kernels16.h — LAMBDA = 16 kernels (eval, batched gen, PRG hook).
+// Included by dcf_hip.hip only.
+#pragma once
+
+#include "aes_lds.h"
+
+namespace {
+
+
+// ------------------------------------------------------------------------
+// k_eval16: DcfImpl::eval (lib.rs:163-204) at LAMBDA = 16.
+//   MODE 0: one key.  MODE 1: K keys, points_per_key % 64 == 0 (key is
+//   wave-uniform -> scalar CW loads).  MODE 2: K keys, any points_per_key.
+// The Hirose PRG at LAMBDA = 16 (prg.rs:42-73 with the diagonal zip):
+//   A = AES_K0(s), B = AES_K0(~s), M = clear bit0 of byte 15
+//   L = ((A^s)&M, (B^~s)&M, lsb(A^s)[0]),  R = (s&M, ~s&M, lsb(B^~s)[0])
+// ------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kBlock, 1) void k_eval16(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
+    const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint64_t total = num_keys * points_per_key;
+  const uint32_t nlev = 8u * nbytes;
+  const uint32_t nchunk = (nbytes + 3u) >> 2;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
+    const uint64_t g = base + (threadIdx.x & 63u);
+    const bool live = g < total;
+    const uint64_t gg = live ? g : total - 1;
+    uint64_t key = 0;
+    if (MODE == 1) key = __builtin_amdgcn_readfirstlane((uint32_t)(gg / points_per_key));
+    if (MODE == 2) key = gg / points_per_key;
+    const uint4 sv = s0s[key];
+    uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w};
+    uint32_t v[4] = {0u, 0u, 0u, 0u};
+    uint32_t t = party;
+    const uint8_t* x = xs + gg * nbytes;
+    uint32_t lev = 0;
+    for (uint32_t c = 0; c < nchunk; ++c) {
+      uint32_t cur = load_bits32(x, c, nbytes);
+      const uint32_t lend = min(32u, nlev - 32u * c);
+      for (uint32_t b = 0; b < lend; ++b, ++lev) {
+        uint32_t st[2][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          st[0][j] = s[j];
+          st[1][j] = ~s[j];
+        }
+        aes256_tt<2>(st, rk, lds, lc);  // st[0] = A, st[1] = B
+        const uint64_t ci = (uint64_t)lev * num_keys + key;
+        const uint4 cs = cw_s[ci];
+        const uint4 cv = cw_v[ci];
+        const uint32_t ct = cw_t[ci];
+        const uint32_t xb = cur >> 31;  // Msb0 bit of x (lib.rs:181)
+        cur <<= 1;
+        const uint32_t keepA = xb - 1u;  // all ones when going left
+        const uint32_t tm = 0u - t;
+        const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w};
+        const uint32_t cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+        // t' (lib.rs:179-180, 183/187): left lsb(A^s)[0] ^ t&tl, right lsb(B^~s)[0] ^ t&tr
+        const uint32_t tl = (st[0][0] ^ s[0]) & 1u;
+        const uint32_t tr = (st[1][0] ^ ~s[0]) & 1u;
+        const uint32_t tn = (xb ? tr : tl) ^ (t & (ct >> xb) & 1u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+          // v ^= v_hat(side) ^ t*cw.v   (lib.rs:182/186)
+          v[j] ^= (((~s[j]) ^ (st[1][j] & keepA)) & msk) ^ (tm & cvw[j]);
+          // s' = s(side) ^ t*cw.s       (lib.rs:177-178, 183/187)
+          s[j] = ((s[j] ^ (st[0][j] & keepA)) & msk) ^ (tm & csw[j]);
+        }
+        t = tn;
+      }
+    }
+    // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192)
+    const uint4 np = cw_np1[key];
+    const uint32_t tm = 0u - t;
+    if (live) {
+      uint4 y;
+      y.x = v[0] ^ s[0] ^ (tm & np.x);
+      y.y = v[1] ^ s[1] ^ (tm & np.y);
+      y.z = v[2] ^ s[2] ^ (tm & np.z);
+      y.w = v[3] ^ s[3] ^ (tm & np.w);
+      ys[g] = y;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------
+// k_gen16: DcfImpl::gen (lib.rs:86-161) at LAMBDA = 16, one lane per key.
+// Four AES blocks per level (PRG on both parties' seeds, lib.rs:103-104).
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock, 1) void k_gen16(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ alpha,
+    const uint4* __restrict__ beta, const uint4* __restrict__ s0_0, const uint4* __restrict__ s0_1,
+    const uint32_t bound, const uint32_t nbytes, const uint64_t num_keys, uint4* __restrict__ cw_s,
+    uint4* __restrict__ cw_v, uint8_t* __restrict__ cw_t, uint4* __restrict__ cw_np1) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint32_t nlev = 8u * nbytes;
+  const uint32_t nchunk = (nbytes + 3u) >> 2;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < num_keys; base += stride) {
+    const uint64_t g = base + (threadIdx.x & 63u);
+    const bool live = g < num_keys;
+    const uint64_t k = live ? g : num_keys - 1;
+    uint32_t s[2][4], va[4] = {0u, 0u, 0u, 0u}, be[4];
+    {
+      const uint4 a0 = s0_0[k], a1 = s0_1[k], bb = beta[k];
+      s[0][0] = a0.x; s[0][1] = a0.y; s[0][2] = a0.z; s[0][3] = a0.w;
+      s[1][0] = a1.x; s[1][1] = a1.y; s[1][2] = a1.z; s[1][3] = a1.w;
+      be[0] = bb.x; be[1] = bb.y; be[2] = bb.z; be[3] = bb.w;
+    }
+    uint32_t t0 = 0u, t1 = 1u;  // lib.rs:100
+    const uint8_t* al = alpha + k * nbytes;
+    uint32_t lev = 0;
+    for (uint32_t c = 0; c < nchunk; ++c) {
+      uint32_t cur = load_bits32(al, c, nbytes);
+      const uint32_t lend = min(32u, nlev - 32u * c);
+      for (uint32_t b = 0; b < lend; ++b, ++lev) {
+        uint32_t st[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          st[0][j] = s[0][j];
+          st[1][j] = ~s[0][j];
+          st[2][j] = s[1][j];
+          st[3][j] = ~s[1][j];
+        }
+        aes256_tt<4>(st, rk, lds, lc);  // A0, B0, A1, B1
+        const uint32_t a = cur >> 31;   // alpha_i, Msb0 (lib.rs:106)
+        cur <<= 1;
+        const uint32_t am = 0u - a;     // all ones when keep = R, lose = L
+        // LtBeta: beta joins v_cw when lose == L (alpha_i = 1); GtBeta when lose == R (lib.rs:114-125)
+        const uint32_t bm = (bound == 0) ? am : ~am;
+        uint32_t scw[4], vcw[4];
+        // PRG outputs per party p: L = ((A^s)&M, (B^~s)&M), R = (s&M, ~s&M)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+          const uint32_t sl0 = (st[0][j] ^ s[0][j]) & msk, vl0 = (st[1][j] ^ ~s[0][j]) & msk;
+          const uint32_t sr0 = s[0][j] & msk, vr0 = ~s[0][j] & msk;
+          const uint32_t sl1 = (st[2][j] ^ s[1][j]) & msk, vl1 = (st[3][j] ^ ~s[1][j]) & msk;
+          const uint32_t sr1 = s[1][j] & msk, vr1 = ~s[1][j] & msk;
+          const uint32_t slose0 = a ? sl0 : sr0, slose1 = a ? sl1 : sr1;
+          const uint32_t vlose0 = a ? vl0 : vr0, vlose1 = a ? vl1 : vr1;
+          const uint32_t vkeep0 = a ? vr0 : vl0, vkeep1 = a ? vr1 : vl1;
+          scw[j] = slose0 ^ slose1;                                    // lib.rs:112
+          vcw[j] = vlose0 ^ vlose1 ^ va[j] ^ (bm & be[j]);             // lib.rs:113-125
+          va[j] ^= vkeep0 ^ vkeep1 ^ vcw[j];                           // lib.rs:126-129
+        }
+        const uint32_t tl0 = (st[0][0] ^ s[0][0]) & 1u, tr0 = (st[1][0] ^ ~s[0][0]) & 1u;
+        const uint32_t tl1 = (st[2][0] ^ s[1][0]) & 1u, tr1 = (st[3][0] ^ ~s[1][0]) & 1u;
+        const uint32_t tlcw = tl0 ^ tl1 ^ a ^ 1u;  // lib.rs:130
+        const uint32_t trcw = tr0 ^ tr1 ^ a;       // lib.rs:131
+        const uint32_t tkcw = a ? trcw : tlcw;
+        const uint32_t m0 = 0u - t0, m1 = 0u - t1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // lib.rs:139-148
+          const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+          const uint32_t sk0 = a ? (s[0][j] & msk) : ((st[0][j] ^ s[0][j]) & msk);
+          const uint32_t sk1 = a ? (s[1][j] & msk) : ((st[2][j] ^ s[1][j]) & msk);
+          s[0][j] = sk0 ^ (m0 & scw[j]);
+          s[1][j] = sk1 ^ (m1 & scw[j]);
+        }
+        const uint32_t nt0 = (a ? tr0 : tl0) ^ (t0 & tkcw);  // lib.rs:149-152
+        const uint32_t nt1 = (a ? tr1 : tl1) ^ (t1 & tkcw);
+        t0 = nt0;
+        t1 = nt1;
+        if (live) {
+          const uint64_t ci = (uint64_t)lev * num_keys + k;
+          cw_s[ci] = make_uint4(scw[0], scw[1], scw[2], scw[3]);
+          cw_v[ci] = make_uint4(vcw[0], vcw[1], vcw[2], vcw[3]);
+          cw_t[ci] = (uint8_t)(tlcw | (trcw << 1));
+        }
+      }
+    }
+    if (live)  // lib.rs:155
+      cw_np1[k] = make_uint4(s[0][0] ^ s[1][0] ^ va[0], s[0][1] ^ s[1][1] ^ va[1], s[0][2] ^ s[1][2] ^ va[2],
+                             s[0][3] ^ s[1][3] ^ va[3]);
+  }
+}
+
+// ------------------------------------------------------------------------
+// k_prg16: Aes256HirosePrg::gen (prg.rs:42-73) at LAMBDA = 16 for m seeds.
+// Output row per seed: s_l | v_l | s_r | v_r | t_l | t_r (66 bytes).
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock, 1) void k_prg16(const uint32_t* __restrict__ tab, const RoundKeys rk,
+                                                     const uint4* __restrict__ seeds, const uint64_t m,
+                                                     uint8_t* __restrict__ out) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < m; g += stride) {
+    const uint4 sv = seeds[g];
+    const uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w};
+    uint32_t st[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      st[0][j] = s[j];
+      st[1][j] = ~s[j];
+    }
+    aes256_tt<2>(st, rk, lds, lc);
+    uint32_t o[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+      o[0][j] = (st[0][j] ^ s[j]) & msk;
+      o[1][j] = (st[1][j] ^ ~s[j]) & msk;
+      o[2][j] = s[j] & msk;
+      o[3][j] = ~s[j] & msk;
+    }
+    uint8_t* row = out + g * 66;
+    for (int q = 0; q < 4; ++q)
+      for (int j = 0; j < 4; ++j)
+        for (int k = 0; k < 4; ++k) row[16 * q + 4 * j + k] = (uint8_t)(o[q][j] >> (8 * k));
+    row[64] = (uint8_t)((st[0][0] ^ s[0]) & 1u);
+    row[65] = (uint8_t)((st[1][0] ^ ~s[0]) & 1u);
+  }
+}
+
+}  // namespace

@@ -1,0 +1,400 @@
+// kernels_wide.h — LAMBDA >= 32 kernels (eval head/tail, gen, PRG hook).
+// Included by dcf_hip.hip only.
+//
+// At LAMBDA >= 32 the Hirose PRG (prg.rs:42-73, diagonal zip (0,0),(1,1))
+// encrypts only bytes [0,16) under cipher 0 and bytes [16,32) under cipher 17;
+// every other byte of the four outputs is the seed (or ~seed), and bit 0 of
+// byte LAMBDA-1 is cleared.  So per level, with A = E0(s[0:16]),
+// B = E0(~s[0:16]), C = E17(s[16:32]), D = E17(~s[16:32]):
+//   s_L = s  with [0:16) := A ^ s[0:16]      v_L = ~s with [0:16)  := B ^ ~s[0:16]
+//   s_R = s  with [16:32) := C ^ s[16:32]    v_R = ~s with [16:32) := D ^ ~s[16:32]
+//   t_L = lsb(A ^ s)[0], t_R = lsb(B ^ ~s)[0]
+// Bytes [32, LAMBDA) of eval's state therefore never see AES and evolve the
+// same way on both branches: eval's output there is LINEAR in the point's
+// t-sequence T = (t_0 .. t_n) (n = 8N even):
+//   y[j] = c[j] ^ XOR_{l=1..n+1} t_{l-1} W_l[j]
+//   W_l = cw_v[l] ^ (l even ? cw_s[l] : 0)   (l <= n),   W_{n+1} = cw_np1
+//   c   = s0
+// except bit 0 of byte LAMBDA-1, which the PRG clears every level:
+//   W_l.bit = cw_v[l].bit ^ (l == n ? cw_s[l].bit : 0),  W_{n+1}.bit = np1.bit,  c.bit = 0.
+// Eval = k_eval_wide_head (AES walk over bytes [0,32), one lane per point,
+// emits y[0:32) and T) + k_eval_wide_tail (y[32:LAMBDA) as a GF(2)
+// combination of W rows, four-Russians tables of 4 rows in LDS).
+// tests/test_gpu_parity.py checks the result bit for bit against the oracle,
+// which runs the reference algorithm literally.
+#pragma once
+
+#include "aes_lds.h"
+
+namespace {
+
+constexpr int kTWords = 8;  // per-point t-vector stride (32 B): n + 1 <= 256 bits, N <= 31
+
+__device__ __forceinline__ void load_tab4(uint32_t* t4, const uint32_t* __restrict__ tab) {
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) t4[i] = tab[i];
+  __syncthreads();
+}
+
+// AES-256 for a few lanes: plain T-table reads from a 4 KiB LDS copy.
+__device__ __forceinline__ void aes256_small(uint32_t (&w)[4], const RoundKeys& rk, const uint32_t* t4) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] ^= rk.w[j];
+  for (int r = 1; r < 14; ++r) {
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = t4[w[j] & 0xff] ^ t4[256 + ((w[(j + 1) & 3] >> 8) & 0xff)] ^
+             t4[512 + ((w[(j + 2) & 3] >> 16) & 0xff)] ^ t4[768 + (w[(j + 3) & 3] >> 24)] ^ rk.w[4 * r + j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = o[j];
+  }
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    o[j] = (t4[512 + (w[j] & 0xff)] & 0xffu) ^ (t4[768 + ((w[(j + 1) & 3] >> 8) & 0xff)] & 0xff00u) ^
+           (t4[(w[(j + 2) & 3] >> 16) & 0xff] & 0xff0000u) ^ (t4[256 + (w[(j + 3) & 3] >> 24)] & 0xff000000u) ^
+           rk.w[56 + j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = o[j];
+}
+
+// ------------------------------------------------------------------------
+// Head: one lane per point; bytes [0,32) of s and v, plus the t-vector.
+// MASK_HEAD: LAMBDA == 32, byte 31 is the last byte (cleared bit lives here).
+// ------------------------------------------------------------------------
+template <bool MASK_HEAD>
+__global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head(
+    const uint32_t* __restrict__ tab, const RoundKeys rk0, const RoundKeys rk17, const uint8_t* __restrict__ cw_s,
+    const uint8_t* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint8_t* __restrict__ cw_np1,
+    const uint8_t* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint32_t lam, const uint64_t num_keys, const uint64_t key, const uint64_t count, uint8_t* __restrict__ ys,
+    uint32_t* __restrict__ tvec) {
+  // Key `key` of a num_keys-key CWB: row l of cw_s / cw_v at (l * num_keys + key) * lam.
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint32_t nlev = 8u * nbytes;
+  const uint32_t nchunk = (nbytes + 3u) >> 2;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t mlast = MASK_HEAD ? kMaskLast : 0xFFFFFFFFu;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < count; base += stride) {
+    const uint64_t g = base + (threadIdx.x & 63u);
+    const bool live = g < count;
+    const uint64_t gg = live ? g : count - 1;
+    uint32_t s[8], v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] = reinterpret_cast<const uint32_t*>(s0)[j];
+      v[j] = 0u;
+    }
+    uint32_t t = party;
+    uint32_t tacc = party, r = 1;  // bit r of the t-vector = t_r
+    uint32_t* trow = tvec + gg * kTWords;
+    const uint8_t* x = xs + gg * nbytes;
+    uint32_t lev = 0;
+    for (uint32_t c = 0; c < nchunk; ++c) {
+      uint32_t cur = load_bits32(x, c, nbytes);
+      const uint32_t lend = min(32u, nlev - 32u * c);
+      for (uint32_t b = 0; b < lend; ++b, ++lev) {
+        uint32_t e0[2][4], e1[2][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          e0[0][j] = s[j];
+          e0[1][j] = ~s[j];
+          e1[0][j] = s[4 + j];
+          e1[1][j] = ~s[4 + j];
+        }
+        aes256_tt<2>(e0, rk0, lds, lc);   // A, B
+        aes256_tt<2>(e1, rk17, lds, lc);  // C, D
+        const uint64_t ro = ((uint64_t)lev * num_keys + key) * lam;
+        const uint4* cs4 = reinterpret_cast<const uint4*>(cw_s + ro);
+        const uint4* cv4 = reinterpret_cast<const uint4*>(cw_v + ro);
+        const uint4 cs0 = cs4[0], cs1 = cs4[1], cv0 = cv4[0], cv1 = cv4[1];
+        const uint32_t csw[8] = {cs0.x, cs0.y, cs0.z, cs0.w, cs1.x, cs1.y, cs1.z, cs1.w};
+        const uint32_t cvw[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+        const uint32_t ct = cw_t[(uint64_t)lev * num_keys + key];
+        const uint32_t xb = cur >> 31;
+        cur <<= 1;
+        const uint32_t L = xb - 1u;  // all ones when going left
+        const uint32_t R = ~L;
+        const uint32_t tm = 0u - t;
+        const uint32_t tl = (e0[0][0] ^ s[0]) & 1u;
+        const uint32_t tr = (e0[1][0] ^ ~s[0]) & 1u;
+        const uint32_t tn = (xb ? tr : tl) ^ (t & (ct >> xb) & 1u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // bytes [0,16): AES only on the left branch
+          v[j] ^= ((~s[j]) ^ (e0[1][j] & L)) ^ (tm & cvw[j]);
+          s[j] = (s[j] ^ (e0[0][j] & L)) ^ (tm & csw[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // bytes [16,32): AES only on the right branch
+          const uint32_t msk = (j == 3) ? mlast : 0xFFFFFFFFu;
+          v[4 + j] ^= (((~s[4 + j]) ^ (e1[1][j] & R)) & msk) ^ (tm & cvw[4 + j]);
+          s[4 + j] = ((s[4 + j] ^ (e1[0][j] & R)) & msk) ^ (tm & csw[4 + j]);
+        }
+        t = tn;
+        tacc |= t << (r & 31u);
+        if ((r & 31u) == 31u) {
+          if (live) trow[r >> 5] = tacc;
+          tacc = 0;
+        }
+        ++r;
+      }
+    }
+    if (live) {
+      if ((r & 31u) != 0) trow[r >> 5] = tacc;
+      const uint32_t tm = 0u - t;
+      const uint4* np4 = reinterpret_cast<const uint4*>(cw_np1 + key * lam);
+      const uint4 n0 = np4[0], n1 = np4[1];
+      const uint32_t nw[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+      uint4* y4 = reinterpret_cast<uint4*>(ys + gg * lam);
+      y4[0] = make_uint4(v[0] ^ s[0] ^ (tm & nw[0]), v[1] ^ s[1] ^ (tm & nw[1]), v[2] ^ s[2] ^ (tm & nw[2]),
+                         v[3] ^ s[3] ^ (tm & nw[3]));
+      y4[1] = make_uint4(v[4] ^ s[4] ^ (tm & nw[4]), v[5] ^ s[5] ^ (tm & nw[5]), v[6] ^ s[6] ^ (tm & nw[6]),
+                         v[7] ^ s[7] ^ (tm & nw[7]));
+    }
+  }
+}
+
+// W row r (coefficient t_r), 16 bytes at byte offset `off` (>= 32), see file header.
+__device__ __forceinline__ uint4 w_row_piece(const uint8_t* __restrict__ cw_s, const uint8_t* __restrict__ cw_v,
+                                             const uint8_t* __restrict__ cw_np1, uint32_t nlev, uint32_t lam,
+                                             uint64_t num_keys, uint64_t key, uint32_t r, uint32_t off) {
+  if (r > nlev || off >= lam) return make_uint4(0u, 0u, 0u, 0u);
+  if (r == nlev) return *reinterpret_cast<const uint4*>(cw_np1 + key * lam + off);
+  const uint32_t l = r + 1;
+  const uint64_t ro = ((uint64_t)r * num_keys + key) * lam + off;
+  const uint4 cv = *reinterpret_cast<const uint4*>(cw_v + ro);
+  const uint4 cs = *reinterpret_cast<const uint4*>(cw_s + ro);
+  const uint32_t even = (l & 1u) ? 0u : 0xFFFFFFFFu;
+  uint4 w = make_uint4(cv.x ^ (cs.x & even), cv.y ^ (cs.y & even), cv.z ^ (cs.z & even), cv.w ^ (cs.w & even));
+  if (off + 16 == lam) {  // bit 0 of byte LAMBDA-1 (bit 24 of the last word)
+    const uint32_t bit = (cv.w ^ ((l == nlev) ? cs.w : 0u)) & 0x01000000u;
+    w.w = (w.w & ~0x01000000u) | bit;
+  }
+  return w;
+}
+
+// ------------------------------------------------------------------------
+// Tail: y[32 + TW*tile .. +TW) for a range of points.  LP = TW/16 lanes per
+// point, each owns one 16-byte piece.  LDS: G[chunk][nibble][LP] uint4,
+// G[c][e] = XOR of W rows 4c+k over the set bits k of e.  All LP lanes of a
+// point read one contiguous TW-byte entry -> conflict-free ds_read_b128.
+// ------------------------------------------------------------------------
+template <int TW>
+__global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __restrict__ cw_s,
+                                                            const uint8_t* __restrict__ cw_v,
+                                                            const uint8_t* __restrict__ cw_np1,
+                                                            const uint8_t* __restrict__ s0, const uint32_t nlev,
+                                                            const uint32_t lam, const uint64_t num_keys,
+                                                            const uint64_t key, const uint32_t* __restrict__ tvec,
+                                                            const uint64_t count, const uint32_t pts_per_block,
+                                                            uint8_t* __restrict__ ys) {
+  constexpr int LP = TW / 16;
+  extern __shared__ uint4 G[];
+  const uint32_t nrows = nlev + 1, nch = (nrows + 3) >> 2;
+  const uint32_t byte0 = 32u + (uint32_t)blockIdx.x * TW;
+  // singles and zero entries
+  for (uint32_t it = threadIdx.x; it < nch * 16u * LP; it += blockDim.x) {
+    const uint32_t q = it % LP, e = (it / LP) & 15u, c = it / (LP * 16);
+    uint4 val = make_uint4(0u, 0u, 0u, 0u);
+    if (e && !(e & (e - 1))) val = w_row_piece(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, 4 * c + (31 - __clz(e)),
+                         byte0 + 16 * q);
+    if (!e || !(e & (e - 1))) G[it] = val;
+  }
+  __syncthreads();
+  for (uint32_t it = threadIdx.x; it < nch * 16u * LP; it += blockDim.x) {
+    const uint32_t q = it % LP, e = (it / LP) & 15u, c = it / (LP * 16);
+    if (e & (e - 1)) {
+      uint4 a = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (e & (1u << k)) {
+          const uint4 b = G[(c * 16 + (1u << k)) * LP + q];
+          a.x ^= b.x; a.y ^= b.y; a.z ^= b.z; a.w ^= b.w;
+        }
+      G[it] = a;
+    }
+  }
+  __syncthreads();
+  const uint32_t q = threadIdx.x % LP;
+  const uint32_t off = byte0 + 16 * q;
+  const bool lane_live = off < lam;
+  uint4 cst = make_uint4(0u, 0u, 0u, 0u);
+  if (lane_live) {
+    cst = *reinterpret_cast<const uint4*>(s0 + off);
+    if (off + 16 == lam) cst.w &= kMaskLast;
+  }
+  const uint64_t p0 = (uint64_t)blockIdx.y * pts_per_block;
+  const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
+  for (uint64_t p = p0 + threadIdx.x / LP; p < p1; p += blockDim.x / LP) {
+    const uint32_t* trow = tvec + p * kTWords;
+    uint4 acc = cst;
+    uint32_t tw = 0;
+    for (uint32_t c = 0; c < nch; ++c) {
+      if ((c & 7u) == 0) tw = trow[c >> 3];
+      const uint32_t e = (tw >> ((c & 7u) * 4u)) & 15u;
+      const uint4 b = G[(c * 16 + e) * LP + q];
+      acc.x ^= b.x; acc.y ^= b.y; acc.z ^= b.z; acc.w ^= b.w;
+    }
+    if (lane_live) *reinterpret_cast<uint4*>(ys + p * lam + off) = acc;
+  }
+}
+
+// ------------------------------------------------------------------------
+// Gen at LAMBDA >= 32: one workgroup per key; thread i owns 16-byte pieces
+// i, i+blockDim, ... of s_0, s_1, v_alpha (kept in `ws`, 3*LAMBDA per key).
+// Per level 8 AES blocks (E0/E17 on s_p and ~s_p, p = 0, 1) by lanes 0..7.
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_gen_wide(
+    const uint32_t* __restrict__ tab, const RoundKeys rk0, const RoundKeys rk17, const uint8_t* __restrict__ alpha,
+    const uint8_t* __restrict__ beta, const uint8_t* __restrict__ s0_0, const uint8_t* __restrict__ s0_1,
+    const uint32_t bound, const uint32_t nbytes, const uint64_t num_keys, const uint64_t key_base, const uint32_t lam,
+    uint8_t* __restrict__ cw_s, uint8_t* __restrict__ cw_v, uint8_t* __restrict__ cw_t, uint8_t* __restrict__ cw_np1,
+    uint8_t* __restrict__ ws) {
+  __shared__ uint32_t t4[1024];
+  __shared__ uint32_t head[2][2][8];  // [buffer][party][word]: s_p bytes [0,32)
+  __shared__ uint32_t eo[2][4][4];    // [party][A,B,C,D][word]
+  load_tab4(t4, tab);
+  const uint64_t k = key_base + blockIdx.x;
+  const uint32_t npieces = lam / 16, nlev = 8u * nbytes;
+  uint4* w_s0 = reinterpret_cast<uint4*>(ws + (uint64_t)blockIdx.x * 3 * lam);
+  uint4* w_s1 = w_s0 + npieces;
+  uint4* w_va = w_s1 + npieces;
+  const uint4* in0 = reinterpret_cast<const uint4*>(s0_0 + k * lam);
+  const uint4* in1 = reinterpret_cast<const uint4*>(s0_1 + k * lam);
+  const uint4* be = reinterpret_cast<const uint4*>(beta + k * lam);
+  for (uint32_t q = threadIdx.x; q < npieces; q += blockDim.x) {
+    w_s0[q] = in0[q];
+    w_s1[q] = in1[q];
+    w_va[q] = make_uint4(0u, 0u, 0u, 0u);
+    if (q < 2) {
+      const uint4 a = in0[q], b = in1[q];
+      head[0][0][4 * q] = a.x; head[0][0][4 * q + 1] = a.y; head[0][0][4 * q + 2] = a.z; head[0][0][4 * q + 3] = a.w;
+      head[0][1][4 * q] = b.x; head[0][1][4 * q + 1] = b.y; head[0][1][4 * q + 2] = b.z; head[0][1][4 * q + 3] = b.w;
+    }
+  }
+  __syncthreads();
+  uint32_t t0 = 0u, t1 = 1u;  // lib.rs:100
+  const uint8_t* al = alpha + k * nbytes;
+  for (uint32_t lev = 0; lev < nlev; ++lev) {
+    const uint32_t buf = lev & 1u;
+    if (threadIdx.x < 8) {
+      const uint32_t p = threadIdx.x >> 2, which = threadIdx.x & 3u, hi = which >> 1;
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t sw = head[buf][p][4 * hi + j];
+        w[j] = (which & 1u) ? ~sw : sw;
+      }
+      aes256_small(w, hi ? rk17 : rk0, t4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) eo[p][which][j] = w[j];
+    }
+    __syncthreads();
+    const uint32_t a = (al[lev >> 3] >> (7 - (lev & 7))) & 1u;  // Msb0 (lib.rs:106)
+    const uint32_t am = 0u - a;
+    const uint32_t bm = (bound == 0) ? am : ~am;
+    const uint32_t h00 = head[buf][0][0], h10 = head[buf][1][0];
+    const uint32_t tl0 = (eo[0][0][0] ^ h00) & 1u, tr0 = (eo[0][1][0] ^ ~h00) & 1u;
+    const uint32_t tl1 = (eo[1][0][0] ^ h10) & 1u, tr1 = (eo[1][1][0] ^ ~h10) & 1u;
+    const uint32_t tlcw = tl0 ^ tl1 ^ a ^ 1u, trcw = tr0 ^ tr1 ^ a;  // lib.rs:130-131
+    const uint32_t tkcw = a ? trcw : tlcw;
+    const uint32_t m0 = 0u - t0, m1 = 0u - t1;
+    for (uint32_t q = threadIdx.x; q < npieces; q += blockDim.x) {
+      const uint4 S0 = w_s0[q], S1 = w_s1[q], VA = w_va[q], BE = be[q];
+      uint32_t s0w[4] = {S0.x, S0.y, S0.z, S0.w}, s1w[4] = {S1.x, S1.y, S1.z, S1.w};
+      uint32_t vaw[4] = {VA.x, VA.y, VA.z, VA.w};
+      const uint32_t bw[4] = {BE.x, BE.y, BE.z, BE.w};
+      uint32_t scw[4], vcw[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t msk = (q == npieces - 1 && j == 3) ? kMaskLast : 0xFFFFFFFFu;
+        // PRG outputs for this piece (see file header)
+        const uint32_t sl0 = ((q == 0) ? (eo[0][0][j] ^ s0w[j]) : s0w[j]) & msk;
+        const uint32_t vl0 = ((q == 0) ? (eo[0][1][j] ^ ~s0w[j]) : ~s0w[j]) & msk;
+        const uint32_t sr0 = ((q == 1) ? (eo[0][2][j] ^ s0w[j]) : s0w[j]) & msk;
+        const uint32_t vr0 = ((q == 1) ? (eo[0][3][j] ^ ~s0w[j]) : ~s0w[j]) & msk;
+        const uint32_t sl1 = ((q == 0) ? (eo[1][0][j] ^ s1w[j]) : s1w[j]) & msk;
+        const uint32_t vl1 = ((q == 0) ? (eo[1][1][j] ^ ~s1w[j]) : ~s1w[j]) & msk;
+        const uint32_t sr1 = ((q == 1) ? (eo[1][2][j] ^ s1w[j]) : s1w[j]) & msk;
+        const uint32_t vr1 = ((q == 1) ? (eo[1][3][j] ^ ~s1w[j]) : ~s1w[j]) & msk;
+        scw[j] = (a ? sl0 : sr0) ^ (a ? sl1 : sr1);                          // lib.rs:112
+        vcw[j] = (a ? vl0 : vr0) ^ (a ? vl1 : vr1) ^ vaw[j] ^ (bm & bw[j]);  // lib.rs:113-125
+        vaw[j] ^= (a ? vr0 : vl0) ^ (a ? vr1 : vl1) ^ vcw[j];                // lib.rs:126-129
+        s0w[j] = (a ? sr0 : sl0) ^ (m0 & scw[j]);                            // lib.rs:139-148
+        s1w[j] = (a ? sr1 : sl1) ^ (m1 & scw[j]);
+      }
+      const uint64_t ci = ((uint64_t)lev * num_keys + k) * lam + 16ull * q;
+      *reinterpret_cast<uint4*>(cw_s + ci) = make_uint4(scw[0], scw[1], scw[2], scw[3]);
+      *reinterpret_cast<uint4*>(cw_v + ci) = make_uint4(vcw[0], vcw[1], vcw[2], vcw[3]);
+      w_s0[q] = make_uint4(s0w[0], s0w[1], s0w[2], s0w[3]);
+      w_s1[q] = make_uint4(s1w[0], s1w[1], s1w[2], s1w[3]);
+      w_va[q] = make_uint4(vaw[0], vaw[1], vaw[2], vaw[3]);
+      if (q < 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          head[buf ^ 1u][0][4 * q + j] = s0w[j];
+          head[buf ^ 1u][1][4 * q + j] = s1w[j];
+        }
+      }
+    }
+    if (threadIdx.x == 0) cw_t[(uint64_t)lev * num_keys + k] = (uint8_t)(tlcw | (trcw << 1));
+    const uint32_t nt0 = (a ? tr0 : tl0) ^ (t0 & tkcw);  // lib.rs:149-152
+    const uint32_t nt1 = (a ? tr1 : tl1) ^ (t1 & tkcw);
+    t0 = nt0;
+    t1 = nt1;
+    __syncthreads();
+  }
+  for (uint32_t q = threadIdx.x; q < npieces; q += blockDim.x) {  // lib.rs:155
+    const uint4 S0 = w_s0[q], S1 = w_s1[q], VA = w_va[q];
+    *reinterpret_cast<uint4*>(cw_np1 + k * lam + 16ull * q) =
+        make_uint4(S0.x ^ S1.x ^ VA.x, S0.y ^ S1.y ^ VA.y, S0.z ^ S1.z ^ VA.z, S0.w ^ S1.w ^ VA.w);
+  }
+}
+
+// PRG test hook at LAMBDA >= 32: one thread per (seed, 16-byte piece).
+__global__ __launch_bounds__(256) void k_prg_wide(const uint32_t* __restrict__ tab, const RoundKeys rk0,
+                                                  const RoundKeys rk17, const uint8_t* __restrict__ seeds,
+                                                  const uint64_t m, const uint32_t lam, uint8_t* __restrict__ out) {
+  __shared__ uint32_t t4[1024];
+  load_tab4(t4, tab);
+  const uint32_t npieces = lam / 16;
+  const uint64_t total = m * npieces;
+  const uint64_t row = 4ull * lam + 2;
+  for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+       it += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t g = it / npieces;
+    const uint32_t q = (uint32_t)(it % npieces);
+    const uint4 sv = *reinterpret_cast<const uint4*>(seeds + g * lam + 16ull * q);
+    const uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w};
+    uint32_t e[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      e[0][j] = s[j];
+      e[1][j] = ~s[j];
+    }
+    if (q < 2) {
+      aes256_small(e[0], q ? rk17 : rk0, t4);
+      aes256_small(e[1], q ? rk17 : rk0, t4);
+    }
+    uint32_t o[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t msk = (q == npieces - 1 && j == 3) ? kMaskLast : 0xFFFFFFFFu;
+      o[0][j] = ((q == 0) ? (e[0][j] ^ s[j]) : s[j]) & msk;
+      o[1][j] = ((q == 0) ? (e[1][j] ^ ~s[j]) : ~s[j]) & msk;
+      o[2][j] = ((q == 1) ? (e[0][j] ^ s[j]) : s[j]) & msk;
+      o[3][j] = ((q == 1) ? (e[1][j] ^ ~s[j]) : ~s[j]) & msk;
+    }
+    uint8_t* r = out + g * row;
+    for (int b = 0; b < 4; ++b)  // rows are 4*LAMBDA+2 bytes: not 16-byte aligned
+      for (int j = 0; j < 16; ++j) r[(uint64_t)b * lam + 16ull * q + j] = (uint8_t)(o[b][j >> 2] >> (8 * (j & 3)));
+    if (q == 0) {
+      r[4ull * lam] = (uint8_t)((e[0][0] ^ s[0]) & 1u);
+      r[4ull * lam + 1] = (uint8_t)((e[1][0] ^ ~s[0]) & 1u);
+    }
+  }
+}
+
+}  // namespace

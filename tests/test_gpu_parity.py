@@ -32,26 +32,65 @@ def test_prg16_golden(dcf, golden):
                                                                       r["tr"])
 
 
-def _lam16_cases(golden):
-    return [c for c in golden("dcf_cases") if c["lambda"] == 16]
+def _full_cases(golden):
+    return [c for c in golden("dcf_cases") if "keys" in c]
+
+
+def test_prg32_golden(dcf, golden):
+    g = golden("prg32")
+    prg = dcf.Aes256HirosePrg([bytes.fromhex(k) for k in g["keys"]], 32)
+    outs = prg.gen_many([bytes.fromhex(r["seed"]) for r in g["rows"]])
+    for r, ((sl, vl, tl), (sr, vr, tr)) in zip(g["rows"], outs):
+        assert (sl.hex(), vl.hex(), tl, sr.hex(), vr.hex(), tr) == (r["sl"], r["vl"], r["tl"], r["sr"], r["vr"],
+                                                                      r["tr"])
+
+
+@pytest.mark.parametrize("lam,nkeys", [(48, 18), (64, 20), (256, 18)])
+def test_prg_wide_vs_oracle(dcf, lam, nkeys):
+    rng = np.random.default_rng(lam)
+    keys = [rng.bytes(32) for _ in range(nkeys)]
+    prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    seeds = [rng.bytes(lam) for _ in range(9)]
+    assert prg.gen_many(seeds) == [P.gen(s) for s in seeds]
 
 
 def test_gen_golden(dcf, golden):
-    for c in _lam16_cases(golden):
-        prg = dcf.Aes256HirosePrg([bytes.fromhex(k) for k in c["keys"]], 16)
-        d = dcf.DcfImpl(c["n_bytes"], 16, prg)
+    for c in _full_cases(golden):
+        lam = c["lambda"]
+        prg = dcf.Aes256HirosePrg([bytes.fromhex(k) for k in c["keys"]], lam)
+        d = dcf.DcfImpl(c["n_bytes"], lam, prg)
         s0s = [bytes.fromhex(s) for s in c["s0s"]]
         k = d.gen(dcf.CmpFn(bytes.fromhex(c["alpha"]), bytes.fromhex(c["beta"])), s0s, dcf.BoundState(c["bound"]))
-        assert dcf.share_to_cwb(k, c["n_bytes"], 16).hex() == c["cwb"], c["name"]
+        assert dcf.share_to_cwb(k, c["n_bytes"], lam).hex() == c["cwb"], c["name"]
+
+
+def test_large_lambda_golden(dcf, golden):
+    """benches/dcf_large_lambda.rs shape (LAMBDA = 16384, 2048 AES keys) at N = 2."""
+    for c in golden("dcf_cases"):
+        if "keys" in c:
+            continue
+        lam, nb = c["lambda"], c["n_bytes"]
+        keys = [detbytes(c["keys_fmt"].format(i=i), 32) for i in range(c["cipher_n"])]
+        prg = dcf.Aes256HirosePrg(keys, lam)
+        d = dcf.DcfImpl(nb, lam, prg)
+        s0s = [detbytes(t, lam) for t in c["s0_tags"]]
+        k = d.gen(dcf.CmpFn(detbytes(c["alpha_tag"], nb), detbytes(c["beta_tag"], lam)), s0s,
+                  dcf.BoundState(c["bound"]))
+        assert hashlib.sha256(dcf.share_to_cwb(k, nb, lam)).hexdigest() == c["cwb_sha256"]
+        xs = [detbytes(c["xs_fmt"].format(i=i), nb) for i in range(c["m"])]
+        for b, key in ((0, "y0_sha256"), (1, "y1_sha256")):
+            ys = d.eval(bool(b), dcf.Share([s0s[b]], k.cws, k.cw_np1), xs)
+            assert hashlib.sha256(ys.tobytes()).hexdigest() == c[key], (c["name"], b)
 
 
 def test_eval_golden(dcf, golden):
-    for c in _lam16_cases(golden):
-        prg = dcf.Aes256HirosePrg([bytes.fromhex(k) for k in c["keys"]], 16)
+    for c in _full_cases(golden):
+        lam = c["lambda"]
+        prg = dcf.Aes256HirosePrg([bytes.fromhex(k) for k in c["keys"]], lam)
         nb = c["n_bytes"]
-        d = dcf.DcfImpl(nb, 16, prg)
+        d = dcf.DcfImpl(nb, lam, prg)
         s0s = [bytes.fromhex(s) for s in c["s0s"]]
-        full = dcf.cwb_to_share(bytes.fromhex(c["cwb"]), nb, 16, s0s)
+        full = dcf.cwb_to_share(bytes.fromhex(c["cwb"]), nb, lam, s0s)
         xs = [bytes.fromhex(x) for x in c["xs"]]
         for b, key in ((0, "y0"), (1, "y1")):
             k = dcf.Share([s0s[b]], full.cws, full.cw_np1)  # lib.rs:382-385: s0s trimmed per party
@@ -105,10 +144,6 @@ def test_eval_length_mismatch_is_error(dcf):
         d.eval(False, k, REF_ALPHAS, np.zeros((4, 16), np.uint8))  # reference would silently truncate
     with pytest.raises(dcf.DcfError):
         d.eval(False, dcf.Share(k.s0s, k.cws[:127], k.cw_np1), REF_ALPHAS)  # lib.rs:165
-
-
-def _be_int(rows_u8):
-    return [int.from_bytes(r.tobytes(), "big") for r in rows_u8]
 
 
 @pytest.mark.parametrize("nb,m", [(16, 1 << 20), (4, (1 << 20) + 37)])
@@ -180,6 +215,50 @@ def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P):
             assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl]))
         # reconstruction at x == alpha is 0 for both bounds (f(alpha) = 0, lib.rs:62)
         assert not (y0h[::P] ^ y1h[::P]).any()
+
+
+@pytest.mark.parametrize("lam,nb,m", [(32, 2, 70), (48, 3, 65), (64, 16, 33), (112, 4, 130), (1024, 2, 40),
+                                      (4096, 16, 12)])
+def test_wide_eval_random_vs_oracle(dcf, lam, nb, m):
+    """LAMBDA >= 32: head/tail kernels vs the literal oracle, both parties, both bounds."""
+    rng = np.random.default_rng(lam * 7 + nb)
+    keys = [rng.bytes(32) for _ in range(18)]
+    prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    for bound in (0, 1):
+        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+        ok = O.gen(P, alpha, beta, s0, s1, bound)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
+        raw = ok.cw_s.tobytes() + ok.cw_v.tobytes() + ok.cw_t.tobytes()
+        assert dcf.share_to_cwb(k, nb, lam) == raw + bytes((-len(raw)) % 16) + ok.cw_np1.tobytes()
+        xs = _rand(rng, (m, nb))
+        xs[0] = np.frombuffer(alpha, np.uint8)
+        for b, s in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+            assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, b, bound)
+
+
+def test_wide_gen_batch_and_multikey(dcf):
+    import torch
+    lam, nb, K, Pp = 64, 2, 5, 7
+    rng = np.random.default_rng(99)
+    keys = [rng.bytes(32) for _ in range(18)]
+    prg, Po = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    alpha, beta, s0, s1 = (_rand(rng, (K, nb)), _rand(rng, (K, lam)), _rand(rng, (K, lam)), _rand(rng, (K, lam)))
+    T = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    cwb = d.gen_batch_device(T(alpha), T(beta), T(s0), T(s1), dcf.BoundState.GtBeta)
+    xs = _rand(rng, (K * Pp, nb))
+    y1 = d.eval_multikey_device(True, cwb, T(s1), T(xs), Pp)
+    torch.cuda.synchronize()
+    cw, y1h = cwb.cpu().numpy(), y1.cpu().numpy()
+    n = 8 * nb
+    cws = cw[:n * K * lam].reshape(n, K, lam)
+    for key in range(K):
+        ok = O.gen(Po, alpha[key].tobytes(), beta[key].tobytes(), s0[key].tobytes(), s1[key].tobytes(), 1)
+        assert np.array_equal(cws[:, key], ok.cw_s)
+        sl = slice(key * Pp, (key + 1) * Pp)
+        assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl]))
 
 
 def test_error_codes_on_device(dcf):
