@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import dcf_amd  # noqa: E402
+from dcf_amd.dist import broadcast_key, weak_slice  # noqa: E402
 
 METRIC = "DCF evals/sec (node) at 128-bit input, λ=16B; AES blocks/s vs INT roofline"
 
@@ -61,12 +62,6 @@ def dist_setup(n_gpus: int):
     return world, rank, local
 
 
-def bcast(t: torch.Tensor, world: int):
-    if world > 1:
-        dist.broadcast(t, src=0)
-    return t
-
-
 def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int):
     """Rank 0 runs gen on its GPU; the CWB and both seeds go to every rank by RCCL broadcast."""
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -78,14 +73,16 @@ def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int):
         k = d.gen(dcf_amd.CmpFn(alpha, beta), [s0, s1], dcf_amd.BoundState.LtBeta)
         cwb.copy_(torch.from_numpy(np.frombuffer(dcf_amd.share_to_cwb(k, n_bytes, lam), np.uint8).copy()))
         seeds.copy_(torch.from_numpy(np.frombuffer(s0 + s1, np.uint8).reshape(2, lam).copy()))
-    bcast(cwb, world)
-    bcast(seeds, world)
+    broadcast_key([cwb, seeds], src=0)
     return cwb, seeds, alpha, beta
 
 
 def gen_points(m: int, n_bytes: int, rank: int, seed: int) -> torch.Tensor:
+    """Rank r's slice [r*m, (r+1)*m) of the global point space (weak scaling),
+    drawn on device from a generator keyed by (seed, slice start)."""
+    start, _ = weak_slice(m, rank)
     g = torch.Generator(device="cuda")
-    g.manual_seed(seed * 1000003 + rank)
+    g.manual_seed(seed * 1000003 + start)
     return torch.randint(0, 256, (m, n_bytes), dtype=torch.uint8, device="cuda", generator=g)
 
 
