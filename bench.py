@@ -41,6 +41,23 @@ PEAK_LDS_LOOKUPS = CUS * LDS_B32_LOOKUPS_PER_CLK_CU * CLK_HZ
 PEAK_AES_BLOCKS = PEAK_LDS_LOOKUPS / AES256_LOOKUPS_PER_BLOCK  # ~87.8 G blocks/s per GPU
 
 
+def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by scripts/prof_summary.py from
+    scripts/gpu_profile.sh: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md §HBM),
+    only when that profile ran this exact launch shape; else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if (t.get("kernel"), t.get("points_per_launch"), t.get("n_bytes"), t.get("lambda")) != (kernel, points, n_bytes,
+                                                                                            lam):
+        return None
+    return t.get("traffic_bytes")
+
+
 def blocks_per_eval(n_bytes: int, lam: int) -> int:
     """The reference's AES-256 block count per eval: 2 per level at LAMBDA = 16,
     4 per level at LAMBDA >= 32 (prg.rs:48-53 called once per level, lib.rs:176)."""
@@ -171,7 +188,8 @@ def run_eval(args, world, rank):
         "roofline": {
             "bound": "lds", "kernel": "k_eval16<0>",
             "achieved": per_gpu_blocks / 1e9, "peak": PEAK_AES_BLOCKS / 1e9, "unit": "G AES-256 blocks/s",
-            "frac": per_gpu_blocks / PEAK_AES_BLOCKS, "traffic": None,
+            "frac": per_gpu_blocks / PEAK_AES_BLOCKS, "traffic": pmc_traffic("k_eval16<0>", m, nb, lam),
+            "algorithmic_bytes": m * (nb + lam),
             "kernel_ms": kern_s * 1e3,
             "note": "blocks = reference count (2 per level, 128 levels); peak = 256 CU x 32 ds_read_b32 "
                     "lookups/clk x 2.4 GHz / 224 lookups per T-table AES-256 block; per GPU",
