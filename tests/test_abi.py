@@ -84,13 +84,17 @@ def test_share_cwb_roundtrip_matches_oracle_layout(hip_lib):
 
 
 def test_product_has_no_oracle_dependency():
-    """The product package must not import or link the oracle."""
+    """The product package must not import, link or load the oracle."""
     pkg = os.path.join(ROOT, "dcf_amd")
+    bad = re.compile(r"(import\s+oracle|from\s+oracle|dcf_oracle|orc_[a-z_]+\(|oracle/)")
     for dirpath, _, files in os.walk(pkg):
         for f in files:
             if f.endswith((".py", ".hip", ".h", ".hpp", ".cpp")):
                 txt = open(os.path.join(dirpath, f)).read()
-                assert "oracle" not in txt.replace("no CPU fallback", ""), f
+                assert not bad.search(txt), f
+    so = os.path.join(pkg, "libdcf_hip.so")
+    if os.path.exists(so):
+        assert b"dcf_oracle" not in open(so, "rb").read()
 
 
 def test_single_hip_runtime_in_process(hip_lib):
