@@ -32,6 +32,7 @@
 #include "aes_lds.h"
 #include "kernels16.h"
 #include "kernels_wide.h"
+#include "kernels_bs.h"
 
 namespace {
 
@@ -90,6 +91,7 @@ struct dcf_prg {
   uint32_t* d_tab = nullptr;  // T0..T3 (4 KiB) on the device
   uint8_t* d_ws = nullptr;    // stream-ordered scratch (LAMBDA >= 32 paths)
   size_t ws_bytes = 0;
+  int eval_mode = DCF_EVAL_AUTO;
 };
 
 namespace {
@@ -224,6 +226,13 @@ void dcf_prg_free(dcf_prg* p) {
 
 size_t dcf_prg_lambda(const dcf_prg* p) { return p ? p->lambda : 0; }
 
+int dcf_prg_set_eval_mode(dcf_prg* p, int mode) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_BITSLICED) return fail(DCF_ERR_ARG, "bad eval mode");
+  p->eval_mode = mode;
+  return DCF_OK;
+}
+
 int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint8_t* alpha, const uint8_t* beta,
                          const uint8_t* s0_0, const uint8_t* s0_1, int bound, uint8_t* cwb_out, void* stream) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");
@@ -283,7 +292,20 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   const uint4* np1 = (const uint4*)(cwb + dcf_cwb_np1_offset(n_bytes, lam, num_keys));
   const dim3 grid((unsigned)grid_for(total, p->cus)), block(kBlock);
   hipStream_t st = (hipStream_t)stream;
-  if (num_keys == 1)
+  const bool bs_ok = (num_keys == 1 && n_bytes <= 16);
+  if (p->eval_mode == DCF_EVAL_BITSLICED) {
+    if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
+    const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;
+    uint64_t blocks = (waves + 3) / 4;
+    const uint64_t cap = (uint64_t)p->cus * 8;
+    if (blocks > cap) blocks = cap;
+    if (n_bytes % 4 == 0)
+      hipLaunchKernelGGL(k_eval16_bs<true>, dim3((unsigned)blocks), dim3(256), 0, st, p->rk[0], cws, cwv, cwt, np1,
+                         (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
+    else
+      hipLaunchKernelGGL(k_eval16_bs<false>, dim3((unsigned)blocks), dim3(256), 0, st, p->rk[0], cws, cwv, cwt, np1,
+                         (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
+  } else if (num_keys == 1)
     hipLaunchKernelGGL(k_eval16<0>, grid, block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
                        (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)1, (uint64_t)ppk,
                        (uint4*)ys);

@@ -1,0 +1,237 @@
+// kernels_bs.h — bitsliced AES-256 on the VALU (LAMBDA = 16).
+// Included by dcf_hip.hip only.
+//
+// Layout: a quad of lanes (4q..4q+3) evaluates 32 points, one per bit.  Lane
+// c = lane & 3 holds column c of the 16-byte AES state for all 32 points as 32
+// registers st[8r + k] = bit k of the row-r byte (bit j of the register =
+// point j).  SubBytes is the 115-gate Boyar-Peralta circuit on each row
+// (bs_sbox.h); MixColumns and AddRoundKey are lane-local; ShiftRows moves
+// rows 1..3 across the quad with DPP quad_perm (row r of column c comes from
+// column c + r).  No LDS: this path runs on the VALU, which the T-table path
+// (LDS-bound) leaves ~60 % idle — k_eval16_hybrid runs both side by side.
+#pragma once
+
+#include "aes_lds.h"
+#include "bs_sbox.h"
+
+namespace {
+
+constexpr uint32_t kBsPoints = 32;   // points per quad
+constexpr uint32_t kWavePoints = 512;  // points per wave (16 quads)
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+// DPP quad_perm encodings: lane c reads lane sel[c]; ctrl = sel0 | sel1<<2 | sel2<<4 | sel3<<6
+constexpr int kQpRot1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // c <- c+1
+constexpr int kQpRot2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // c <- c+2
+constexpr int kQpRot3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // c <- c+3
+constexpr int kQpBcast0 = 0;                                   // c <- 0
+
+// 32 x 32 bit transpose (LSB convention): afterwards a[j] bit i = old a[i] bit j.
+__device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
+  uint32_t m = 0x0000FFFFu;
+#pragma unroll
+  for (int j = 16; j != 0; j >>= 1, m ^= (m << j)) {
+#pragma unroll
+    for (int k = 0; k < 32; k = (k + j + 1) & ~j) {
+      const uint32_t t = ((a[k] >> j) ^ a[k + j]) & m;
+      a[k + j] ^= t;
+      a[k] ^= t << j;
+    }
+  }
+}
+
+// Round keys as LDS words rkl[4r + c]: lane c reads its column word of round r
+// (a wave-uniform-index select from kernel-argument SGPRs becomes divergent control flow).
+__device__ __forceinline__ void rk_to_lds(uint32_t* rkl, const RoundKeys& rk) {
+  for (int i = threadIdx.x; i < 60; i += blockDim.x) rkl[i] = rk.w[i];
+  __syncthreads();
+}
+
+// st ^= key column (bit 8r+k of kw -> all-ones mask); invert = 1 XORs ~key.
+__device__ __forceinline__ void bs_ark(uint32_t (&st)[32], uint32_t kw) {
+  // Opaque to the optimiser: otherwise LICM hoists all 15 x 32 key masks out of
+  // the level loop and the kernel needs ~500 registers.
+  asm volatile("" : "+v"(kw));
+#pragma unroll
+  for (int i = 0; i < 32; ++i) st[i] ^= (uint32_t)__builtin_amdgcn_sbfe((int)kw, i, 1);
+}
+
+__device__ __forceinline__ void bs_subbytes(uint32_t (&st)[32]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    uint32_t row[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row[k] = st[8 * r + k];
+    bs_sbox(row);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st[8 * r + k] = row[k];
+  }
+}
+
+__device__ __forceinline__ void bs_shiftrows(uint32_t (&st)[32]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    st[8 + k] = qperm<kQpRot1>(st[8 + k]);
+    st[16 + k] = qperm<kQpRot2>(st[16 + k]);
+    st[24 + k] = qperm<kQpRot3>(st[24 + k]);
+  }
+}
+
+// MixColumns on this lane's column: out_r = xtime(a_r ^ a_{r+1}) ^ T ^ a_r, T = a0^a1^a2^a3.
+__device__ __forceinline__ void bs_mixcolumns(uint32_t (&st)[32]) {
+  uint32_t T[8], a0[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a0[k] = st[k];
+    T[k] = st[k] ^ st[8 + k] ^ st[16 + k] ^ st[24 + k];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    uint32_t d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = st[8 * r + k] ^ ((r == 3) ? a0[k] : st[8 * (r + 1) + k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t xt = (k == 0) ? d[7] : ((k == 1 || k == 3 || k == 4) ? (d[k - 1] ^ d[7]) : d[k - 1]);
+      st[8 * r + k] = xt ^ T[k] ^ st[8 * r + k];
+    }
+  }
+}
+
+// AES-256 encryption of 32 blocks (quad-sliced).  `inv_in`: encrypt ~st instead.
+__device__ __forceinline__ void bs_aes256(uint32_t (&st)[32], const uint32_t* rkl, uint32_t c, bool inv_in) {
+  bs_ark(st, inv_in ? ~rkl[c] : rkl[c]);
+#pragma unroll 1
+  for (int r = 1; r < 14; ++r) {
+    bs_subbytes(st);
+    bs_shiftrows(st);
+    bs_mixcolumns(st);
+    bs_ark(st, rkl[4 * r + c]);
+  }
+  bs_subbytes(st);
+  bs_shiftrows(st);
+  bs_ark(st, rkl[56 + c]);
+}
+
+// Broadcast a uniform 16-byte value's column c into bitsliced registers.
+__device__ __forceinline__ void bs_splat(uint32_t (&st)[32], uint32_t w) {
+#pragma unroll
+  for (int i = 0; i < 32; ++i) st[i] = (uint32_t)__builtin_amdgcn_sbfe((int)w, i, 1);
+}
+
+__device__ __forceinline__ uint32_t sel4(uint4 v, uint32_t c) {
+  return (c & 2u) ? ((c & 1u) ? v.w : v.z) : ((c & 1u) ? v.y : v.x);
+}
+
+// One wave's batch of 512 points (32 per quad), party `party`, single key.
+// xl: this wave's 2 KiB of LDS holding 32 levels of transposed x, [level][quad].
+template <bool XALIGNED>
+__device__ __forceinline__ void bs_eval_batch(const uint32_t* rkl, const uint4* __restrict__ cw_s,
+                                              const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
+                                              const uint4 np1, const uint4 s0v, const uint32_t party,
+                                              const uint8_t* __restrict__ xs, const uint32_t nbytes,
+                                              const uint64_t m, const uint64_t p_base, uint32_t* xl,
+                                              uint4* __restrict__ ys) {
+  const uint32_t lane = threadIdx.x & 63u, c = lane & 3u, quad = lane >> 2;
+  const uint64_t p0 = p_base + (uint64_t)quad * kBsPoints;
+  const uint32_t nlev = 8u * nbytes, nchunk = (nbytes + 3u) >> 2;
+  uint32_t s[32], v[32];
+  bs_splat(s, sel4(s0v, c));
+#pragma unroll
+  for (int i = 0; i < 32; ++i) v[i] = 0u;
+  uint32_t T = party ? 0xFFFFFFFFu : 0u;                // t of the 32 points
+  const uint32_t mlast = (c == 3u) ? 0u : 0xFFFFFFFFu;  // register 24 of column 3 = bit 0 of byte 15
+  uint32_t lev = 0;
+  for (uint32_t cc = 0; cc < nchunk; ++cc) {
+    // Lane cc of each quad transposes the quad's 32 x words for levels [32cc, 32cc+32) into LDS.
+    __builtin_amdgcn_wave_barrier();
+    if (c == cc) {
+      uint32_t w[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {  // rows past m are clamped (their outputs are not stored)
+        const uint64_t p = min(p0 + j, m - 1);
+        if (XALIGNED)
+          w[j] = bswap32(*reinterpret_cast<const uint32_t*>(xs + p * nbytes + 4 * cc));
+        else
+          w[j] = load_bits32(xs + p * nbytes, cc, nbytes);
+      }
+      transpose32(w);  // w[i] bit j = bit i of point j's Msb0-ordered word = level 32cc + 31 - i
+#pragma unroll
+      for (int i = 0; i < 32; ++i) xl[(31u - i) * 16u + quad] = w[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t lend = min(32u, nlev - 32u * cc);
+    for (uint32_t b = 0; b < lend; ++b, ++lev) {
+      const uint32_t X = xl[b * 16u + quad];  // bit j: x bit of point j (1 = right)
+      const uint4 cs = cw_s[lev], cv = cw_v[lev];
+      const uint32_t ct = cw_t[lev];
+      const uint32_t csw = sel4(cs, c), cvw = sel4(cv, c);
+      uint32_t st[32];
+      // B = AES(~s): v ^= ((~s) ^ (B & ~X)) & M ^ (T & cw.v)   (lib.rs:182/186)
+#pragma unroll
+      for (int i = 0; i < 32; ++i) st[i] = s[i];
+      bs_aes256(st, rkl, c, true);
+      const uint32_t tR = qperm<kQpBcast0>(st[0] ^ ~s[0]);  // lsb(B ^ ~s)[0] of each point
+      uint32_t cvo = cvw;
+      asm volatile("" : "+v"(cvo));  // keep the 32 CW masks from being materialised before the AES
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        uint32_t hv = (~s[i]) ^ (st[i] & ~X);
+        if (i == 24) hv &= mlast;
+        v[i] ^= hv ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)cvo, i, 1));
+      }
+      // A = AES(s): s' = (s ^ (A & ~X)) & M ^ (T & cw.s)   (lib.rs:177-178, 183/187)
+#pragma unroll
+      for (int i = 0; i < 32; ++i) st[i] = s[i];
+      bs_aes256(st, rkl, c, false);
+      const uint32_t tL = qperm<kQpBcast0>(st[0] ^ s[0]);
+      uint32_t cso = csw;
+      asm volatile("" : "+v"(cso));
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        uint32_t hs = s[i] ^ (st[i] & ~X);
+        if (i == 24) hs &= mlast;
+        s[i] = hs ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)cso, i, 1));
+      }
+      // t' = side t ^ (t & side cw.t)   (lib.rs:179-180)
+      const uint32_t ctl = 0u - (ct & 1u), ctr = 0u - ((ct >> 1) & 1u);
+      T = ((X & tR) | (~X & tL)) ^ (T & ((X & ctr) | (~X & ctl)));
+    }
+  }
+  // y = v ^ s ^ t * cw_np1   (lib.rs:192), then back to one dword per point
+  const uint32_t npw = sel4(np1, c);
+#pragma unroll
+  for (int i = 0; i < 32; ++i) v[i] ^= s[i] ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)npw, i, 1));
+  transpose32(v);  // v[j] = column-c dword of point j
+  uint32_t* y32 = reinterpret_cast<uint32_t*>(ys);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const uint64_t p = p0 + j;
+    if (p < m) y32[p * 4 + c] = v[j];
+  }
+}
+
+// Stand-alone bitsliced eval (single key, N <= 16), one wave per 512-point batch.
+template <bool XALIGNED>
+__global__ __launch_bounds__(256, 3) void k_eval16_bs(const RoundKeys rk, const uint4* __restrict__ cw_s,
+                                                   const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
+                                                   const uint4* __restrict__ cw_np1, const uint4* __restrict__ s0,
+                                                   const uint32_t party, const uint8_t* __restrict__ xs,
+                                                   const uint32_t nbytes, const uint64_t m, uint4* __restrict__ ys) {
+  __shared__ uint32_t xl_all[4][32 * 16];
+  __shared__ uint32_t rkl[60];
+  rk_to_lds(rkl, rk);
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint4 np1 = cw_np1[0], s0v = s0[0];
+  for (uint64_t b = gwave; b * kWavePoints < m; b += nwaves)
+    bs_eval_batch<XALIGNED>(rkl, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m, b * kWavePoints, xl_all[wave],
+                            ys);
+}
+
+}  // namespace

@@ -151,6 +151,10 @@ class Aes256HirosePrg:
     def handle(self) -> ctypes.c_void_p:
         return self._h
 
+    def set_eval_mode(self, mode: int) -> None:
+        """AES engine for LAMBDA = 16 eval: 0 auto, 1 LDS T-table, 2 VALU bitsliced."""
+        check(_lib.load().dcf_prg_set_eval_mode(self._h, int(mode)))
+
     def gen(self, seed: bytes):
         """`Prg::gen` (lib.rs:52-54) for one seed — the GPU PRG kernel, not a CPU path."""
         return self.gen_many([seed])[0]

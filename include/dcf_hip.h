@@ -66,6 +66,11 @@ extern "C" {
 #define DCF_BOUND_LT_BETA 0
 #define DCF_BOUND_GT_BETA 1
 
+/* AES engine for LAMBDA = 16 eval (dcf_prg_set_eval_mode); results are identical. */
+#define DCF_EVAL_AUTO 0      /* library's choice (fastest eligible) */
+#define DCF_EVAL_TTABLE 1    /* LDS T-table AES, one lane per point */
+#define DCF_EVAL_BITSLICED 2 /* VALU bitsliced AES, 32 points per lane quad (single key, N <= 16) */
+
 /* Opaque: an Aes256HirosePrg (prg.rs:22-24) whose AES-256 schedules live on one
  * device, i.e. `DcfImpl::new(Aes256HirosePrg::new(keys))` (lib.rs:74, prg.rs:27). */
 typedef struct dcf_prg dcf_prg;
@@ -83,6 +88,10 @@ const char* dcf_last_error(void);
 int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int device, dcf_prg** out);
 void dcf_prg_free(dcf_prg* prg);
 size_t dcf_prg_lambda(const dcf_prg* prg);
+
+/* Select the AES engine used by eval at LAMBDA = 16 (DCF_EVAL_*).  Tuning and
+ * test knob only: every engine returns identical bytes. */
+int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 
 /* CWB layout helpers (see above). */
 size_t dcf_cwb_bytes(size_t n_bytes, size_t lambda, size_t num_keys);

@@ -114,11 +114,16 @@ def test_reference_reconstruction_kat(dcf, bound):
         assert y0[2].tobytes() != bytes(16) and y1[2].tobytes() != bytes(16)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("nb", [1, 2, 3, 4, 5, 7, 8, 12, 16, 17, 32])
-def test_eval_random_vs_oracle(dcf, nb):
+def test_eval_random_vs_oracle(dcf, nb, mode):
+    """mode 1 = LDS T-table engine, mode 2 = VALU bitsliced engine (N <= 16 only)."""
+    if mode == 2 and nb > 16:
+        pytest.skip("bitsliced engine covers N <= 16")
     rng = np.random.default_rng(100 + nb)
     keys = [rng.bytes(32) for _ in range(2)]
     prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    prg.set_eval_mode(mode)
     d = dcf.DcfImpl(nb, 16, prg)
     alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
     ok = O.gen(P, alpha, beta, s0, s1, int(nb % 2))
@@ -126,7 +131,7 @@ def test_eval_random_vs_oracle(dcf, nb):
     cwb = dcf.share_to_cwb(k, nb, 16)
     raw = ok.cw_s.tobytes() + ok.cw_v.tobytes() + ok.cw_t.tobytes()
     assert cwb == raw + bytes((-len(raw)) % 16) + ok.cw_np1.tobytes()
-    for m in (0, 1, 63, 64, 65, 777):
+    for m in (0, 1, 31, 33, 63, 64, 65, 513, 777):
         xs = _rand(rng, (m, nb))
         if m > 3:
             xs[0] = np.frombuffer(alpha, np.uint8)
@@ -146,14 +151,16 @@ def test_eval_length_mismatch_is_error(dcf):
         d.eval(False, dcf.Share(k.s0s, k.cws[:127], k.cw_np1), REF_ALPHAS)  # lib.rs:165
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("nb,m", [(16, 1 << 20), (4, (1 << 20) + 37)])
-def test_eval_device_large_sample_and_reconstruction(dcf, nb, m):
+def test_eval_device_large_sample_and_reconstruction(dcf, nb, m, mode):
     """Large batch on device: bit-exact on a sample vs the oracle, and the
     reconstruction property y0 ^ y1 == beta * [x < alpha] on every point."""
     import torch
     rng = np.random.default_rng(nb)
     keys = [rng.bytes(32) for _ in range(2)]
     prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    prg.set_eval_mode(mode)
     d = dcf.DcfImpl(nb, 16, prg)
     alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
     k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
