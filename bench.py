@@ -145,6 +145,8 @@ def run_eval(args, world, rank):
     keys = [rng.bytes(32) for _ in range(2)]
     prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
     prg.set_eval_mode(args.eval_mode)
+    if args.hybrid_split is not None:
+        prg.set_hybrid_split(args.hybrid_split)
     d = dcf_amd.DcfImpl(nb, lam, prg)
     cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002)
     s0 = seeds[0].contiguous()
@@ -264,7 +266,8 @@ def main():
     ap.add_argument("--n-bytes", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--eval-mode", type=int, default=0, help="AES engine: 0 auto, 1 T-table, 2 bitsliced")
+    ap.add_argument("--eval-mode", type=int, default=0, help="AES engine: 0 auto, 1 T-table, 2 bitsliced, 3 hybrid")
+    ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves of 12 per workgroup")
     args = ap.parse_args()
     if args.workload == "c2":
         args.n_bytes = args.n_bytes or 4

@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdcf_hip.so")
 
 DCF_OK = 0
-EVAL_AUTO, EVAL_TTABLE, EVAL_BITSLICED = 0, 1, 2
+EVAL_AUTO, EVAL_TTABLE, EVAL_BITSLICED, EVAL_HYBRID = 0, 1, 2, 3
 ERRORS = {
     -1: "DCF_ERR_ARG",
     -2: "DCF_ERR_LAMBDA",
@@ -27,6 +27,7 @@ ERRORS = {
 # Every symbol the header declares (tests check the library exports all of them).
 EXPORTS = [
     "dcf_version", "dcf_last_error", "dcf_hirose_prg_new", "dcf_prg_free", "dcf_prg_lambda", "dcf_prg_set_eval_mode",
+    "dcf_prg_set_hybrid_split",
     "dcf_cwb_bytes", "dcf_cwb_np1_offset", "dcf_gen", "dcf_eval", "dcf_prg_gen",
     "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device",
 ]
@@ -65,6 +66,7 @@ def load(path: str = LIB_PATH):
         "dcf_prg_free": ([vp], None),
         "dcf_prg_lambda": ([vp], sz),
         "dcf_prg_set_eval_mode": ([vp, i], i),
+        "dcf_prg_set_hybrid_split": ([vp, i], i),
         "dcf_cwb_bytes": ([sz, sz, sz], sz),
         "dcf_cwb_np1_offset": ([sz, sz, sz], sz),
         "dcf_gen": ([vp, sz, u8p, u8p, u8p, u8p, i, u8p], i),

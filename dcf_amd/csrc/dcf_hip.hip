@@ -91,7 +91,9 @@ struct dcf_prg {
   uint32_t* d_tab = nullptr;  // T0..T3 (4 KiB) on the device
   uint8_t* d_ws = nullptr;    // stream-ordered scratch (LAMBDA >= 32 paths)
   size_t ws_bytes = 0;
+  uint32_t* d_ctr = nullptr;  // work counter of the hybrid eval kernel
   int eval_mode = DCF_EVAL_AUTO;
+  int hybrid_tt_waves = 6;    // T-table waves of the 12-wave hybrid workgroup
 };
 
 namespace {
@@ -220,6 +222,7 @@ void dcf_prg_free(dcf_prg* p) {
     DeviceGuard dg(p->device);
     if (p->d_tab) (void)hipFree(p->d_tab);
     if (p->d_ws) (void)hipFree(p->d_ws);
+    if (p->d_ctr) (void)hipFree(p->d_ctr);
   }
   delete p;
 }
@@ -228,8 +231,15 @@ size_t dcf_prg_lambda(const dcf_prg* p) { return p ? p->lambda : 0; }
 
 int dcf_prg_set_eval_mode(dcf_prg* p, int mode) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");
-  if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_BITSLICED) return fail(DCF_ERR_ARG, "bad eval mode");
+  if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_HYBRID) return fail(DCF_ERR_ARG, "bad eval mode");
   p->eval_mode = mode;
+  return DCF_OK;
+}
+
+int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  if (ttable_waves < 0 || ttable_waves > kHybridWaves) return fail(DCF_ERR_ARG, "ttable_waves must be in [0, 12]");
+  p->hybrid_tt_waves = ttable_waves;
   return DCF_OK;
 }
 
@@ -293,7 +303,24 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   const dim3 grid((unsigned)grid_for(total, p->cus)), block(kBlock);
   hipStream_t st = (hipStream_t)stream;
   const bool bs_ok = (num_keys == 1 && n_bytes <= 16);
-  if (p->eval_mode == DCF_EVAL_BITSLICED) {
+  int mode = p->eval_mode;
+  if (mode == DCF_EVAL_AUTO) mode = bs_ok ? DCF_EVAL_HYBRID : DCF_EVAL_TTABLE;
+  if (mode == DCF_EVAL_HYBRID) {
+    if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "hybrid eval: single key, N <= 16");
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+    const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
+    uint64_t blocks = (units + kHybridWaves - 1) / kHybridWaves;
+    if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
+    if (n_bytes % 4 == 0)
+      hipLaunchKernelGGL(k_eval16_hybrid<true>, dim3((unsigned)blocks), dim3(kHybridWaves * 64), 0, st, p->d_tab,
+                         p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes,
+                         (uint64_t)total, (uint32_t)p->hybrid_tt_waves, p->d_ctr, (uint4*)ys);
+    else
+      hipLaunchKernelGGL(k_eval16_hybrid<false>, dim3((unsigned)blocks), dim3(kHybridWaves * 64), 0, st, p->d_tab,
+                         p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes,
+                         (uint64_t)total, (uint32_t)p->hybrid_tt_waves, p->d_ctr, (uint4*)ys);
+  } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
     const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;
     uint64_t blocks = (waves + 3) / 4;

@@ -15,6 +15,61 @@ namespace {
 //   A = AES_K0(s), B = AES_K0(~s), M = clear bit0 of byte 15
 //   L = ((A^s)&M, (B^~s)&M, lsb(A^s)[0]),  R = (s&M, ~s&M, lsb(B^~s)[0])
 // ------------------------------------------------------------------------
+// One point, one lane: returns y for point gg of key `key` (the whole
+// lib.rs:166-193 closure).  Used by k_eval16 and by the hybrid kernel.
+__device__ __forceinline__ uint4 tt_eval_one(const uint32_t* lds, uint32_t lc, const RoundKeys& rk,
+                                             const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
+                                             const uint8_t* __restrict__ cw_t, const uint4 np, const uint4 sv,
+                                             uint32_t party, const uint8_t* __restrict__ x, uint32_t nbytes,
+                                             uint64_t num_keys, uint64_t key) {
+  const uint32_t nlev = 8u * nbytes;
+  const uint32_t nchunk = (nbytes + 3u) >> 2;
+  uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w};
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  uint32_t t = party;
+  uint32_t lev = 0;
+  for (uint32_t c = 0; c < nchunk; ++c) {
+    uint32_t cur = load_bits32(x, c, nbytes);
+    const uint32_t lend = min(32u, nlev - 32u * c);
+    for (uint32_t b = 0; b < lend; ++b, ++lev) {
+      uint32_t st[2][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        st[0][j] = s[j];
+        st[1][j] = ~s[j];
+      }
+      aes256_tt<2>(st, rk, lds, lc);  // st[0] = A, st[1] = B
+      const uint64_t ci = (uint64_t)lev * num_keys + key;
+      const uint4 cs = cw_s[ci];
+      const uint4 cv = cw_v[ci];
+      const uint32_t ct = cw_t[ci];
+      const uint32_t xb = cur >> 31;  // Msb0 bit of x (lib.rs:181)
+      cur <<= 1;
+      const uint32_t keepA = xb - 1u;  // all ones when going left
+      const uint32_t tm = 0u - t;
+      const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w};
+      const uint32_t cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+      // t' (lib.rs:179-180, 183/187): left lsb(A^s)[0] ^ t&tl, right lsb(B^~s)[0] ^ t&tr
+      const uint32_t tl = (st[0][0] ^ s[0]) & 1u;
+      const uint32_t tr = (st[1][0] ^ ~s[0]) & 1u;
+      const uint32_t tn = (xb ? tr : tl) ^ (t & (ct >> xb) & 1u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+        // v ^= v_hat(side) ^ t*cw.v   (lib.rs:182/186)
+        v[j] ^= (((~s[j]) ^ (st[1][j] & keepA)) & msk) ^ (tm & cvw[j]);
+        // s' = s(side) ^ t*cw.s       (lib.rs:177-178, 183/187)
+        s[j] = ((s[j] ^ (st[0][j] & keepA)) & msk) ^ (tm & csw[j]);
+      }
+      t = tn;
+    }
+  }
+  // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192)
+  const uint32_t tm = 0u - t;
+  return make_uint4(v[0] ^ s[0] ^ (tm & np.x), v[1] ^ s[1] ^ (tm & np.y), v[2] ^ s[2] ^ (tm & np.z),
+                    v[3] ^ s[3] ^ (tm & np.w));
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock, 1) void k_eval16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
@@ -25,8 +80,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16(
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
   const uint64_t total = num_keys * points_per_key;
-  const uint32_t nlev = 8u * nbytes;
-  const uint32_t nchunk = (nbytes + 3u) >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
     const uint64_t g = base + (threadIdx.x & 63u);
@@ -35,59 +88,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16(
     uint64_t key = 0;
     if (MODE == 1) key = __builtin_amdgcn_readfirstlane((uint32_t)(gg / points_per_key));
     if (MODE == 2) key = gg / points_per_key;
-    const uint4 sv = s0s[key];
-    uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w};
-    uint32_t v[4] = {0u, 0u, 0u, 0u};
-    uint32_t t = party;
-    const uint8_t* x = xs + gg * nbytes;
-    uint32_t lev = 0;
-    for (uint32_t c = 0; c < nchunk; ++c) {
-      uint32_t cur = load_bits32(x, c, nbytes);
-      const uint32_t lend = min(32u, nlev - 32u * c);
-      for (uint32_t b = 0; b < lend; ++b, ++lev) {
-        uint32_t st[2][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          st[0][j] = s[j];
-          st[1][j] = ~s[j];
-        }
-        aes256_tt<2>(st, rk, lds, lc);  // st[0] = A, st[1] = B
-        const uint64_t ci = (uint64_t)lev * num_keys + key;
-        const uint4 cs = cw_s[ci];
-        const uint4 cv = cw_v[ci];
-        const uint32_t ct = cw_t[ci];
-        const uint32_t xb = cur >> 31;  // Msb0 bit of x (lib.rs:181)
-        cur <<= 1;
-        const uint32_t keepA = xb - 1u;  // all ones when going left
-        const uint32_t tm = 0u - t;
-        const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w};
-        const uint32_t cvw[4] = {cv.x, cv.y, cv.z, cv.w};
-        // t' (lib.rs:179-180, 183/187): left lsb(A^s)[0] ^ t&tl, right lsb(B^~s)[0] ^ t&tr
-        const uint32_t tl = (st[0][0] ^ s[0]) & 1u;
-        const uint32_t tr = (st[1][0] ^ ~s[0]) & 1u;
-        const uint32_t tn = (xb ? tr : tl) ^ (t & (ct >> xb) & 1u);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
-          // v ^= v_hat(side) ^ t*cw.v   (lib.rs:182/186)
-          v[j] ^= (((~s[j]) ^ (st[1][j] & keepA)) & msk) ^ (tm & cvw[j]);
-          // s' = s(side) ^ t*cw.s       (lib.rs:177-178, 183/187)
-          s[j] = ((s[j] ^ (st[0][j] & keepA)) & msk) ^ (tm & csw[j]);
-        }
-        t = tn;
-      }
-    }
-    // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192)
-    const uint4 np = cw_np1[key];
-    const uint32_t tm = 0u - t;
-    if (live) {
-      uint4 y;
-      y.x = v[0] ^ s[0] ^ (tm & np.x);
-      y.y = v[1] ^ s[1] ^ (tm & np.y);
-      y.z = v[2] ^ s[2] ^ (tm & np.z);
-      y.w = v[3] ^ s[3] ^ (tm & np.w);
-      ys[g] = y;
-    }
+    const uint4 y = tt_eval_one(lds, lc, rk, cw_s, cw_v, cw_t, cw_np1[key], s0s[key], party, xs + gg * nbytes,
+                                nbytes, num_keys, key);
+    if (live) ys[g] = y;
   }
 }
 

@@ -235,3 +235,56 @@ __global__ __launch_bounds__(256, 3) void k_eval16_bs(const RoundKeys rk, const 
 }
 
 }  // namespace
+
+namespace {
+
+// ------------------------------------------------------------------------
+// k_eval16_hybrid: both AES engines in one launch, one 12-wave workgroup per
+// CU.  Waves [0, n_tt) run the LDS T-table engine (LDS-bound), waves
+// [n_tt, 12) the bitsliced engine (VALU-bound), so the CU's LDS and VALU are
+// busy at the same time.  Work is dequeued in 512-point units from one global
+// counter (reset by the host before each launch): each engine takes units at
+// its own pace, so the split adapts to their relative speed.
+// ------------------------------------------------------------------------
+constexpr int kHybridWaves = 12;
+
+__device__ __forceinline__ uint32_t dequeue_unit(uint32_t* ctr) {
+  uint32_t u = 0;
+  if ((threadIdx.x & 63u) == 0) u = atomicAdd(ctr, 1u);
+  return __builtin_amdgcn_readfirstlane(u);
+}
+
+template <bool XALIGNED>
+__global__ __launch_bounds__(kHybridWaves * 64) void k_eval16_hybrid(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
+    const uint4* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint64_t m, const uint32_t n_tt, uint32_t* __restrict__ ctr, uint4* __restrict__ ys) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint32_t xl_all[kHybridWaves][32 * 16];
+  __shared__ uint32_t rkl[60];
+  lds_fill_tables(lds, tab);
+  rk_to_lds(rkl, rk);
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint64_t nunits = (m + kWavePoints - 1) / kWavePoints;
+  const uint4 np1 = cw_np1[0], s0v = s0[0];
+  if (wave < n_tt) {
+    const uint32_t lc = lane_const();
+    for (uint32_t u = dequeue_unit(ctr); u < nunits; u = dequeue_unit(ctr)) {
+      const uint64_t base = (uint64_t)u * kWavePoints;
+      for (uint32_t it = 0; it < kWavePoints / 64 && base + 64u * it < m; ++it) {
+        const uint64_t g = base + 64u * it + lane;
+        const uint64_t gg = g < m ? g : m - 1;
+        const uint4 y = tt_eval_one(lds, lc, rk, cw_s, cw_v, cw_t, np1, s0v, party, xs + gg * nbytes, nbytes, 1, 0);
+        if (g < m) ys[g] = y;
+      }
+    }
+  } else {
+    uint32_t* xl = xl_all[wave];
+    for (uint32_t u = dequeue_unit(ctr); u < nunits; u = dequeue_unit(ctr))
+      bs_eval_batch<XALIGNED>(rkl, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m, (uint64_t)u * kWavePoints, xl,
+                              ys);
+  }
+}
+
+}  // namespace

@@ -152,8 +152,12 @@ class Aes256HirosePrg:
         return self._h
 
     def set_eval_mode(self, mode: int) -> None:
-        """AES engine for LAMBDA = 16 eval: 0 auto, 1 LDS T-table, 2 VALU bitsliced."""
+        """AES engine for LAMBDA = 16 eval: 0 auto, 1 LDS T-table, 2 VALU bitsliced, 3 hybrid."""
         check(_lib.load().dcf_prg_set_eval_mode(self._h, int(mode)))
+
+    def set_hybrid_split(self, ttable_waves: int) -> None:
+        """Hybrid engine: T-table waves out of 12 per workgroup (rest bitsliced)."""
+        check(_lib.load().dcf_prg_set_hybrid_split(self._h, int(ttable_waves)))
 
     def gen(self, seed: bytes):
         """`Prg::gen` (lib.rs:52-54) for one seed — the GPU PRG kernel, not a CPU path."""

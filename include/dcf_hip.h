@@ -70,6 +70,7 @@ extern "C" {
 #define DCF_EVAL_AUTO 0      /* library's choice (fastest eligible) */
 #define DCF_EVAL_TTABLE 1    /* LDS T-table AES, one lane per point */
 #define DCF_EVAL_BITSLICED 2 /* VALU bitsliced AES, 32 points per lane quad (single key, N <= 16) */
+#define DCF_EVAL_HYBRID 3    /* both engines side by side on every CU (single key, N <= 16) */
 
 /* Opaque: an Aes256HirosePrg (prg.rs:22-24) whose AES-256 schedules live on one
  * device, i.e. `DcfImpl::new(Aes256HirosePrg::new(keys))` (lib.rs:74, prg.rs:27). */
@@ -92,6 +93,10 @@ size_t dcf_prg_lambda(const dcf_prg* prg);
 /* Select the AES engine used by eval at LAMBDA = 16 (DCF_EVAL_*).  Tuning and
  * test knob only: every engine returns identical bytes. */
 int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
+
+/* Hybrid engine: how many of the 12 waves per workgroup run the T-table engine
+ * (the rest run the bitsliced engine).  Tuning knob; results are identical. */
+int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves);
 
 /* CWB layout helpers (see above). */
 size_t dcf_cwb_bytes(size_t n_bytes, size_t lambda, size_t num_keys);

@@ -114,11 +114,11 @@ def test_reference_reconstruction_kat(dcf, bound):
         assert y0[2].tobytes() != bytes(16) and y1[2].tobytes() != bytes(16)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("nb", [1, 2, 3, 4, 5, 7, 8, 12, 16, 17, 32])
 def test_eval_random_vs_oracle(dcf, nb, mode):
-    """mode 1 = LDS T-table engine, mode 2 = VALU bitsliced engine (N <= 16 only)."""
-    if mode == 2 and nb > 16:
+    """mode 1 = LDS T-table engine, 2 = VALU bitsliced engine, 3 = hybrid (2 and 3: N <= 16 only)."""
+    if mode in (2, 3) and nb > 16:
         pytest.skip("bitsliced engine covers N <= 16")
     rng = np.random.default_rng(100 + nb)
     keys = [rng.bytes(32) for _ in range(2)]
@@ -151,7 +151,7 @@ def test_eval_length_mismatch_is_error(dcf):
         d.eval(False, dcf.Share(k.s0s, k.cws[:127], k.cw_np1), REF_ALPHAS)  # lib.rs:165
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("nb,m", [(16, 1 << 20), (4, (1 << 20) + 37)])
 def test_eval_device_large_sample_and_reconstruction(dcf, nb, m, mode):
     """Large batch on device: bit-exact on a sample vs the oracle, and the
@@ -266,6 +266,27 @@ def test_wide_gen_batch_and_multikey(dcf):
         assert np.array_equal(cws[:, key], ok.cw_s)
         sl = slice(key * Pp, (key + 1) * Pp)
         assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl]))
+
+
+@pytest.mark.parametrize("split", [0, 1, 6, 11, 12])
+def test_hybrid_splits_identical(dcf, split):
+    """Every T-table/bitsliced wave split of the hybrid engine returns the same bytes."""
+    import torch
+    rng = np.random.default_rng(split)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg = dcf.Aes256HirosePrg(keys, 16)
+    d = dcf.DcfImpl(16, 16, prg)
+    k = d.gen(dcf.CmpFn(rng.bytes(16), rng.bytes(16)), [rng.bytes(16), rng.bytes(16)], dcf.BoundState.GtBeta)
+    cwb = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, 16, 16), np.uint8).copy()).cuda()
+    s0 = torch.from_numpy(np.frombuffer(k.s0s[0], np.uint8).copy()).cuda()
+    xs = torch.from_numpy(_rand(rng, (300_001, 16))).cuda()
+    prg.set_eval_mode(1)
+    ref = d.eval_device(False, cwb, s0, xs)
+    prg.set_eval_mode(3)
+    prg.set_hybrid_split(split)
+    got = d.eval_device(False, cwb, s0, xs)
+    torch.cuda.synchronize()
+    assert torch.equal(ref, got)
 
 
 def test_error_codes_on_device(dcf):
