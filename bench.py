@@ -146,7 +146,7 @@ def run_eval(args, world, rank):
     prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
     prg.set_eval_mode(args.eval_mode)
     if args.hybrid_split is not None:
-        prg.set_hybrid_split(args.hybrid_split)
+        prg.set_hybrid_split(args.hybrid_split, args.hybrid_mem)
     d = dcf_amd.DcfImpl(nb, lam, prg)
     cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002)
     s0 = seeds[0].contiguous()
@@ -267,7 +267,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--eval-mode", type=int, default=0, help="AES engine: 0 auto, 1 T-table, 2 bitsliced, 3 hybrid")
-    ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves of 12 per workgroup")
+    ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves per workgroup")
+    ap.add_argument("--hybrid-mem", type=int, default=1, help="hybrid: 1 = 16 waves + scratch slabs, 0 = 12 waves")
     args = ap.parse_args()
     if args.workload == "c2":
         args.n_bytes = args.n_bytes or 4

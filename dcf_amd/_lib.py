@@ -66,7 +66,7 @@ def load(path: str = LIB_PATH):
         "dcf_prg_free": ([vp], None),
         "dcf_prg_lambda": ([vp], sz),
         "dcf_prg_set_eval_mode": ([vp, i], i),
-        "dcf_prg_set_hybrid_split": ([vp, i], i),
+        "dcf_prg_set_hybrid_split": ([vp, i, i], i),
         "dcf_cwb_bytes": ([sz, sz, sz], sz),
         "dcf_cwb_np1_offset": ([sz, sz, sz], sz),
         "dcf_gen": ([vp, sz, u8p, u8p, u8p, u8p, i, u8p], i),

@@ -92,8 +92,11 @@ struct dcf_prg {
   uint8_t* d_ws = nullptr;    // stream-ordered scratch (LAMBDA >= 32 paths)
   size_t ws_bytes = 0;
   uint32_t* d_ctr = nullptr;  // work counter of the hybrid eval kernel
+  void* d_slabs = nullptr;    // per-wave s/v slabs of the hybrid kernel (MEM variant)
+  size_t slab_bytes = 0;
   int eval_mode = DCF_EVAL_AUTO;
-  int hybrid_tt_waves = 6;    // T-table waves of the 12-wave hybrid workgroup
+  int hybrid_tt_waves = 8;    // T-table waves per hybrid workgroup
+  int hybrid_mem = 1;         // 1: 16-wave workgroups with s/v slabs; 0: 12 waves, s/v in registers
 };
 
 namespace {
@@ -223,6 +226,7 @@ void dcf_prg_free(dcf_prg* p) {
     if (p->d_tab) (void)hipFree(p->d_tab);
     if (p->d_ws) (void)hipFree(p->d_ws);
     if (p->d_ctr) (void)hipFree(p->d_ctr);
+    if (p->d_slabs) (void)hipFree(p->d_slabs);
   }
   delete p;
 }
@@ -236,10 +240,12 @@ int dcf_prg_set_eval_mode(dcf_prg* p, int mode) {
   return DCF_OK;
 }
 
-int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves) {
+int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves, int slab_variant) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");
-  if (ttable_waves < 0 || ttable_waves > kHybridWaves) return fail(DCF_ERR_ARG, "ttable_waves must be in [0, 12]");
+  if (ttable_waves < 0 || ttable_waves > 16) return fail(DCF_ERR_ARG, "ttable_waves must be in [0, 16]");
+  if (slab_variant != 0 && slab_variant != 1) return fail(DCF_ERR_ARG, "slab_variant must be 0 or 1");
   p->hybrid_tt_waves = ttable_waves;
+  p->hybrid_mem = slab_variant;
   return DCF_OK;
 }
 
@@ -307,19 +313,42 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   if (mode == DCF_EVAL_AUTO) mode = bs_ok ? DCF_EVAL_HYBRID : DCF_EVAL_TTABLE;
   if (mode == DCF_EVAL_HYBRID) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "hybrid eval: single key, N <= 16");
+    const bool mem = p->hybrid_mem != 0;
+    const int waves = mem ? 16 : kHybridWaves;
+    int ntt = p->hybrid_tt_waves;
+    if (mem && ntt < 1) ntt = 1;  // 15 LDS x-slots for bitsliced waves
+    if (ntt > waves) ntt = waves;
     if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
     HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
     const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
-    uint64_t blocks = (units + kHybridWaves - 1) / kHybridWaves;
+    uint64_t blocks = (units + waves - 1) / waves;
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
-    if (n_bytes % 4 == 0)
-      hipLaunchKernelGGL(k_eval16_hybrid<true>, dim3((unsigned)blocks), dim3(kHybridWaves * 64), 0, st, p->d_tab,
-                         p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes,
-                         (uint64_t)total, (uint32_t)p->hybrid_tt_waves, p->d_ctr, (uint4*)ys);
-    else
-      hipLaunchKernelGGL(k_eval16_hybrid<false>, dim3((unsigned)blocks), dim3(kHybridWaves * 64), 0, st, p->d_tab,
-                         p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes,
-                         (uint64_t)total, (uint32_t)p->hybrid_tt_waves, p->d_ctr, (uint4*)ys);
+    uint4* slabs = nullptr;
+    if (mem) {
+      const size_t need = (size_t)p->cus * 16 * kSlabUint4 * sizeof(uint4);
+      if (p->slab_bytes < need) {
+        if (p->d_slabs) {
+          HIP_TRY(hipStreamSynchronize(st));
+          HIP_TRY(hipFree(p->d_slabs));
+          p->d_slabs = nullptr;
+          p->slab_bytes = 0;
+        }
+        HIP_TRY(hipMalloc(&p->d_slabs, need));
+        p->slab_bytes = need;
+      }
+      slabs = reinterpret_cast<uint4*>(p->d_slabs);
+    }
+    const dim3 g((unsigned)blocks), b((unsigned)(waves * 64));
+#define DCF_HYB(XA, MEM)                                                                                   \
+  hipLaunchKernelGGL((k_eval16_hybrid<XA, MEM>), g, b, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,       \
+                     (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint32_t)ntt, \
+                     p->d_ctr, slabs, (uint4*)ys)
+    const bool xa = n_bytes % 4 == 0;
+    if (xa && mem) DCF_HYB(true, true);
+    else if (xa) DCF_HYB(true, false);
+    else if (mem) DCF_HYB(false, true);
+    else DCF_HYB(false, false);
+#undef DCF_HYB
   } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
     const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;

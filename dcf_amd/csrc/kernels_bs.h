@@ -215,6 +215,134 @@ __device__ __forceinline__ void bs_eval_batch(const uint32_t* rkl, const uint4* 
   }
 }
 
+// Same batch with the 32-register s and v of each lane kept in a per-wave
+// scratch slab (16 KiB: [s q0..q7 | v q0..q7][64 lanes] uint4, coalesced)
+// instead of registers: the lane then needs ~100 VGPRs, so 4 waves fit per
+// SIMD and hide the S-box's dependency chains.  s/v are touched once per AES
+// pass (~14.7K VALU ops per level per lane), so the slab traffic is small and
+// L1/L2-resident.
+template <bool XALIGNED>
+__device__ __forceinline__ void bs_eval_batch_mem(const uint32_t* rkl, const uint4* __restrict__ cw_s,
+                                                  const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
+                                                  const uint4 np1, const uint4 s0v, const uint32_t party,
+                                                  const uint8_t* __restrict__ xs, const uint32_t nbytes,
+                                                  const uint64_t m, const uint64_t p_base, uint32_t* xl,
+                                                  uint4* __restrict__ slab, uint4* __restrict__ ys) {
+  const uint32_t lane = threadIdx.x & 63u, c = lane & 3u, quad = lane >> 2;
+  const uint64_t p0 = p_base + (uint64_t)quad * kBsPoints;
+  const uint32_t nlev = 8u * nbytes, nchunk = (nbytes + 3u) >> 2;
+  uint4* __restrict__ sp = slab + lane;           // s quad q at sp[64 q]
+  uint4* __restrict__ vp = slab + 8 * 64 + lane;  // v quad q at vp[64 q]
+  {
+    const int w = (int)sel4(s0v, c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      sp[64 * q] = make_uint4((uint32_t)__builtin_amdgcn_sbfe(w, 4 * q, 1), (uint32_t)__builtin_amdgcn_sbfe(w, 4 * q + 1, 1),
+                              (uint32_t)__builtin_amdgcn_sbfe(w, 4 * q + 2, 1), (uint32_t)__builtin_amdgcn_sbfe(w, 4 * q + 3, 1));
+      vp[64 * q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  uint32_t T = party ? 0xFFFFFFFFu : 0u;
+  const uint32_t mlast = (c == 3u) ? 0u : 0xFFFFFFFFu;
+  uint32_t lev = 0;
+  for (uint32_t cc = 0; cc < nchunk; ++cc) {
+    __builtin_amdgcn_wave_barrier();
+    if (c == cc) {
+      uint32_t w[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const uint64_t p = min(p0 + j, m - 1);
+        if (XALIGNED)
+          w[j] = bswap32(*reinterpret_cast<const uint32_t*>(xs + p * nbytes + 4 * cc));
+        else
+          w[j] = load_bits32(xs + p * nbytes, cc, nbytes);
+      }
+      transpose32(w);
+#pragma unroll
+      for (int i = 0; i < 32; ++i) xl[(31u - i) * 16u + quad] = w[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t lend = min(32u, nlev - 32u * cc);
+    for (uint32_t b = 0; b < lend; ++b, ++lev) {
+      const uint32_t X = xl[b * 16u + quad];
+      const uint4 cs = cw_s[lev], cv = cw_v[lev];
+      const uint32_t ct = cw_t[lev];
+      uint32_t csw = sel4(cs, c), cvw = sel4(cv, c);
+      uint32_t st[32];
+      // B = AES(~s); v ^= ((~s) ^ (B & ~X)) & M ^ (T & cw.v)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 a = sp[64 * q];
+        st[4 * q] = a.x; st[4 * q + 1] = a.y; st[4 * q + 2] = a.z; st[4 * q + 3] = a.w;
+      }
+      bs_aes256(st, rkl, c, true);
+      asm volatile("" : "+v"(cvw));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 a = sp[64 * q];
+        uint4 vv = vp[64 * q];
+        const uint32_t sa[4] = {a.x, a.y, a.z, a.w};
+        uint32_t va[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * q + e;
+          uint32_t hv = (~sa[e]) ^ (st[i] & ~X);
+          if (i == 24) hv &= mlast;
+          va[e] ^= hv ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)cvw, i, 1));
+        }
+        vp[64 * q] = make_uint4(va[0], va[1], va[2], va[3]);
+      }
+      const uint32_t s00 = sp[0].x;
+      const uint32_t tR = qperm<kQpBcast0>(st[0] ^ ~s00);
+      // A = AES(s); s' = (s ^ (A & ~X)) & M ^ (T & cw.s)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 a = sp[64 * q];
+        st[4 * q] = a.x; st[4 * q + 1] = a.y; st[4 * q + 2] = a.z; st[4 * q + 3] = a.w;
+      }
+      bs_aes256(st, rkl, c, false);
+      const uint32_t tL = qperm<kQpBcast0>(st[0] ^ s00);
+      asm volatile("" : "+v"(csw));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 a = sp[64 * q];
+        const uint32_t sa[4] = {a.x, a.y, a.z, a.w};
+        uint32_t ns[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * q + e;
+          uint32_t hs = sa[e] ^ (st[i] & ~X);
+          if (i == 24) hs &= mlast;
+          ns[e] = hs ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)csw, i, 1));
+        }
+        sp[64 * q] = make_uint4(ns[0], ns[1], ns[2], ns[3]);
+      }
+      const uint32_t ctl = 0u - (ct & 1u), ctr = 0u - ((ct >> 1) & 1u);
+      T = ((X & tR) | (~X & tL)) ^ (T & ((X & ctr) | (~X & ctl)));
+    }
+  }
+  const uint32_t npw = sel4(np1, c);
+  uint32_t y[32];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint4 a = sp[64 * q], vv = vp[64 * q];
+    const uint32_t sa[4] = {a.x, a.y, a.z, a.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 4 * q + e;
+      y[i] = va[e] ^ sa[e] ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)npw, i, 1));
+    }
+  }
+  transpose32(y);
+  uint32_t* y32 = reinterpret_cast<uint32_t*>(ys);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const uint64_t p = p0 + j;
+    if (p < m) y32[p * 4 + c] = y[j];
+  }
+}
+
 // Stand-alone bitsliced eval (single key, N <= 16), one wave per 512-point batch.
 template <bool XALIGNED>
 __global__ __launch_bounds__(256, 3) void k_eval16_bs(const RoundKeys rk, const uint4* __restrict__ cw_s,
@@ -254,14 +382,21 @@ __device__ __forceinline__ uint32_t dequeue_unit(uint32_t* ctr) {
   return __builtin_amdgcn_readfirstlane(u);
 }
 
-template <bool XALIGNED>
-__global__ __launch_bounds__(kHybridWaves * 64) void k_eval16_hybrid(
+// MEM = false: s/v in registers (168 VGPRs, 12 waves per workgroup).
+// MEM = true:  s/v in a per-wave scratch slab (<= 128 VGPRs, 16 waves), n_tt >= 1.
+constexpr uint32_t kSlabUint4 = 16 * 64;  // per-wave slab: 16 KiB
+
+template <bool XALIGNED, bool MEM>
+__global__ __launch_bounds__((MEM ? 16 : kHybridWaves) * 64) void k_eval16_hybrid(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
-    const uint64_t m, const uint32_t n_tt, uint32_t* __restrict__ ctr, uint4* __restrict__ ys) {
+    const uint64_t m, const uint32_t n_tt, uint32_t* __restrict__ ctr, uint4* __restrict__ slabs,
+    uint4* __restrict__ ys) {
+  constexpr int kWaves = MEM ? 16 : kHybridWaves;
+  constexpr int kXlSlots = MEM ? 15 : kHybridWaves;  // LDS budget: 128 KiB tables + 2 KiB per bitsliced wave
   __shared__ uint32_t lds[kLdsWords];
-  __shared__ uint32_t xl_all[kHybridWaves][32 * 16];
+  __shared__ uint32_t xl_all[kXlSlots][32 * 16];
   __shared__ uint32_t rkl[60];
   lds_fill_tables(lds, tab);
   rk_to_lds(rkl, rk);
@@ -280,10 +415,16 @@ __global__ __launch_bounds__(kHybridWaves * 64) void k_eval16_hybrid(
       }
     }
   } else {
-    uint32_t* xl = xl_all[wave];
-    for (uint32_t u = dequeue_unit(ctr); u < nunits; u = dequeue_unit(ctr))
-      bs_eval_batch<XALIGNED>(rkl, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m, (uint64_t)u * kWavePoints, xl,
-                              ys);
+    uint32_t* xl = xl_all[MEM ? wave - n_tt : wave];
+    uint4* slab = slabs + ((uint64_t)blockIdx.x * kWaves + wave) * kSlabUint4;
+    for (uint32_t u = dequeue_unit(ctr); u < nunits; u = dequeue_unit(ctr)) {
+      if (MEM)
+        bs_eval_batch_mem<XALIGNED>(rkl, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m,
+                                    (uint64_t)u * kWavePoints, xl, slab, ys);
+      else
+        bs_eval_batch<XALIGNED>(rkl, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m, (uint64_t)u * kWavePoints,
+                                xl, ys);
+    }
   }
 }
 

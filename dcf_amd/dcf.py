@@ -155,9 +155,10 @@ class Aes256HirosePrg:
         """AES engine for LAMBDA = 16 eval: 0 auto, 1 LDS T-table, 2 VALU bitsliced, 3 hybrid."""
         check(_lib.load().dcf_prg_set_eval_mode(self._h, int(mode)))
 
-    def set_hybrid_split(self, ttable_waves: int) -> None:
-        """Hybrid engine: T-table waves out of 12 per workgroup (rest bitsliced)."""
-        check(_lib.load().dcf_prg_set_hybrid_split(self._h, int(ttable_waves)))
+    def set_hybrid_split(self, ttable_waves: int, slab_variant: int = 1) -> None:
+        """Hybrid engine: T-table waves per workgroup (rest bitsliced); slab_variant 1 = 16-wave
+        workgroups with bitsliced state in scratch slabs, 0 = 12 waves with state in registers."""
+        check(_lib.load().dcf_prg_set_hybrid_split(self._h, int(ttable_waves), int(slab_variant)))
 
     def gen(self, seed: bytes):
         """`Prg::gen` (lib.rs:52-54) for one seed — the GPU PRG kernel, not a CPU path."""

@@ -94,9 +94,12 @@ size_t dcf_prg_lambda(const dcf_prg* prg);
  * test knob only: every engine returns identical bytes. */
 int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 
-/* Hybrid engine: how many of the 12 waves per workgroup run the T-table engine
- * (the rest run the bitsliced engine).  Tuning knob; results are identical. */
-int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves);
+/* Hybrid engine tuning (results are identical for every setting):
+ *   slab_variant 1: 16-wave workgroups, bitsliced s/v state in a scratch slab;
+ *   slab_variant 0: 12-wave workgroups, bitsliced state in registers;
+ *   ttable_waves:  waves per workgroup running the T-table engine (the rest
+ *                  run the bitsliced engine; clamped to [1, 16] / [0, 12]). */
+int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves, int slab_variant);
 
 /* CWB layout helpers (see above). */
 size_t dcf_cwb_bytes(size_t n_bytes, size_t lambda, size_t num_keys);

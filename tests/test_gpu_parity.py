@@ -268,8 +268,8 @@ def test_wide_gen_batch_and_multikey(dcf):
         assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl]))
 
 
-@pytest.mark.parametrize("split", [0, 1, 6, 11, 12])
-def test_hybrid_splits_identical(dcf, split):
+@pytest.mark.parametrize("split,variant", [(0, 0), (6, 0), (12, 0), (1, 1), (8, 1), (15, 1), (16, 1)])
+def test_hybrid_splits_identical(dcf, split, variant):
     """Every T-table/bitsliced wave split of the hybrid engine returns the same bytes."""
     import torch
     rng = np.random.default_rng(split)
@@ -283,7 +283,7 @@ def test_hybrid_splits_identical(dcf, split):
     prg.set_eval_mode(1)
     ref = d.eval_device(False, cwb, s0, xs)
     prg.set_eval_mode(3)
-    prg.set_hybrid_split(split)
+    prg.set_hybrid_split(split, variant)
     got = d.eval_device(False, cwb, s0, xs)
     torch.cuda.synchronize()
     assert torch.equal(ref, got)
