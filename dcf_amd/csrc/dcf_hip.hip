@@ -89,6 +89,7 @@ struct dcf_prg {
   size_t cipher_n = 0;
   std::vector<RoundKeys> rk;  // Aes256::new per key (prg.rs:28-31)
   uint32_t* d_tab = nullptr;  // T0..T3 (4 KiB) on the device
+  uint4* d_km = nullptr;      // bitsliced round-key masks of cipher 0 (15 x 4 x 8 uint4)
   uint8_t* d_ws = nullptr;    // stream-ordered scratch (LAMBDA >= 32 paths)
   size_t ws_bytes = 0;
   uint32_t* d_ctr = nullptr;  // work counter of the hybrid eval kernel
@@ -208,10 +209,18 @@ int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int 
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     p->cus = prop.multiProcessorCount;
+  // Bitsliced key masks: word e of uint4 (16 r + 4 c + q) = -(bit 4q+e of column c of round key r).
+  std::vector<uint32_t> km(15 * 4 * 8 * 4);
+  for (int r = 0; r < 15; r++)
+    for (int c = 0; c < 4; c++)
+      for (int i = 0; i < 32; i++) km[((r * 4 + c) * 8) * 4 + i] = ((p->rk[0].w[4 * r + c] >> i) & 1u) ? ~0u : 0u;
   hipError_t e = hipMalloc(&p->d_tab, sizeof(g_tab));
   if (e == hipSuccess) e = hipMemcpy(p->d_tab, g_tab, sizeof(g_tab), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&p->d_km, km.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(p->d_km, km.data(), km.size() * 4, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     if (p->d_tab) (void)hipFree(p->d_tab);
+    if (p->d_km) (void)hipFree(p->d_km);
     delete p;
     return fail(DCF_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e));
   }
@@ -224,6 +233,7 @@ void dcf_prg_free(dcf_prg* p) {
   {
     DeviceGuard dg(p->device);
     if (p->d_tab) (void)hipFree(p->d_tab);
+    if (p->d_km) (void)hipFree(p->d_km);
     if (p->d_ws) (void)hipFree(p->d_ws);
     if (p->d_ctr) (void)hipFree(p->d_ctr);
     if (p->d_slabs) (void)hipFree(p->d_slabs);
@@ -342,7 +352,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #define DCF_HYB(XA, MEM)                                                                                   \
   hipLaunchKernelGGL((k_eval16_hybrid<XA, MEM>), g, b, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,       \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint32_t)ntt, \
-                     p->d_ctr, slabs, (uint4*)ys)
+                     p->d_ctr, slabs, p->d_km, (uint4*)ys)
     const bool xa = n_bytes % 4 == 0;
     if (xa && mem) DCF_HYB(true, true);
     else if (xa) DCF_HYB(true, false);
@@ -356,10 +366,10 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     const uint64_t cap = (uint64_t)p->cus * 8;
     if (blocks > cap) blocks = cap;
     if (n_bytes % 4 == 0)
-      hipLaunchKernelGGL(k_eval16_bs<true>, dim3((unsigned)blocks), dim3(256), 0, st, p->rk[0], cws, cwv, cwt, np1,
+      hipLaunchKernelGGL(k_eval16_bs<true>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
                          (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
     else
-      hipLaunchKernelGGL(k_eval16_bs<false>, dim3((unsigned)blocks), dim3(256), 0, st, p->rk[0], cws, cwv, cwt, np1,
+      hipLaunchKernelGGL(k_eval16_bs<false>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
                          (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
   } else if (num_keys == 1)
     hipLaunchKernelGGL(k_eval16<0>, grid, block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,

@@ -21,7 +21,9 @@ constexpr uint32_t kWavePoints = 512;  // points per wave (16 quads)
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+  // mov_dpp (no `old` operand): quad_perm reads a valid lane for every lane, so no
+  // v_mov of a fallback value is needed before each DPP move.
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
 // DPP quad_perm encodings: lane c reads lane sel[c]; ctrl = sel0 | sel1<<2 | sel2<<4 | sel3<<6
 constexpr int kQpRot1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // c <- c+1
@@ -41,22 +43,6 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
       a[k] ^= t << j;
     }
   }
-}
-
-// Round keys as LDS words rkl[4r + c]: lane c reads its column word of round r
-// (a wave-uniform-index select from kernel-argument SGPRs becomes divergent control flow).
-__device__ __forceinline__ void rk_to_lds(uint32_t* rkl, const RoundKeys& rk) {
-  for (int i = threadIdx.x; i < 60; i += blockDim.x) rkl[i] = rk.w[i];
-  __syncthreads();
-}
-
-// st ^= key column (bit 8r+k of kw -> all-ones mask); invert = 1 XORs ~key.
-__device__ __forceinline__ void bs_ark(uint32_t (&st)[32], uint32_t kw) {
-  // Opaque to the optimiser: otherwise LICM hoists all 15 x 32 key masks out of
-  // the level loop and the kernel needs ~500 registers.
-  asm volatile("" : "+v"(kw));
-#pragma unroll
-  for (int i = 0; i < 32; ++i) st[i] ^= (uint32_t)__builtin_amdgcn_sbfe((int)kw, i, 1);
 }
 
 __device__ __forceinline__ void bs_subbytes(uint32_t (&st)[32]) {
@@ -80,41 +66,68 @@ __device__ __forceinline__ void bs_shiftrows(uint32_t (&st)[32]) {
   }
 }
 
-// MixColumns on this lane's column: out_r = xtime(a_r ^ a_{r+1}) ^ T ^ a_r, T = a0^a1^a2^a3.
-__device__ __forceinline__ void bs_mixcolumns(uint32_t (&st)[32]) {
+#define DCF_B3(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))
+// bitop3 immediates (imm = f(src0 = 0xF0, src1 = 0xCC, src2 = 0xAA)):
+constexpr uint32_t kXor3 = 0x96;  // a ^ b ^ c
+
+// Round-key masks of cipher 0 for the bitsliced engine: uint4 km[32 r + 8 c + q]
+// holds, as four all-ones/zero words, bits 4q..4q+3 of column c of round key r
+// (rounds 0..14; 7.5 KiB, built on the host from the key schedule, L1-resident).
+__device__ __forceinline__ void bs_ark_tab(uint32_t (&st)[32], const uint4* __restrict__ km, bool inv) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint4 k = km[q];
+    const uint32_t kk[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) st[4 * q + e] ^= inv ? ~kk[e] : kk[e];
+  }
+}
+
+// MixColumns + AddRoundKey on this lane's column:
+//   out_r = xtime(a_r ^ a_{r+1}) ^ (T ^ a_r ^ key_r),  T = a0 ^ a1 ^ a2 ^ a3.
+__device__ __forceinline__ void bs_mixcolumns_ark(uint32_t (&st)[32], const uint4* __restrict__ km) {
   uint32_t T[8], a0[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     a0[k] = st[k];
-    T[k] = st[k] ^ st[8 + k] ^ st[16 + k] ^ st[24 + k];
+    T[k] = DCF_B3(st[k], st[8 + k], st[16 + k], kXor3) ^ st[24 + k];
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
+    const uint4 k0 = km[2 * r], k1 = km[2 * r + 1];
+    const uint32_t key[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
     uint32_t d[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = st[8 * r + k] ^ ((r == 3) ? a0[k] : st[8 * (r + 1) + k]);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const uint32_t xt = (k == 0) ? d[7] : ((k == 1 || k == 3 || k == 4) ? (d[k - 1] ^ d[7]) : d[k - 1]);
-      st[8 * r + k] = xt ^ T[k] ^ st[8 * r + k];
+      const uint32_t e = DCF_B3(T[k], st[8 * r + k], key[k], kXor3);
+      if (k == 0)
+        st[8 * r + k] = d[7] ^ e;
+      else if (k == 1 || k == 3 || k == 4)
+        st[8 * r + k] = DCF_B3(d[k - 1], d[7], e, kXor3);
+      else
+        st[8 * r + k] = d[k - 1] ^ e;
     }
   }
 }
 
 // AES-256 encryption of 32 blocks (quad-sliced).  `inv_in`: encrypt ~st instead.
-__device__ __forceinline__ void bs_aes256(uint32_t (&st)[32], const uint32_t* rkl, uint32_t c, bool inv_in) {
-  bs_ark(st, inv_in ? ~rkl[c] : rkl[c]);
+// km: this lane's column of the round-key masks (km + 8 c; round r at + 32 r).
+__device__ __forceinline__ void bs_aes256(uint32_t (&st)[32], const uint4* __restrict__ km, bool inv_in) {
+  bs_ark_tab(st, km, inv_in);
 #pragma unroll 1
   for (int r = 1; r < 14; ++r) {
     bs_subbytes(st);
     bs_shiftrows(st);
-    bs_mixcolumns(st);
-    bs_ark(st, rkl[4 * r + c]);
+    bs_mixcolumns_ark(st, km + 32 * r);
   }
   bs_subbytes(st);
   bs_shiftrows(st);
-  bs_ark(st, rkl[56 + c]);
+  bs_ark_tab(st, km + 32 * 14, false);
 }
+
+#undef DCF_B3
 
 // Broadcast a uniform 16-byte value's column c into bitsliced registers.
 __device__ __forceinline__ void bs_splat(uint32_t (&st)[32], uint32_t w) {
@@ -129,7 +142,7 @@ __device__ __forceinline__ uint32_t sel4(uint4 v, uint32_t c) {
 // One wave's batch of 512 points (32 per quad), party `party`, single key.
 // xl: this wave's 2 KiB of LDS holding 32 levels of transposed x, [level][quad].
 template <bool XALIGNED>
-__device__ __forceinline__ void bs_eval_batch(const uint32_t* rkl, const uint4* __restrict__ cw_s,
+__device__ __forceinline__ void bs_eval_batch(const uint4* __restrict__ km, const uint4* __restrict__ cw_s,
                                               const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
                                               const uint4 np1, const uint4 s0v, const uint32_t party,
                                               const uint8_t* __restrict__ xs, const uint32_t nbytes,
@@ -138,6 +151,7 @@ __device__ __forceinline__ void bs_eval_batch(const uint32_t* rkl, const uint4* 
   const uint32_t lane = threadIdx.x & 63u, c = lane & 3u, quad = lane >> 2;
   const uint64_t p0 = p_base + (uint64_t)quad * kBsPoints;
   const uint32_t nlev = 8u * nbytes, nchunk = (nbytes + 3u) >> 2;
+  const uint4* __restrict__ kmc = km + 8 * c;
   uint32_t s[32], v[32];
   bs_splat(s, sel4(s0v, c));
 #pragma unroll
@@ -174,7 +188,7 @@ __device__ __forceinline__ void bs_eval_batch(const uint32_t* rkl, const uint4* 
       // B = AES(~s): v ^= ((~s) ^ (B & ~X)) & M ^ (T & cw.v)   (lib.rs:182/186)
 #pragma unroll
       for (int i = 0; i < 32; ++i) st[i] = s[i];
-      bs_aes256(st, rkl, c, true);
+      bs_aes256(st, kmc, true);
       const uint32_t tR = qperm<kQpBcast0>(st[0] ^ ~s[0]);  // lsb(B ^ ~s)[0] of each point
       uint32_t cvo = cvw;
       asm volatile("" : "+v"(cvo));  // keep the 32 CW masks from being materialised before the AES
@@ -187,7 +201,7 @@ __device__ __forceinline__ void bs_eval_batch(const uint32_t* rkl, const uint4* 
       // A = AES(s): s' = (s ^ (A & ~X)) & M ^ (T & cw.s)   (lib.rs:177-178, 183/187)
 #pragma unroll
       for (int i = 0; i < 32; ++i) st[i] = s[i];
-      bs_aes256(st, rkl, c, false);
+      bs_aes256(st, kmc, false);
       const uint32_t tL = qperm<kQpBcast0>(st[0] ^ s[0]);
       uint32_t cso = csw;
       asm volatile("" : "+v"(cso));
@@ -222,7 +236,7 @@ __device__ __forceinline__ void bs_eval_batch(const uint32_t* rkl, const uint4* 
 // pass (~14.7K VALU ops per level per lane), so the slab traffic is small and
 // L1/L2-resident.
 template <bool XALIGNED>
-__device__ __forceinline__ void bs_eval_batch_mem(const uint32_t* rkl, const uint4* __restrict__ cw_s,
+__device__ __forceinline__ void bs_eval_batch_mem(const uint4* __restrict__ km, const uint4* __restrict__ cw_s,
                                                   const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
                                                   const uint4 np1, const uint4 s0v, const uint32_t party,
                                                   const uint8_t* __restrict__ xs, const uint32_t nbytes,
@@ -231,6 +245,7 @@ __device__ __forceinline__ void bs_eval_batch_mem(const uint32_t* rkl, const uin
   const uint32_t lane = threadIdx.x & 63u, c = lane & 3u, quad = lane >> 2;
   const uint64_t p0 = p_base + (uint64_t)quad * kBsPoints;
   const uint32_t nlev = 8u * nbytes, nchunk = (nbytes + 3u) >> 2;
+  const uint4* __restrict__ kmc = km + 8 * c;
   uint4* __restrict__ sp = slab + lane;           // s quad q at sp[64 q]
   uint4* __restrict__ vp = slab + 8 * 64 + lane;  // v quad q at vp[64 q]
   {
@@ -276,7 +291,7 @@ __device__ __forceinline__ void bs_eval_batch_mem(const uint32_t* rkl, const uin
         const uint4 a = sp[64 * q];
         st[4 * q] = a.x; st[4 * q + 1] = a.y; st[4 * q + 2] = a.z; st[4 * q + 3] = a.w;
       }
-      bs_aes256(st, rkl, c, true);
+      bs_aes256(st, kmc, true);
       asm volatile("" : "+v"(cvw));
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -301,7 +316,7 @@ __device__ __forceinline__ void bs_eval_batch_mem(const uint32_t* rkl, const uin
         const uint4 a = sp[64 * q];
         st[4 * q] = a.x; st[4 * q + 1] = a.y; st[4 * q + 2] = a.z; st[4 * q + 3] = a.w;
       }
-      bs_aes256(st, rkl, c, false);
+      bs_aes256(st, kmc, false);
       const uint32_t tL = qperm<kQpBcast0>(st[0] ^ s00);
       asm volatile("" : "+v"(csw));
 #pragma unroll
@@ -345,20 +360,18 @@ __device__ __forceinline__ void bs_eval_batch_mem(const uint32_t* rkl, const uin
 
 // Stand-alone bitsliced eval (single key, N <= 16), one wave per 512-point batch.
 template <bool XALIGNED>
-__global__ __launch_bounds__(256, 3) void k_eval16_bs(const RoundKeys rk, const uint4* __restrict__ cw_s,
+__global__ __launch_bounds__(256, 3) void k_eval16_bs(const uint4* __restrict__ km, const uint4* __restrict__ cw_s,
                                                    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
                                                    const uint4* __restrict__ cw_np1, const uint4* __restrict__ s0,
                                                    const uint32_t party, const uint8_t* __restrict__ xs,
                                                    const uint32_t nbytes, const uint64_t m, uint4* __restrict__ ys) {
   __shared__ uint32_t xl_all[4][32 * 16];
-  __shared__ uint32_t rkl[60];
-  rk_to_lds(rkl, rk);
   const uint32_t wave = threadIdx.x >> 6;
   const uint64_t gwave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   const uint4 np1 = cw_np1[0], s0v = s0[0];
   for (uint64_t b = gwave; b * kWavePoints < m; b += nwaves)
-    bs_eval_batch<XALIGNED>(rkl, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m, b * kWavePoints, xl_all[wave],
+    bs_eval_batch<XALIGNED>(km, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m, b * kWavePoints, xl_all[wave],
                             ys);
 }
 
@@ -392,14 +405,12 @@ __global__ __launch_bounds__((MEM ? 16 : kHybridWaves) * 64) void k_eval16_hybri
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t m, const uint32_t n_tt, uint32_t* __restrict__ ctr, uint4* __restrict__ slabs,
-    uint4* __restrict__ ys) {
+    const uint4* __restrict__ km, uint4* __restrict__ ys) {
   constexpr int kWaves = MEM ? 16 : kHybridWaves;
   constexpr int kXlSlots = MEM ? 15 : kHybridWaves;  // LDS budget: 128 KiB tables + 2 KiB per bitsliced wave
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint32_t xl_all[kXlSlots][32 * 16];
-  __shared__ uint32_t rkl[60];
   lds_fill_tables(lds, tab);
-  rk_to_lds(rkl, rk);
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint64_t nunits = (m + kWavePoints - 1) / kWavePoints;
   const uint4 np1 = cw_np1[0], s0v = s0[0];
@@ -419,10 +430,10 @@ __global__ __launch_bounds__((MEM ? 16 : kHybridWaves) * 64) void k_eval16_hybri
     uint4* slab = slabs + ((uint64_t)blockIdx.x * kWaves + wave) * kSlabUint4;
     for (uint32_t u = dequeue_unit(ctr); u < nunits; u = dequeue_unit(ctr)) {
       if (MEM)
-        bs_eval_batch_mem<XALIGNED>(rkl, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m,
+        bs_eval_batch_mem<XALIGNED>(km, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m,
                                     (uint64_t)u * kWavePoints, xl, slab, ys);
       else
-        bs_eval_batch<XALIGNED>(rkl, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m, (uint64_t)u * kWavePoints,
+        bs_eval_batch<XALIGNED>(km, cw_s, cw_v, cw_t, np1, s0v, party, xs, nbytes, m, (uint64_t)u * kWavePoints,
                                 xl, ys);
     }
   }
