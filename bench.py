@@ -33,12 +33,34 @@ from dcf_amd.dist import broadcast_key, weak_slice  # noqa: E402
 
 METRIC = "DCF evals/sec (node) at 128-bit input, λ=16B; AES blocks/s vs INT roofline"
 
-# ---- roofline constants (MI355X_MICROARCH.md) ----
+# ---- roofline constants (MI355X_MICROARCH.md; op counts from the gfx950 disassembly) ----
 CUS, CLK_HZ = 256, 2.4e9
-LDS_B32_LOOKUPS_PER_CLK_CU = 32          # ds_read_b32: 64 lanes / 2 LDS cycles (§LDS table)
-AES256_LOOKUPS_PER_BLOCK = 14 * 16       # T-table AES-256: 16 table reads per round
-PEAK_LDS_LOOKUPS = CUS * LDS_B32_LOOKUPS_PER_CLK_CU * CLK_HZ
-PEAK_AES_BLOCKS = PEAK_LDS_LOOKUPS / AES256_LOOKUPS_PER_BLOCK  # ~87.8 G blocks/s per GPU
+LDS_LOOKUPS = CUS * 32 * CLK_HZ      # ds_read_b32: 64 lanes per 2 LDS cycles per CU (§LDS table)
+VALU_OPS = CUS * 128 * CLK_HZ        # 4 SIMD-32 per CU, wave64 op every 2 cycles per SIMD
+TT_LDS_PER_BLOCK = 14 * 16           # T-table AES-256: 16 lookups per round
+TT_VALU_PER_BLOCK = 370              # 1 v_perm per lookup + 2 v_bitop3 per column + DCF share
+BS_VALU_PER_BLOCK = 800              # bitsliced: 453 VALU per lane-round / 8 blocks per lane, + last round, ARK, DCF
+PEAK_TT_BLOCKS = LDS_LOOKUPS / TT_LDS_PER_BLOCK  # ~87.8 G blocks/s: T-table alone is LDS-bound
+
+
+def hybrid_peak() -> float:
+    """Best blocks/s with both engines on every CU: the T-table engine takes the whole
+    LDS issue rate, the bitsliced engine the VALU it leaves (a 2-resource LP)."""
+    b_tt = PEAK_TT_BLOCKS
+    valu_left = VALU_OPS - b_tt * TT_VALU_PER_BLOCK
+    return b_tt + max(0.0, valu_left) / BS_VALU_PER_BLOCK
+
+
+ENGINE = {0: "hybrid", 1: "ttable", 2: "bitsliced", 3: "hybrid"}
+KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16<0>", "bitsliced": "k_eval16_bs"}
+
+
+def engine_peak(engine: str) -> float:
+    if engine == "ttable":
+        return PEAK_TT_BLOCKS
+    if engine == "bitsliced":
+        return VALU_OPS / BS_VALU_PER_BLOCK
+    return hybrid_peak()
 
 
 def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int):
@@ -179,6 +201,9 @@ def run_eval(args, world, rank):
     value = total_evals / wall
     bpe = blocks_per_eval(nb, lam)
     per_gpu_blocks = m * bpe / kern_s
+    engine = ENGINE[args.eval_mode] if nb <= 16 else "ttable"
+    kernel = KERNEL[engine]
+    peak = engine_peak(engine)
     out = {
         "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
@@ -189,14 +214,17 @@ def run_eval(args, world, rank):
                    "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
         "aes_blocks_per_s": value * bpe,
         "roofline": {
-            "bound": "lds", "kernel": "k_eval16<0>",
-            "achieved": per_gpu_blocks / 1e9, "peak": PEAK_AES_BLOCKS / 1e9, "unit": "G AES-256 blocks/s",
-            "frac": per_gpu_blocks / PEAK_AES_BLOCKS, "traffic": pmc_traffic("k_eval16<0>", m, nb, lam),
-            "algorithmic_bytes": m * (nb + lam),
-            "kernel_ms": kern_s * 1e3,
-            "note": "blocks = reference count (2 per level, 128 levels); peak = 256 CU x 32 ds_read_b32 "
-                    "lookups/clk x 2.4 GHz / 224 lookups per T-table AES-256 block; per GPU",
+            "bound": "lds" if engine == "ttable" else ("valu" if engine == "bitsliced" else "lds+valu"),
+            "kernel": kernel, "engine": engine,
+            "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-256 blocks/s",
+            "frac": per_gpu_blocks / peak, "traffic": pmc_traffic(kernel, m, nb, lam),
+            "algorithmic_bytes": m * (nb + lam), "kernel_ms": kern_s * 1e3,
             "hbm_GBps": m * (nb + lam) / kern_s / 1e9,
+            "ttable_only_peak": PEAK_TT_BLOCKS / 1e9,
+            "note": "blocks = reference count (2 AES-256 per level, 8N levels); peak per GPU at 2.4 GHz: "
+                    "T-table engine LDS-bound (32 ds_read_b32 lookups/clk/CU, 224 per block), bitsliced "
+                    "engine VALU-bound (128 lane-ops/clk/CU, ~800 per block); hybrid = LDS-saturating "
+                    "T-table + bitsliced on the VALU left over (DESIGN.md §4)",
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -96,7 +96,7 @@ struct dcf_prg {
   void* d_slabs = nullptr;    // per-wave s/v slabs of the hybrid kernel (MEM variant)
   size_t slab_bytes = 0;
   int eval_mode = DCF_EVAL_AUTO;
-  int hybrid_tt_waves = 8;    // T-table waves per hybrid workgroup
+  int hybrid_tt_waves = 13;   // T-table waves per hybrid workgroup (r01 sweep: 13 of 16 best)
   int hybrid_mem = 1;         // 1: 16-wave workgroups with s/v slabs; 0: 12 waves, s/v in registers
 };
 

@@ -83,10 +83,13 @@ def pmc_traffic(d, kernel_prefix="k_eval16<0>"):
 
 
 if __name__ == "__main__":
+    # prof_summary.py <run dir> [<pmc_traffic.json out> <kernel prefix>]
     main(sys.argv[1])
     if len(sys.argv) > 2:
         import json
-        t = pmc_traffic(sys.argv[1])
+        prefix = sys.argv[3] if len(sys.argv) > 3 else "k_eval16<0>"
+        t = pmc_traffic(sys.argv[1], prefix)
         t["source"] = sys.argv[1]
+        t["kernel"] = prefix
         with open(sys.argv[2], "w") as f:
             json.dump(t, f, indent=1)
