@@ -29,7 +29,7 @@ EXPORTS = [
     "dcf_version", "dcf_last_error", "dcf_hirose_prg_new", "dcf_prg_free", "dcf_prg_lambda", "dcf_prg_set_eval_mode",
     "dcf_prg_set_hybrid_split",
     "dcf_cwb_bytes", "dcf_cwb_np1_offset", "dcf_gen", "dcf_eval", "dcf_prg_gen",
-    "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device",
+    "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device", "dcf_eval_full_domain_device",
 ]
 
 
@@ -75,6 +75,7 @@ def load(path: str = LIB_PATH):
         "dcf_gen_batch_device": ([vp, sz, sz, u8p, u8p, u8p, u8p, i, u8p, vp], i),
         "dcf_eval_device": ([vp, sz, i, u8p, u8p, u8p, sz, u8p, vp], i),
         "dcf_eval_multikey_device": ([vp, sz, sz, sz, i, u8p, u8p, u8p, u8p, vp], i),
+        "dcf_eval_full_domain_device": ([vp, sz, i, u8p, u8p, u8p, vp], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

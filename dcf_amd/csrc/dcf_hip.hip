@@ -23,6 +23,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dcf_hip.h"
@@ -396,6 +397,59 @@ int dcf_eval_multikey_device(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t
                              const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys,
                              void* stream) {
   return eval_launch(p, n_bytes, num_keys, points_per_key, party, cwb, s0s, xs, ys, stream);
+}
+
+int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uint8_t* cwb, const uint8_t* s0,
+                                uint8_t* ys, void* stream) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
+  if (n_bytes > 4) return fail(DCF_ERR_UNSUPPORTED, "full-domain eval: N <= 4 (2^32 outputs)");
+  if (party != 0 && party != 1) return fail(DCF_ERR_ARG, "party must be 0 or 1");
+  if (!cwb || !s0 || !ys) return fail(DCF_ERR_ARG, "null buffer");
+  DeviceGuard dg(p->device);
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t nlev = (uint32_t)(8 * n_bytes);
+  const uint64_t npts = 1ull << nlev;
+  const size_t lam = p->lambda;
+  if (lam != 16) {  // no tree sharing at LAMBDA >= 32: materialise the domain and run eval
+    DevBuf xs;  // eval_wide owns the workspace, so the points get their own buffer
+    HIP_TRY(xs.alloc(npts * n_bytes));
+    hipLaunchKernelGGL(k_domain_points, dim3(1024), dim3(256), 0, st, (uint32_t)n_bytes, npts, (uint8_t*)xs.p);
+    HIP_TRY(hipGetLastError());
+    int rc = eval_wide(p, n_bytes, 1, 0, party, cwb, s0, (const uint8_t*)xs.p, npts, ys, st);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(st));  // xs is freed on return
+    return DCF_OK;
+  }
+  // Two ping-pong node buffers of 2^(n-1) nodes: s (16 B), v (16 B), t (1 B).
+  const uint64_t maxnodes = npts / 2;
+  const size_t nodeb = 33;
+  int rc = ensure_ws(p, 2 * maxnodes * nodeb + 64, st);
+  if (rc) return rc;
+  uint8_t* w = p->d_ws;
+  uint4* s_a = (uint4*)w;
+  uint4* v_a = s_a + maxnodes;
+  uint8_t* t_a = (uint8_t*)(v_a + maxnodes);
+  uint4* s_b = (uint4*)(w + maxnodes * nodeb + 16 - (maxnodes * nodeb) % 16);
+  uint4* v_b = s_b + maxnodes;
+  uint8_t* t_b = (uint8_t*)(v_b + maxnodes);
+  const size_t n = 8 * n_bytes;
+  const uint4* cws = (const uint4*)cwb;
+  const uint4* cwv = (const uint4*)(cwb + n * lam);
+  const uint8_t* cwt = cwb + 2 * n * lam;
+  const uint4* np1 = (const uint4*)(cwb + dcf_cwb_np1_offset(n_bytes, lam, 1));
+  hipLaunchKernelGGL(k_fd_root16, dim3(1), dim3(64), 0, st, (const uint4*)s0, (uint32_t)party, s_a, v_a, t_a);
+  HIP_TRY(hipGetLastError());
+  for (uint32_t lev = 0; lev < nlev; ++lev) {
+    const uint64_t parents = 1ull << lev;
+    hipLaunchKernelGGL(k_fd_level16, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b, (uint4*)ys);
+    HIP_TRY(hipGetLastError());
+    std::swap(s_a, s_b);
+    std::swap(v_a, v_b);
+    std::swap(t_a, t_b);
+  }
+  return DCF_OK;
 }
 
 int dcf_gen(dcf_prg* p, size_t n_bytes, const uint8_t* alpha, const uint8_t* beta, const uint8_t* s0_0,

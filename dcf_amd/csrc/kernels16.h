@@ -229,3 +229,94 @@ __global__ __launch_bounds__(kBlock, 1) void k_prg16(const uint32_t* __restrict_
 }
 
 }  // namespace
+
+namespace {
+
+// ------------------------------------------------------------------------
+// Full-domain eval at LAMBDA = 16: y for every x in [0, 2^n),
+// n = 8N, by breadth-first tree expansion.  One lane per parent node per
+// level: one PRG call (A, B) yields BOTH children, so the whole domain costs
+// 2 AES blocks per leaf instead of 2n per point.  Node state (s, v, t) lives in
+// SoA buffers indexed by the big-endian x prefix; the last level writes y.
+// Child rules are lib.rs:176-189 with x-bit 0 (left) / 1 (right).
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
+    const uint32_t lev, const uint32_t nlev, const uint64_t nparents, const uint4* __restrict__ s_in,
+    const uint4* __restrict__ v_in, const uint8_t* __restrict__ t_in, uint4* __restrict__ s_out,
+    uint4* __restrict__ v_out, uint8_t* __restrict__ t_out, uint4* __restrict__ ys) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint4 cs = cw_s[lev], cv = cw_v[lev], np = cw_np1[0];
+  const uint32_t ct = cw_t[lev];
+  const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+  const uint32_t npw[4] = {np.x, np.y, np.z, np.w};
+  const bool last = lev + 1 == nlev;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < nparents; base += stride) {
+    const uint64_t j = base + (threadIdx.x & 63u);
+    const bool live = j < nparents;
+    const uint64_t jj = live ? j : nparents - 1;
+    const uint4 sv = s_in[jj], vv = v_in[jj];
+    const uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w}, v[4] = {vv.x, vv.y, vv.z, vv.w};
+    const uint32_t t = t_in[jj];
+    uint32_t st[2][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      st[0][k] = s[k];
+      st[1][k] = ~s[k];
+    }
+    aes256_tt<2>(st, rk, lds, lc);  // A, B
+    const uint32_t tm = 0u - t;
+    uint32_t sl[4], vl[4], sr[4], vr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t msk = (k == 3) ? kMaskLast : 0xFFFFFFFFu;
+      sl[k] = ((st[0][k] ^ s[k]) & msk) ^ (tm & csw[k]);
+      sr[k] = (s[k] & msk) ^ (tm & csw[k]);
+      vl[k] = v[k] ^ ((st[1][k] ^ ~s[k]) & msk) ^ (tm & cvw[k]);
+      vr[k] = v[k] ^ ((~s[k]) & msk) ^ (tm & cvw[k]);
+    }
+    const uint32_t tl = ((st[0][0] ^ s[0]) & 1u) ^ (t & ct & 1u);
+    const uint32_t tr = ((st[1][0] ^ ~s[0]) & 1u) ^ (t & (ct >> 1) & 1u);
+    if (!live) continue;
+    if (last) {  // y = v ^ s ^ t * cw_np1 (lib.rs:192)
+      const uint32_t ml = 0u - tl, mr = 0u - tr;
+      ys[2 * j] = make_uint4(vl[0] ^ sl[0] ^ (ml & npw[0]), vl[1] ^ sl[1] ^ (ml & npw[1]),
+                             vl[2] ^ sl[2] ^ (ml & npw[2]), vl[3] ^ sl[3] ^ (ml & npw[3]));
+      ys[2 * j + 1] = make_uint4(vr[0] ^ sr[0] ^ (mr & npw[0]), vr[1] ^ sr[1] ^ (mr & npw[1]),
+                                 vr[2] ^ sr[2] ^ (mr & npw[2]), vr[3] ^ sr[3] ^ (mr & npw[3]));
+    } else {
+      s_out[2 * j] = make_uint4(sl[0], sl[1], sl[2], sl[3]);
+      s_out[2 * j + 1] = make_uint4(sr[0], sr[1], sr[2], sr[3]);
+      v_out[2 * j] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+      v_out[2 * j + 1] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
+      t_out[2 * j] = (uint8_t)tl;
+      t_out[2 * j + 1] = (uint8_t)tr;
+    }
+  }
+}
+
+// Root node for full-domain eval: s = s0 (k.s0s[0]), v = 0, t = party.
+__global__ void k_fd_root16(const uint4* __restrict__ s0, const uint32_t party, uint4* __restrict__ s,
+                            uint4* __restrict__ v, uint8_t* __restrict__ t) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    s[0] = s0[0];
+    v[0] = make_uint4(0u, 0u, 0u, 0u);
+    t[0] = (uint8_t)party;
+  }
+}
+
+// All 2^n points of an n-bit domain as big-endian N-byte strings (LAMBDA >= 32 full domain).
+__global__ void k_domain_points(const uint32_t nbytes, const uint64_t count, uint8_t* __restrict__ xs) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    for (uint32_t b = 0; b < nbytes; ++b) {
+      const uint32_t sh = 8u * (nbytes - 1u - b);
+      xs[i * nbytes + b] = sh < 64 ? (uint8_t)(i >> sh) : 0u;
+    }
+}
+
+}  // namespace

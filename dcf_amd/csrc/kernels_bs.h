@@ -229,12 +229,11 @@ __device__ __forceinline__ void bs_eval_batch(const uint4* __restrict__ km, cons
   }
 }
 
-// Same batch with the 32-register s and v of each lane kept in a per-wave
-// scratch slab (16 KiB: [s q0..q7 | v q0..q7][64 lanes] uint4, coalesced)
-// instead of registers: the lane then needs ~100 VGPRs, so 4 waves fit per
-// SIMD and hide the S-box's dependency chains.  s/v are touched once per AES
-// pass (~14.7K VALU ops per level per lane), so the slab traffic is small and
-// L1/L2-resident.
+// Same batch with the 32-register v accumulator of each lane kept in a per-wave
+// scratch slab ([v q0..q7][64 lanes] uint4, coalesced 1 KiB accesses) instead
+// of registers, so the lane fits in 128 VGPRs and 4 waves share each SIMD to
+// hide the S-box's dependency chains.  v is read and written once per level
+// (256 B per lane against ~12.7K VALU ops).
 template <bool XALIGNED>
 __device__ __forceinline__ void bs_eval_batch_mem(const uint4* __restrict__ km, const uint4* __restrict__ cw_s,
                                                   const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
@@ -246,17 +245,11 @@ __device__ __forceinline__ void bs_eval_batch_mem(const uint4* __restrict__ km, 
   const uint64_t p0 = p_base + (uint64_t)quad * kBsPoints;
   const uint32_t nlev = 8u * nbytes, nchunk = (nbytes + 3u) >> 2;
   const uint4* __restrict__ kmc = km + 8 * c;
-  uint4* __restrict__ sp = slab + lane;           // s quad q at sp[64 q]
-  uint4* __restrict__ vp = slab + 8 * 64 + lane;  // v quad q at vp[64 q]
-  {
-    const int w = (int)sel4(s0v, c);
+  uint4* __restrict__ vp = slab + lane;  // v quad q at vp[64 q]
+  uint32_t s[32];
+  bs_splat(s, sel4(s0v, c));
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      sp[64 * q] = make_uint4((uint32_t)__builtin_amdgcn_sbfe(w, 4 * q, 1), (uint32_t)__builtin_amdgcn_sbfe(w, 4 * q + 1, 1),
-                              (uint32_t)__builtin_amdgcn_sbfe(w, 4 * q + 2, 1), (uint32_t)__builtin_amdgcn_sbfe(w, 4 * q + 3, 1));
-      vp[64 * q] = make_uint4(0u, 0u, 0u, 0u);
-    }
-  }
+  for (int q = 0; q < 8; ++q) vp[64 * q] = make_uint4(0u, 0u, 0u, 0u);
   uint32_t T = party ? 0xFFFFFFFFu : 0u;
   const uint32_t mlast = (c == 3u) ? 0u : 0xFFFFFFFFu;
   uint32_t lev = 0;
@@ -285,53 +278,36 @@ __device__ __forceinline__ void bs_eval_batch_mem(const uint4* __restrict__ km, 
       const uint32_t ct = cw_t[lev];
       uint32_t csw = sel4(cs, c), cvw = sel4(cv, c);
       uint32_t st[32];
-      // B = AES(~s); v ^= ((~s) ^ (B & ~X)) & M ^ (T & cw.v)
+      // B = AES(~s); v ^= ((~s) ^ (B & ~X)) & M ^ (T & cw.v)   (v lives in the slab)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint4 a = sp[64 * q];
-        st[4 * q] = a.x; st[4 * q + 1] = a.y; st[4 * q + 2] = a.z; st[4 * q + 3] = a.w;
-      }
+      for (int i = 0; i < 32; ++i) st[i] = s[i];
       bs_aes256(st, kmc, true);
       asm volatile("" : "+v"(cvw));
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const uint4 a = sp[64 * q];
         uint4 vv = vp[64 * q];
-        const uint32_t sa[4] = {a.x, a.y, a.z, a.w};
         uint32_t va[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * q + e;
-          uint32_t hv = (~sa[e]) ^ (st[i] & ~X);
+          uint32_t hv = (~s[i]) ^ (st[i] & ~X);
           if (i == 24) hv &= mlast;
           va[e] ^= hv ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)cvw, i, 1));
         }
         vp[64 * q] = make_uint4(va[0], va[1], va[2], va[3]);
       }
-      const uint32_t s00 = sp[0].x;
-      const uint32_t tR = qperm<kQpBcast0>(st[0] ^ ~s00);
+      const uint32_t tR = qperm<kQpBcast0>(st[0] ^ ~s[0]);
       // A = AES(s); s' = (s ^ (A & ~X)) & M ^ (T & cw.s)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint4 a = sp[64 * q];
-        st[4 * q] = a.x; st[4 * q + 1] = a.y; st[4 * q + 2] = a.z; st[4 * q + 3] = a.w;
-      }
+      for (int i = 0; i < 32; ++i) st[i] = s[i];
       bs_aes256(st, kmc, false);
-      const uint32_t tL = qperm<kQpBcast0>(st[0] ^ s00);
+      const uint32_t tL = qperm<kQpBcast0>(st[0] ^ s[0]);
       asm volatile("" : "+v"(csw));
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint4 a = sp[64 * q];
-        const uint32_t sa[4] = {a.x, a.y, a.z, a.w};
-        uint32_t ns[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * q + e;
-          uint32_t hs = sa[e] ^ (st[i] & ~X);
-          if (i == 24) hs &= mlast;
-          ns[e] = hs ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)csw, i, 1));
-        }
-        sp[64 * q] = make_uint4(ns[0], ns[1], ns[2], ns[3]);
+      for (int i = 0; i < 32; ++i) {
+        uint32_t hs = s[i] ^ (st[i] & ~X);
+        if (i == 24) hs &= mlast;
+        s[i] = hs ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)csw, i, 1));
       }
       const uint32_t ctl = 0u - (ct & 1u), ctr = 0u - ((ct >> 1) & 1u);
       T = ((X & tR) | (~X & tL)) ^ (T & ((X & ctr) | (~X & ctl)));
@@ -341,12 +317,12 @@ __device__ __forceinline__ void bs_eval_batch_mem(const uint4* __restrict__ km, 
   uint32_t y[32];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const uint4 a = sp[64 * q], vv = vp[64 * q];
-    const uint32_t sa[4] = {a.x, a.y, a.z, a.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+    const uint4 vv = vp[64 * q];
+    const uint32_t va[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int i = 4 * q + e;
-      y[i] = va[e] ^ sa[e] ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)npw, i, 1));
+      y[i] = va[e] ^ s[i] ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)npw, i, 1));
     }
   }
   transpose32(y);
@@ -397,7 +373,7 @@ __device__ __forceinline__ uint32_t dequeue_unit(uint32_t* ctr) {
 
 // MEM = false: s/v in registers (168 VGPRs, 12 waves per workgroup).
 // MEM = true:  s/v in a per-wave scratch slab (<= 128 VGPRs, 16 waves), n_tt >= 1.
-constexpr uint32_t kSlabUint4 = 16 * 64;  // per-wave slab: 16 KiB
+constexpr uint32_t kSlabUint4 = 8 * 64;  // per-wave slab: 8 KiB (v)
 
 template <bool XALIGNED, bool MEM>
 __global__ __launch_bounds__((MEM ? 16 : kHybridWaves) * 64) void k_eval16_hybrid(

@@ -269,3 +269,15 @@ class DcfImpl:
                                                    _tptr(cwb), _tptr(s0s), _tptr(xs), _tptr(ys),
                                                    _stream(self.prg.device)))
         return ys
+
+    def eval_full_domain_device(self, b: bool, cwb, s0, ys=None):
+        """`Dcf::eval` at every x in [0, 2^(8N)) (increasing, big-endian x): (2^(8N), LAMBDA) device tensor."""
+        import torch
+        npts = 1 << (8 * self.n_bytes)
+        if ys is None:
+            ys = torch.empty((npts, self.lam), dtype=torch.uint8, device=cwb.device)
+        if ys.numel() != npts * self.lam:
+            raise DcfError(-5, "ys must hold 2^(8N) outputs")
+        check(_lib.load().dcf_eval_full_domain_device(self.prg.handle, self.n_bytes, int(bool(b)), _tptr(cwb),
+                                                      _tptr(s0), _tptr(ys), _stream(self.prg.device)))
+        return ys

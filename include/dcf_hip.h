@@ -138,6 +138,14 @@ int dcf_eval_device(dcf_prg* prg, size_t n_bytes, int party, const uint8_t* cwb,
 int dcf_eval_multikey_device(dcf_prg* prg, size_t n_bytes, size_t num_keys, size_t points_per_key, int party,
                              const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, void* stream);
 
+/* Full-domain eval: ys[x] = Dcf::eval(party, k, x) for every x in
+ * [0, 2^(8N)), x read big-endian (Msb0, lib.rs:181) — i.e. the output of
+ * dcf_eval_device over all points in increasing order.  ys: 2^(8N) * lambda
+ * bytes.  At lambda = 16 the tree is expanded breadth-first (2 AES blocks per
+ * leaf instead of 16N per point); N <= 4. */
+int dcf_eval_full_domain_device(dcf_prg* prg, size_t n_bytes, int party, const uint8_t* cwb, const uint8_t* s0,
+                                uint8_t* ys, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -296,3 +296,28 @@ def test_error_codes_on_device(dcf):
     with pytest.raises(dcf.DcfError) as e:
         dcf.Aes256HirosePrg([bytes(32)] * 2, 8)
     assert e.value.code == -2
+
+
+@pytest.mark.parametrize("nb,lam", [(1, 16), (2, 16), (1, 32), (1, 64)])
+def test_full_domain_eval_vs_oracle(dcf, nb, lam):
+    """Full-domain eval (tree expansion) == pointwise oracle eval over every x."""
+    import torch
+    rng = np.random.default_rng(nb * 100 + lam)
+    keys = [rng.bytes(32) for _ in range(2 if lam == 16 else 18)]
+    prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+    ok = O.gen(P, alpha, beta, s0, s1, 0)
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
+    cwb = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, nb, lam), np.uint8).copy()).cuda()
+    xs = np.array([list(i.to_bytes(nb, "big")) for i in range(1 << (8 * nb))], np.uint8)
+    ys = []
+    for b, s in ((0, s0), (1, s1)):
+        y = d.eval_full_domain_device(bool(b), cwb, torch.from_numpy(np.frombuffer(s, np.uint8).copy()).cuda())
+        torch.cuda.synchronize()
+        yh = y.cpu().numpy()
+        assert np.array_equal(yh, O.eval_(P, b, ok, s, xs, nthreads=8)), (nb, lam, b)
+        ys.append(yh)
+    a = int.from_bytes(alpha, "big")
+    rec = ys[0] ^ ys[1]
+    assert not rec[a:].any() and (rec[:a] == np.frombuffer(beta, np.uint8)).all()
