@@ -30,6 +30,7 @@ EXPORTS = [
     "dcf_prg_set_hybrid_split",
     "dcf_cwb_bytes", "dcf_cwb_np1_offset", "dcf_gen", "dcf_eval", "dcf_prg_gen",
     "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device", "dcf_eval_full_domain_device",
+    "dcf_share_bincode_bytes", "dcf_share_to_bincode", "dcf_share_from_bincode",
 ]
 
 
@@ -76,6 +77,9 @@ def load(path: str = LIB_PATH):
         "dcf_eval_device": ([vp, sz, i, u8p, u8p, u8p, sz, u8p, vp], i),
         "dcf_eval_multikey_device": ([vp, sz, sz, sz, i, u8p, u8p, u8p, u8p, vp], i),
         "dcf_eval_full_domain_device": ([vp, sz, i, u8p, u8p, u8p, vp], i),
+        "dcf_share_bincode_bytes": ([sz, sz, sz], sz),
+        "dcf_share_to_bincode": ([sz, sz, u8p, u8p, sz, u8p, sz], i),
+        "dcf_share_from_bincode": ([sz, sz, u8p, sz, u8p, u8p, sz, ctypes.POINTER(sz)], i),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

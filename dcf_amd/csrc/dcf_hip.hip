@@ -399,6 +399,92 @@ int dcf_eval_multikey_device(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t
   return eval_launch(p, n_bytes, num_keys, points_per_key, party, cwb, s0s, xs, ys, stream);
 }
 
+// ---- serde / bincode wire format of Share (lib.rs:217-340) ----
+// bincode 1.x `serialize` (the crate's declared dep, Cargo.toml:44): little-endian,
+// u64 length prefix per Vec, struct fields in declaration order, bool as one byte.
+
+size_t dcf_share_bincode_bytes(size_t n_bytes, size_t lambda, size_t num_s0s) {
+  const size_t n = 8 * n_bytes;
+  return 8 + num_s0s * (8 + lambda) + 8 + n * (2 * (8 + lambda) + 2) + 8 + lambda;
+}
+
+static void put_u64(uint8_t*& o, uint64_t v) {
+  for (int i = 0; i < 8; i++) *o++ = (uint8_t)(v >> (8 * i));
+}
+
+int dcf_share_to_bincode(size_t n_bytes, size_t lambda, const uint8_t* cwb, const uint8_t* s0s, size_t num_s0s,
+                         uint8_t* out, size_t out_len) {
+  if (!cwb || !out || (num_s0s && !s0s)) return fail(DCF_ERR_ARG, "null argument");
+  if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
+  if (lambda == 0 || lambda % 16) return fail(DCF_ERR_LAMBDA, "lambda must be a positive multiple of 16");
+  if (out_len != dcf_share_bincode_bytes(n_bytes, lambda, num_s0s)) return fail(DCF_ERR_LEN, "bad out_len");
+  const size_t n = 8 * n_bytes;
+  uint8_t* o = out;
+  put_u64(o, num_s0s);  // s0s: Vec<Vec<u8>> (lib.rs:291-292)
+  for (size_t i = 0; i < num_s0s; i++) {
+    put_u64(o, lambda);
+    memcpy(o, s0s + i * lambda, lambda);
+    o += lambda;
+  }
+  put_u64(o, n);  // cws: Vec<Cw> (lib.rs:293), Cw = (s, v, tl, tr) (lib.rs:222-227)
+  for (size_t i = 0; i < n; i++) {
+    put_u64(o, lambda);
+    memcpy(o, cwb + i * lambda, lambda);
+    o += lambda;
+    put_u64(o, lambda);
+    memcpy(o, cwb + (n + i) * lambda, lambda);
+    o += lambda;
+    const uint8_t t = cwb[2 * n * lambda + i];
+    *o++ = t & 1;
+    *o++ = (t >> 1) & 1;
+  }
+  put_u64(o, lambda);  // cw_np1 (lib.rs:294)
+  memcpy(o, cwb + dcf_cwb_np1_offset(n_bytes, lambda, 1), lambda);
+  return DCF_OK;
+}
+
+int dcf_share_from_bincode(size_t n_bytes, size_t lambda, const uint8_t* in, size_t in_len, uint8_t* cwb_out,
+                           uint8_t* s0s_out, size_t max_s0s, size_t* num_s0s) {
+  if (!in || !cwb_out || !num_s0s) return fail(DCF_ERR_ARG, "null argument");
+  if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
+  if (lambda == 0 || lambda % 16) return fail(DCF_ERR_LAMBDA, "lambda must be a positive multiple of 16");
+  const size_t n = 8 * n_bytes;
+  size_t pos = 0;
+  auto u64 = [&](uint64_t* v) {
+    if (in_len - pos < 8) return false;
+    *v = 0;
+    for (int i = 0; i < 8; i++) *v |= (uint64_t)in[pos + i] << (8 * i);
+    pos += 8;
+    return true;
+  };
+  auto arr = [&](uint8_t* dst) {  // Vec<u8> that must hold exactly lambda bytes (copy_from_slice, lib.rs:251)
+    uint64_t len;
+    if (!u64(&len) || len != lambda || in_len - pos < lambda) return false;
+    if (dst) memcpy(dst, in + pos, lambda);
+    pos += lambda;
+    return true;
+  };
+  uint64_t ns;
+  if (!u64(&ns)) return fail(DCF_ERR_KEY, "truncated Share (s0s length)");
+  if (ns > max_s0s && s0s_out) return fail(DCF_ERR_LEN, "more seeds than s0s_out holds");
+  for (uint64_t i = 0; i < ns; i++)
+    if (!arr(s0s_out ? s0s_out + i * lambda : nullptr)) return fail(DCF_ERR_KEY, "bad seed in s0s");
+  uint64_t ncw;
+  if (!u64(&ncw)) return fail(DCF_ERR_KEY, "truncated Share (cws length)");
+  if (ncw != n) return fail(DCF_ERR_KEY, "cws.len() != N * 8 (lib.rs:165)");
+  memset(cwb_out, 0, dcf_cwb_bytes(n_bytes, lambda, 1));
+  for (size_t i = 0; i < n; i++) {
+    if (!arr(cwb_out + i * lambda) || !arr(cwb_out + (n + i) * lambda)) return fail(DCF_ERR_KEY, "bad Cw.s / Cw.v");
+    if (in_len - pos < 2 || in[pos] > 1 || in[pos + 1] > 1) return fail(DCF_ERR_KEY, "bad Cw bool (bincode bool is 0/1)");
+    cwb_out[2 * n * lambda + i] = (uint8_t)(in[pos] | (in[pos + 1] << 1));
+    pos += 2;
+  }
+  if (!arr(cwb_out + dcf_cwb_np1_offset(n_bytes, lambda, 1))) return fail(DCF_ERR_KEY, "bad cw_np1");
+  if (pos != in_len) return fail(DCF_ERR_KEY, "trailing bytes after Share");
+  *num_s0s = (size_t)ns;
+  return DCF_OK;
+}
+
 int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uint8_t* cwb, const uint8_t* s0,
                                 uint8_t* ys, void* stream) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");

@@ -138,6 +138,22 @@ int dcf_eval_device(dcf_prg* prg, size_t n_bytes, int party, const uint8_t* cwb,
 int dcf_eval_multikey_device(dcf_prg* prg, size_t n_bytes, size_t num_keys, size_t points_per_key, int party,
                              const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, void* stream);
 
+/* ---- key wire format (host only, no GPU) ----
+ * `Share` as serialised by serde + bincode 1.x `bincode::serialize` (lib.rs:217-340;
+ * Cargo.toml:44): little-endian, u64 length before every Vec, fields in
+ * declaration order, bool = one byte 0/1:
+ *   u64 |s0s|, |s0s| x (u64 lambda, lambda bytes)
+ *   u64 8N,    8N x (u64 lambda, Cw.s, u64 lambda, Cw.v, u8 tl, u8 tr)
+ *   u64 lambda, cw_np1
+ * from_bincode writes the single-key CWB and the seeds; a Vec of the wrong
+ * length (the reference's copy_from_slice panics, lib.rs:251), a bool byte > 1,
+ * cws.len() != 8N (lib.rs:165), truncation or trailing bytes -> DCF_ERR_KEY. */
+size_t dcf_share_bincode_bytes(size_t n_bytes, size_t lambda, size_t num_s0s);
+int dcf_share_to_bincode(size_t n_bytes, size_t lambda, const uint8_t* cwb, const uint8_t* s0s, size_t num_s0s,
+                         uint8_t* out, size_t out_len);
+int dcf_share_from_bincode(size_t n_bytes, size_t lambda, const uint8_t* in, size_t in_len, uint8_t* cwb_out,
+                           uint8_t* s0s_out, size_t max_s0s, size_t* num_s0s);
+
 /* Full-domain eval: ys[x] = Dcf::eval(party, k, x) for every x in
  * [0, 2^(8N)), x read big-endian (Msb0, lib.rs:181) — i.e. the output of
  * dcf_eval_device over all points in increasing order.  ys: 2^(8N) * lambda
