@@ -52,7 +52,7 @@ def hybrid_peak() -> float:
 
 
 ENGINE = {0: "hybrid", 1: "ttable", 2: "bitsliced", 3: "hybrid"}
-KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16<0>", "bitsliced": "k_eval16_bs"}
+KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "bitsliced": "k_eval16_bs"}
 
 
 def engine_peak(engine: str) -> float:
@@ -140,7 +140,7 @@ def cpu_baseline(keys, n_bytes, lam, cwb_h: bytes, s0: bytes, xs_sample: np.ndar
     k.cw_t[:] = np.frombuffer(cwb_h[2 * n * lam:2 * n * lam + n], np.uint8)
     off = dcf_amd.cwb_np1_offset(n_bytes, lam, 1)
     k.cw_np1[:] = np.frombuffer(cwb_h[off:off + lam], np.uint8)
-    cal = xs_sample[: min(len(xs_sample), 8192 * threads)]
+    cal = xs_sample[: min(len(xs_sample), max(threads, 8192 * threads * 16 // lam))]
     t0 = time.perf_counter()
     y = O.eval_(P, 0, k, s0, cal, nthreads=threads)
     dt = time.perf_counter() - t0
@@ -161,10 +161,11 @@ def cpu_baseline(keys, n_bytes, lam, cwb_h: bytes, s0: bytes, xs_sample: np.ndar
 
 
 def run_eval(args, world, rank):
-    nb, lam = args.n_bytes, 16
+    nb, lam = args.n_bytes, args.lam
     m = args.points
     rng = np.random.default_rng(0xDCF0001)
-    keys = [rng.bytes(32) for _ in range(2)]
+    # benches/dcf_batch_eval.rs:7 uses 2 AES keys at LAMBDA = 16; benches/dcf_large_lambda.rs:10 uses 2048.
+    keys = [rng.bytes(32) for _ in range(2 if lam == 16 else 2048)]
     prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
     prg.set_eval_mode(args.eval_mode)
     if args.hybrid_split is not None:
@@ -201,15 +202,15 @@ def run_eval(args, world, rank):
     value = total_evals / wall
     bpe = blocks_per_eval(nb, lam)
     per_gpu_blocks = m * bpe / kern_s
-    engine = ENGINE[args.eval_mode] if nb <= 16 else "ttable"
-    kernel = KERNEL[engine]
+    engine = ENGINE[args.eval_mode] if (nb <= 16 and lam == 16) else "ttable"
+    kernel = KERNEL[engine] if lam == 16 else "k_eval_wide_head+k_eval_wide_tail"
     peak = engine_peak(engine)
     out = {
         "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"{args.workload.upper()}: N={nb} ({8 * nb}-bit x), lambda={lam}, Aes256HirosePrg, 1 key, "
-                               f"{m} points/GPU in HBM, party 0, eval only",
+        "config": {"workload": f"{args.workload.upper()}: N={nb} ({8 * nb}-bit x), lambda={lam}, Aes256HirosePrg "
+                               f"({len(keys)} AES keys), 1 key, {m} points/GPU in HBM, party 0, eval only",
                    "n_bytes": nb, "lambda": lam, "points_per_gpu": m, "global_points": m * world,
                    "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
         "aes_blocks_per_s": value * bpe,
@@ -228,7 +229,7 @@ def run_eval(args, world, rank):
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        ns = min(m, 1 << 26)
+        ns = min(m, 1 << 26, max(4096, (1 << 30) // lam))  # at most ~1 GiB of outputs copied back
         xs_h = xs[:ns].cpu().numpy()
         ys_h = ys[:ns].cpu().numpy()
         cwb_h = cwb.cpu().numpy().tobytes()
@@ -288,7 +289,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--n-bytes", type=int, default=None)
@@ -298,14 +299,24 @@ def main():
     ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves per workgroup")
     ap.add_argument("--hybrid-mem", type=int, default=1, help="hybrid: 1 = 16 waves + scratch slabs, 0 = 12 waves")
     args = ap.parse_args()
-    if args.workload == "c2":
+    args.lam = 16
+    if args.workload == "c1":    # benches/dcf_batch_eval.rs:17 shape
+        args.n_bytes = args.n_bytes or 16
+        args.points = args.points or 100_000
+    elif args.workload == "c2":  # 32-bit input
         args.n_bytes = args.n_bytes or 4
         args.points = args.points or (1 << 24)
+    elif args.workload == "c4":  # benches/dcf_large_lambda.rs:10-11 shape, 2^22 points per GPU
+        args.n_bytes = args.n_bytes or 16
+        args.points = args.points or (1 << 22)
+        args.lam = 16384
     else:
         args.n_bytes = args.n_bytes or 16
         args.points = args.points or (1 << 28)
     world, rank, _ = dist_setup(args.gpus)
     out = run_c5(args, world, rank) if args.workload == "c5" else run_eval(args, world, rank)
+    if args.workload != "c3":
+        out["metric"] = f"DCF evals/sec, workload {args.workload.upper()} (not the BASELINE.json headline config)"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
