@@ -51,12 +51,13 @@ def hybrid_peak() -> float:
     return b_tt + max(0.0, valu_left) / BS_VALU_PER_BLOCK
 
 
-ENGINE = {0: "hybrid", 1: "ttable", 2: "bitsliced", 3: "hybrid"}
-KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "bitsliced": "k_eval16_bs"}
+ENGINE = {0: "stream", 1: "ttable", 2: "bitsliced", 3: "hybrid", 4: "stream"}
+KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "bitsliced": "k_eval16_bs",
+          "stream": "k_eval16_stream"}
 
 
 def engine_peak(engine: str) -> float:
-    if engine == "ttable":
+    if engine in ("ttable", "stream"):
         return PEAK_TT_BLOCKS
     if engine == "bitsliced":
         return VALU_OPS / BS_VALU_PER_BLOCK
@@ -84,6 +85,17 @@ def blocks_per_eval(n_bytes: int, lam: int) -> int:
     """The reference's AES-256 block count per eval: 2 per level at LAMBDA = 16,
     4 per level at LAMBDA >= 32 (prg.rs:48-53 called once per level, lib.rs:176)."""
     return (2 if lam == 16 else 4) * 8 * n_bytes
+
+
+def zero_bits(xs: torch.Tensor) -> int:
+    """Number of 0 bits in the points = left steps = the A blocks the stream engine
+    encrypts on top of one B block per level (kernels_stream.h)."""
+    lut = torch.tensor([8 - bin(i).count("1") for i in range(256)], dtype=torch.int32, device=xs.device)
+    flat = xs.reshape(-1)
+    tot = 0
+    for off in range(0, flat.numel(), 1 << 26):
+        tot += int(lut[flat[off:off + (1 << 26)].to(torch.int64)].sum().item())
+    return tot
 
 
 def dist_setup(n_gpus: int):
@@ -201,8 +213,13 @@ def run_eval(args, world, rank):
     total_evals = m * world * args.steps
     value = total_evals / wall
     bpe = blocks_per_eval(nb, lam)
-    per_gpu_blocks = m * bpe / kern_s
-    engine = ENGINE[args.eval_mode] if (nb <= 16 and lam == 16) else "ttable"
+    engine = ENGINE[args.eval_mode] if lam == 16 else "ttable"
+    if engine in ("hybrid", "bitsliced") and nb > 16:
+        engine = "ttable"
+    # Blocks the dominant kernel actually encrypts per eval: the reference count, except the
+    # stream engine, which encrypts B on every level and A on left (x bit 0) levels only.
+    exec_bpe = (8 * nb + zero_bits(xs) / m) if engine == "stream" else bpe
+    per_gpu_blocks = m * exec_bpe / kern_s
     kernel = KERNEL[engine] if lam == 16 else "k_eval_wide_head+k_eval_wide_tail"
     peak = engine_peak(engine)
     out = {
@@ -215,17 +232,20 @@ def run_eval(args, world, rank):
                    "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
         "aes_blocks_per_s": value * bpe,
         "roofline": {
-            "bound": "lds" if engine == "ttable" else ("valu" if engine == "bitsliced" else "lds+valu"),
+            "bound": "lds" if engine in ("ttable", "stream") else ("valu" if engine == "bitsliced" else "lds+valu"),
             "kernel": kernel, "engine": engine,
             "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-256 blocks/s",
             "frac": per_gpu_blocks / peak, "traffic": pmc_traffic(kernel, m, nb, lam),
             "algorithmic_bytes": m * (nb + lam), "kernel_ms": kern_s * 1e3,
             "hbm_GBps": m * (nb + lam) / kern_s / 1e9,
             "ttable_only_peak": PEAK_TT_BLOCKS / 1e9,
-            "note": "blocks = reference count (2 AES-256 per level, 8N levels); peak per GPU at 2.4 GHz: "
-                    "T-table engine LDS-bound (32 ds_read_b32 lookups/clk/CU, 224 per block), bitsliced "
-                    "engine VALU-bound (128 lane-ops/clk/CU, ~800 per block); hybrid = LDS-saturating "
-                    "T-table + bitsliced on the VALU left over (DESIGN.md §4)",
+            "executed_blocks_per_eval": exec_bpe, "reference_blocks_per_eval": bpe,
+            "note": "achieved = AES-256 blocks the kernel encrypts per second (stream engine: B every "
+                    "level + A on left levels; other engines: the reference count, 2 per level); "
+                    "aes_blocks_per_s above uses the reference count.  Peak per GPU at 2.4 GHz: T-table "
+                    "engines LDS-bound (32 ds_read_b32 lookups/clk/CU, 224 per block), bitsliced VALU-bound "
+                    "(128 lane-ops/clk/CU, ~800 per block); hybrid = LDS-saturating T-table + bitsliced on "
+                    "the VALU left over (DESIGN.md section 4)",
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -295,7 +315,7 @@ def main():
     ap.add_argument("--n-bytes", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--eval-mode", type=int, default=0, help="AES engine: 0 auto, 1 T-table, 2 bitsliced, 3 hybrid")
+    ap.add_argument("--eval-mode", type=int, default=0, help="AES engine: 0 auto, 1 T-table, 2 bitsliced, 3 hybrid, 4 stream")
     ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves per workgroup")
     ap.add_argument("--hybrid-mem", type=int, default=1, help="hybrid: 1 = 16 waves + scratch slabs, 0 = 12 waves")
     args = ap.parse_args()

@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdcf_hip.so")
 
 DCF_OK = 0
-EVAL_AUTO, EVAL_TTABLE, EVAL_BITSLICED, EVAL_HYBRID = 0, 1, 2, 3
+EVAL_AUTO, EVAL_TTABLE, EVAL_BITSLICED, EVAL_HYBRID, EVAL_STREAM = 0, 1, 2, 3, 4
 ERRORS = {
     -1: "DCF_ERR_ARG",
     -2: "DCF_ERR_LAMBDA",

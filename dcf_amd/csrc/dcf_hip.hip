@@ -34,6 +34,7 @@
 #include "kernels16.h"
 #include "kernels_wide.h"
 #include "kernels_bs.h"
+#include "kernels_stream.h"
 
 namespace {
 
@@ -246,7 +247,7 @@ size_t dcf_prg_lambda(const dcf_prg* p) { return p ? p->lambda : 0; }
 
 int dcf_prg_set_eval_mode(dcf_prg* p, int mode) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");
-  if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_HYBRID) return fail(DCF_ERR_ARG, "bad eval mode");
+  if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_STREAM) return fail(DCF_ERR_ARG, "bad eval mode");
   p->eval_mode = mode;
   return DCF_OK;
 }
@@ -321,7 +322,11 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   hipStream_t st = (hipStream_t)stream;
   const bool bs_ok = (num_keys == 1 && n_bytes <= 16);
   int mode = p->eval_mode;
-  if (mode == DCF_EVAL_AUTO) mode = bs_ok ? DCF_EVAL_HYBRID : DCF_EVAL_TTABLE;
+  // Auto: one key -> the stream engine (T-table, right steps encrypt B only; C3: 407 M
+  // evals/s vs 353 M hybrid, 332 M T-table).  Many keys -> lockstep T-table, whose waves
+  // share one key's CWs through scalar loads (C5: 264 M vs 206 M evals/s with streams,
+  // whose lanes sit on different levels and miss L1 on the level-major CW layout).
+  if (mode == DCF_EVAL_AUTO) mode = (num_keys == 1) ? DCF_EVAL_STREAM : DCF_EVAL_TTABLE;
   // Single-key T-table eval also runs in the hybrid kernel, with every wave on
   // the T-table engine: its 512-point work units measured 13 % faster than
   // k_eval16<0>'s grid-stride loop (r01 sweep, 331.7 vs 292 M evals/s).
@@ -364,6 +369,23 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     else if (mem) DCF_HYB(false, true);
     else DCF_HYB(false, false);
 #undef DCF_HYB
+  } else if (mode == DCF_EVAL_STREAM) {
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+    const uint64_t units = (total + kStreamUnit - 1) / kStreamUnit;
+    if (units > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "stream eval: more than 2^32 work units");
+    uint64_t blocks = (units + 15) / 16;
+    if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
+    const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16, multi = num_keys > 1;
+#define DCF_STREAM(XR, MK)                                                                                    \
+  hipLaunchKernelGGL((k_eval16_stream<2, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], cws, \
+                     cwv, cwt, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,  \
+                     (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys)
+    if (xreg && multi) DCF_STREAM(true, true);
+    else if (xreg) DCF_STREAM(true, false);
+    else if (multi) DCF_STREAM(false, true);
+    else DCF_STREAM(false, false);
+#undef DCF_STREAM
   } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
     const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;

@@ -1,0 +1,232 @@
+// kernels_stream.h — LAMBDA = 16 eval with per-lane AES block scheduling.
+// Included by dcf_hip.hip only (after kernels_bs.h: reuses dequeue_unit).
+//
+// At LAMBDA = 16 one level of the GGM walk (lib.rs:174-189 over prg.rs:42-73)
+// needs AES_K0(~s) = B on every step but AES_K0(s) = A only on a LEFT step:
+//   right (x bit 1): s' = s&M ^ t*cw.s,  v ^= ~s&M ^ t*cw.v,  t' = lsb(B^~s) ^ t&tr
+//   left  (x bit 0): s' = (A^s)&M ^ t*cw.s,  v ^= (B^~s)&M ^ t*cw.v,  t' = lsb(A^s) ^ t&tl
+// A lockstep kernel computes A and B on every level (2 blocks); here each lane
+// runs NS independent points ("streams") and every AES slot encrypts the NEXT
+// block its stream needs — B, then A only if the step goes left — so every
+// encrypted block is used: 1 + (zero bits of x)/8N blocks per level, 1.5 on
+// average for uniform x instead of 2.  Outputs are bit-identical; the streams of
+// one wave sit on different levels, so correction words are per-lane vector
+// loads (L1/L2-resident: 4.2 KB per key) instead of scalar loads.
+//
+// Work: each wave takes kStreamUnit consecutive points at a time from one
+// global counter and hands them to its finished streams (wave-aggregated, in
+// uniform control flow), so a wave's x reads and y writes stay within a few KiB;
+// a stream with nothing left goes idle and the wave exits when all its streams
+// are idle.  (A static strided assignment of points to streams measured 25 %
+// slower: scattered 16-byte x reads and y writes.)  Multi-key (MULTI): point p
+// belongs to key p / points_per_key; CW index = level * K + key.
+#pragma once
+
+#include "aes_lds.h"
+
+namespace {
+
+constexpr uint32_t kStreamUnit = 256;  // points per refill of a wave
+
+// Lane's rank among the set bits of `mask` (bits below this lane).
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+template <int NS, bool XREG, bool MULTI>
+struct StreamLane {
+  uint32_t s[NS][4], v[NS][4], t[NS], ph[NS], lev[NS], cur[NS];
+  uint32_t xw[NS][4];             // XREG: queue of the point's next x words, as loaded (byte-swapped on use)
+  bool fresh[NS];                 // XREG: take cur from the queue head xw[0] before the next update
+  const uint8_t* xp[NS];          // !XREG: the point's row in xs
+  uint64_t ci[NS], pt[NS], key[NS];
+  bool alive[NS];
+};
+
+template <int NS, bool XREG, bool MULTI>
+__device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int i, uint64_t p,
+                                             const uint4* __restrict__ s0s, const uint4 s0v, uint32_t party,
+                                             const uint8_t* __restrict__ xs, uint32_t nbytes, uint64_t ppk) {
+  const uint64_t k = MULTI ? p / ppk : 0;
+  const uint4 sv = MULTI ? s0s[k] : s0v;  // k.s0s[0] (lib.rs:168)
+  L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) L.v[i][j] = 0u;
+  L.t[i] = party;  // lib.rs:169
+  L.ph[i] = 0u;
+  L.lev[i] = 0u;
+  L.ci[i] = k;
+  L.key[i] = k;
+  L.pt[i] = p;
+  L.alive[i] = true;
+  const uint8_t* row = xs + p * nbytes;
+  if (XREG) {
+    if (nbytes == 16) {
+      const uint4 x = *reinterpret_cast<const uint4*>(row);
+      L.xw[i][0] = x.x; L.xw[i][1] = x.y; L.xw[i][2] = x.z; L.xw[i][3] = x.w;
+    } else {
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        L.xw[i][w] = (4u * w < nbytes) ? reinterpret_cast<const uint32_t*>(row)[w] : 0u;
+    }
+    L.fresh[i] = true;
+  } else {
+    L.xp[i] = row;
+    L.cur[i] = load_bits32(row, 0, nbytes);
+  }
+}
+
+// Give every lane whose stream i is free (`mine`) a new point, or retire the
+// stream when the counter is exhausted.  Called in wave-uniform control flow.
+template <int NS, bool XREG, bool MULTI>
+__device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint64_t& unext,
+                                              uint64_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
+                                              uint64_t nunits, uint64_t total, const uint4* __restrict__ s0s,
+                                              const uint4 s0v, uint32_t party, const uint8_t* __restrict__ xs,
+                                              uint32_t nbytes, uint64_t ppk) {
+  uint64_t need = __ballot(mine);
+  while (need) {
+    if (unext >= uend && !exhausted) {
+      const uint32_t u = dequeue_unit(ctr);
+      if (u >= nunits) {
+        exhausted = true;
+      } else {
+        unext = (uint64_t)u * kStreamUnit;
+        uend = min(unext + kStreamUnit, total);
+      }
+    }
+    if (exhausted && unext >= uend) {
+      if (mine) {
+        L.alive[i] = false;
+        L.ci[i] = 0;  // keep the idle stream's CW loads in bounds
+      }
+      return;
+    }
+    const uint32_t rank = lane_rank(need);
+    const bool take = mine && (uint64_t)rank < uend - unext;
+    if (take) stream_start(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk);
+    const uint64_t taken = __ballot(take);
+    unext += (uint64_t)__popcll(taken);
+    need &= ~taken;
+    mine = mine && !take;
+  }
+}
+
+template <int NS, bool XREG, bool MULTI, int WG = kBlock>
+__global__ __launch_bounds__(WG, 1) void k_eval16_stream(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
+    const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
+    uint4* __restrict__ ys) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint32_t nlev = 8u * nbytes;
+  const uint64_t nunits = (total + kStreamUnit - 1) / kStreamUnit;
+  const uint64_t K = MULTI ? num_keys : 1;
+  uint64_t unext = 0, uend = 0;
+  bool exhausted = false;
+  const uint4 s0v = s0s[0];
+  StreamLane<NS, XREG, MULTI> L;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    L.fresh[i] = false;
+    L.alive[i] = false;
+    L.ci[i] = 0;
+    L.ph[i] = 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i)
+    stream_refill(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs, nbytes, ppk);
+
+  for (;;) {
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) any = any || L.alive[i];
+    if (!__ballot(any)) break;
+    // Correction words of each stream's current level (vector loads, issued before the AES).
+    uint4 cs[NS], cv[NS];
+    uint32_t ct[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      cs[i] = cw_s[L.ci[i]];
+      cv[i] = cw_v[L.ci[i]];
+      ct[i] = cw_t[L.ci[i]];
+    }
+    // Slot i encrypts ~s (B) in phase 0 and s (A) in phase 1.
+    uint32_t st[NS][4];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint32_t inv = L.ph[i] - 1u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[i][j] = L.s[i][j] ^ inv;
+    }
+    aes256_tt<NS>(st, rk, lds, lc);
+    // Pin the CW loads above the update: without this the compiler sinks the
+    // cw_t load into the (divergent) level-done path and waits on it there.
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+      asm volatile("" : "+v"(cs[i].x), "+v"(cs[i].y), "+v"(cs[i].z), "+v"(cs[i].w), "+v"(cv[i].x), "+v"(cv[i].y),
+                   "+v"(cv[i].z), "+v"(cv[i].w), "+v"(ct[i]));
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      if (XREG) {  // next 32 x bits from the word queue (raw loads, byte-swapped here)
+        const bool nw = L.fresh[i];
+        L.cur[i] = nw ? bswap32(L.xw[i][0]) : L.cur[i];
+        L.xw[i][0] = nw ? L.xw[i][1] : L.xw[i][0];
+        L.xw[i][1] = nw ? L.xw[i][2] : L.xw[i][1];
+        L.xw[i][2] = nw ? L.xw[i][3] : L.xw[i][2];
+      }
+      const uint32_t p = L.ph[i], xb = L.cur[i] >> 31;  // Msb0 bit of x (lib.rs:181)
+      const uint32_t adv = L.alive[i] ? (p | xb) : 0u;   // this step finishes the level
+      const uint32_t inv = p - 1u;                        // all ones on a B step
+      const uint32_t keepB = xb - 1u;                     // all ones when going left
+      const uint32_t tm = 0u - L.t[i], am = 0u - adv, pm = 0u - p;
+      const uint32_t csw[4] = {cs[i].x, cs[i].y, cs[i].z, cs[i].w};
+      const uint32_t cvw[4] = {cv[i].x, cv[i].y, cv[i].z, cv[i].w};
+      const uint32_t d0 = st[i][0] ^ L.s[i][0] ^ inv;  // (A^s) or (B^~s), word 0
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+        const uint32_t in = L.s[i][j] ^ inv;
+        // B step: v ^= v_hat(side) ^ t*cw.v, v_hat = (~s ^ [left] B) & M   (lib.rs:182/186)
+        const uint32_t vhat = (in ^ (st[i][j] & keepB)) & msk;
+        L.v[i][j] ^= inv & (vhat ^ (tm & cvw[j]));
+        // level done: s' = s(side) ^ t*cw.s, s(side) = (A^s)&M (left) or s&M (right)  (lib.rs:177-178)
+        const uint32_t sx = L.s[i][j] ^ (st[i][j] & pm);  // p: A ^ s
+        const uint32_t sn = (sx & msk) ^ (tm & csw[j]);
+        L.s[i][j] = (am & sn) | (~am & L.s[i][j]);
+      }
+      // t' = lsb(side) ^ t & cw.t(side)   (lib.rs:179-180, 183/187)
+      const uint32_t tb = (d0 ^ (L.t[i] & (ct[i] >> xb))) & 1u;
+      L.t[i] = (am & tb) | (~am & L.t[i]);
+      L.ph[i] = adv ^ 1u;
+      const uint32_t nl = L.lev[i] + adv;
+      const bool bnd = adv && (nl & 31u) == 0u;  // this stream's next 32 x bits start here
+      L.cur[i] <<= adv;
+      if (XREG)
+        L.fresh[i] = bnd;
+      else if (bnd && nl < nlev)
+        L.cur[i] = load_bits32(L.xp[i], nl >> 5, nbytes);
+      L.lev[i] = nl;
+      L.ci[i] += adv ? K : 0;
+    }
+    // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const bool done = L.alive[i] && L.lev[i] == nlev;
+      if (done) {
+        const uint4 np = cw_np1[L.key[i]];
+        const uint32_t tm = 0u - L.t[i];
+        ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
+                                 L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
+      }
+      if (__ballot(done))
+        stream_refill(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs, nbytes,
+                      ppk);
+    }
+  }
+}
+
+}  // namespace

@@ -152,7 +152,8 @@ class Aes256HirosePrg:
         return self._h
 
     def set_eval_mode(self, mode: int) -> None:
-        """AES engine for LAMBDA = 16 eval: 0 auto, 1 LDS T-table, 2 VALU bitsliced, 3 hybrid."""
+        """AES engine for LAMBDA = 16 eval: 0 auto, 1 LDS T-table, 2 VALU bitsliced, 3 hybrid,
+        4 stream (LDS T-table, per-lane block scheduling)."""
         check(_lib.load().dcf_prg_set_eval_mode(self._h, int(mode)))
 
     def set_hybrid_split(self, ttable_waves: int, slab_variant: int = 1) -> None:

@@ -67,10 +67,11 @@ extern "C" {
 #define DCF_BOUND_GT_BETA 1
 
 /* AES engine for LAMBDA = 16 eval (dcf_prg_set_eval_mode); results are identical. */
-#define DCF_EVAL_AUTO 0      /* library's choice (fastest eligible) */
+#define DCF_EVAL_AUTO 0      /* library's choice: STREAM for one key, TTABLE for many */
 #define DCF_EVAL_TTABLE 1    /* LDS T-table AES, one lane per point */
 #define DCF_EVAL_BITSLICED 2 /* VALU bitsliced AES, 32 points per lane quad (single key, N <= 16) */
 #define DCF_EVAL_HYBRID 3    /* both engines side by side on every CU (single key, N <= 16) */
+#define DCF_EVAL_STREAM 4    /* LDS T-table AES, per-lane block scheduling: a right step encrypts B only */
 
 /* Opaque: an Aes256HirosePrg (prg.rs:22-24) whose AES-256 schedules live on one
  * device, i.e. `DcfImpl::new(Aes256HirosePrg::new(keys))` (lib.rs:74, prg.rs:27). */

@@ -1,0 +1,16 @@
+"""Print mean-per-dispatch PMC values of the eval kernels in gpurun_out/<tag>/*/ (scripts/pmc_engines.sh)."""
+import glob
+import os
+import sqlite3
+import sys
+from collections import defaultdict
+
+for d in sorted(glob.glob(os.path.join(sys.argv[1], "*/"))):
+    for db in glob.glob(os.path.join(d, "*.db")):
+        c = sqlite3.connect(db)
+        agg = defaultdict(lambda: defaultdict(list))
+        for k, cn, v in c.execute("select kernel_name, counter_name, value from counters_collection"):
+            if "k_eval" in k:
+                agg[k.split("(")[0].split("::")[-1][:40]][cn].append(v)
+        for k, cs in agg.items():
+            print(os.path.basename(d.rstrip("/")), k, {cn: "%.4g" % (sum(v) / len(v)) for cn, v in sorted(cs.items())})

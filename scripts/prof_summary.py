@@ -29,7 +29,8 @@ def main(d):
         print("|---|---|---|---|---|")
         for name, calls, tot, avg, pct in c.execute(
                 "select name, total_calls, total_duration, average, percentage from top_kernels"):
-            print(f"| {short(name)} | {calls} | {tot / 1e6:.3f} | {avg / 1e6:.3f} | {pct:.2f} |")
+            # top_kernels durations are in microseconds
+            print(f"| {short(name)} | {calls} | {tot / 1e3:.3f} | {avg / 1e3:.3f} | {pct:.2f} |")
         print()
         rows = list(c.execute("select name, duration, vgpr_count, accum_vgpr_count, sgpr_count, lds_size, "
                               "grid_x, workgroup_x from kernels"))
@@ -87,9 +88,14 @@ if __name__ == "__main__":
     main(sys.argv[1])
     if len(sys.argv) > 2:
         import json
-        prefix = sys.argv[3] if len(sys.argv) > 3 else "k_eval16<0>"
+        prefix = sys.argv[3] if len(sys.argv) > 3 else "k_eval16_stream"
         t = pmc_traffic(sys.argv[1], prefix)
         t["source"] = sys.argv[1]
         t["kernel"] = prefix
+        # the launch shape of scripts/gpu_profile.sh's bench run (bench.py defaults, workload C3)
+        t.update({"workload": "C3", "points_per_launch": 1 << 28, "n_bytes": 16, "lambda": 16,
+                  "algorithmic_bytes": (1 << 28) * 32,
+                  "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- "
+                             "python bench.py --steps 2 --warmup 1 --no-cpu"})
         with open(sys.argv[2], "w") as f:
             json.dump(t, f, indent=1)

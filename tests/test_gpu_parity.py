@@ -114,10 +114,11 @@ def test_reference_reconstruction_kat(dcf, bound):
         assert y0[2].tobytes() != bytes(16) and y1[2].tobytes() != bytes(16)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("nb", [1, 2, 3, 4, 5, 7, 8, 12, 16, 17, 32])
 def test_eval_random_vs_oracle(dcf, nb, mode):
-    """mode 1 = LDS T-table engine, 2 = VALU bitsliced engine, 3 = hybrid (2 and 3: N <= 16 only)."""
+    """mode 1 = LDS T-table engine, 2 = VALU bitsliced engine, 3 = hybrid (2 and 3: N <= 16 only),
+    4 = T-table with per-lane block scheduling (stream engine)."""
     if mode in (2, 3) and nb > 16:
         pytest.skip("bitsliced engine covers N <= 16")
     rng = np.random.default_rng(100 + nb)
@@ -151,7 +152,7 @@ def test_eval_length_mismatch_is_error(dcf):
         d.eval(False, dcf.Share(k.s0s, k.cws[:127], k.cw_np1), REF_ALPHAS)  # lib.rs:165
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("nb,m", [(16, 1 << 20), (4, (1 << 20) + 37)])
 def test_eval_device_large_sample_and_reconstruction(dcf, nb, m, mode):
     """Large batch on device: bit-exact on a sample vs the oracle, and the
@@ -188,13 +189,15 @@ def test_eval_device_large_sample_and_reconstruction(dcf, nb, m, mode):
     assert not rec[~lt].any()
 
 
+@pytest.mark.parametrize("mode", [1, 4])
 @pytest.mark.parametrize("K,P", [(1, 100), (37, 64), (10, 13), (300, 128)])
-def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P):
+def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P, mode):
     import torch
     nb = 16
     rng = np.random.default_rng(K * 1000 + P)
     keys = [rng.bytes(32) for _ in range(2)]
     prg, Po = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    prg.set_eval_mode(mode)
     d = dcf.DcfImpl(nb, 16, prg)
     alpha, beta, s0, s1 = (_rand(rng, (K, nb)), _rand(rng, (K, 16)), _rand(rng, (K, 16)), _rand(rng, (K, 16)))
     T = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
