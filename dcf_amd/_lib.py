@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdcf_hip.so")
+# DCF_HIP_LIB: an alternative in-tree build of the same library (kernel-variant experiments).
+LIB_PATH = os.environ.get("DCF_HIP_LIB") or os.path.join(_HERE, "libdcf_hip.so")
 
 DCF_OK = 0
 EVAL_AUTO, EVAL_TTABLE, EVAL_BITSLICED, EVAL_HYBRID, EVAL_STREAM = 0, 1, 2, 3, 4

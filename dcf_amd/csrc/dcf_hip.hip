@@ -104,9 +104,9 @@ struct dcf_prg {
 
 namespace {
 
-constexpr uint64_t kWideChunk = 1ull << 20;   // points per head/tail pass (t-vector scratch 32 MiB)
+constexpr uint64_t kWideChunk = 1ull << 20;   // points per head/tail pass (t-vector scratch 64 MiB)
 constexpr uint64_t kGenChunk = 4096;          // keys per wide-gen launch (scratch 3*LAMBDA per key)
-constexpr uint32_t kTailPts = 4096;           // points per tail workgroup
+constexpr uint32_t kTailPts = 4096;          // points per tail workgroup
 
 int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
   if (p->ws_bytes >= bytes) return DCF_OK;

@@ -28,7 +28,10 @@
 
 namespace {
 
-constexpr int kTWords = 8;  // per-point t-vector stride (32 B): n + 1 <= 256 bits, N <= 31
+// Per-point t-vector (head -> tail), 64 B: byte c holds rows 4c..4c+3 of the
+// t-sequence in bits 0..3 (bit k = t_{4c+k}), i.e. the four-Russians index of
+// chunk c, ready for v_perm address building in the tail.  n + 1 <= 256 rows, N <= 31.
+constexpr int kTWords = 16;
 
 __device__ __forceinline__ void load_tab4(uint32_t* t4, const uint32_t* __restrict__ tab) {
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) t4[i] = tab[i];
@@ -88,7 +91,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head(
       v[j] = 0u;
     }
     uint32_t t = party;
-    uint32_t tacc = party, r = 1;  // bit r of the t-vector = t_r
+    uint32_t tacc = party, r = 1;  // t_r goes to bit (r & 3) of byte r >> 2
     uint32_t* trow = tvec + gg * kTWords;
     const uint8_t* x = xs + gg * nbytes;
     uint32_t lev = 0;
@@ -133,16 +136,16 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head(
           s[4 + j] = ((s[4 + j] ^ (e1[0][j] & R)) & msk) ^ (tm & csw[4 + j]);
         }
         t = tn;
-        tacc |= t << (r & 31u);
-        if ((r & 31u) == 31u) {
-          if (live) trow[r >> 5] = tacc;
+        tacc |= t << (8u * ((r >> 2) & 3u) + (r & 3u));
+        if ((r & 15u) == 15u) {
+          if (live) trow[r >> 4] = tacc;
           tacc = 0;
         }
         ++r;
       }
     }
     if (live) {
-      if ((r & 31u) != 0) trow[r >> 5] = tacc;
+      if ((r & 15u) != 0) trow[r >> 4] = tacc;
       const uint32_t tm = 0u - t;
       const uint4* np4 = reinterpret_cast<const uint4*>(cw_np1 + key * lam);
       const uint4 n0 = np4[0], n1 = np4[1];
@@ -227,17 +230,70 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
   }
   const uint64_t p0 = (uint64_t)blockIdx.y * pts_per_block;
   const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
-  for (uint64_t p = p0 + threadIdx.x / LP; p < p1; p += blockDim.x / LP) {
-    const uint32_t* trow = tvec + p * kTWords;
-    uint4 acc = cst;
-    uint32_t tw = 0;
-    for (uint32_t c = 0; c < nch; ++c) {
-      if ((c & 7u) == 0) tw = trow[c >> 3];
-      const uint32_t e = (tw >> ((c & 7u) * 4u)) & 15u;
-      const uint4 b = G[(c * 16 + e) * LP + q];
-      acc.x ^= b.x; acc.y ^= b.y; acc.z ^= b.z; acc.w ^= b.w;
+  const uint32_t pstep = blockDim.x / LP;
+  // The point's t-vector (64 B) is loaded one point ahead, so the LDS row reads
+  // of a point never wait on a global load.
+  uint64_t p = p0 + threadIdx.x / LP;
+  const uint4* tv4 = reinterpret_cast<const uint4*>(tvec);
+  uint4 nt[4] = {};
+  if (p < p1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) nt[k] = tv4[4 * p + k];
+  }
+  // Row read of chunk c: G + c * 16 * TW + e * TW + q * 16 bytes.  At TW = 256 one
+  // v_perm builds e * 256 + q * 16 (+ 64 KiB for c >= 16) from the t byte and a lane
+  // constant, and c * 4096 mod 64 KiB rides in the ds_read offset field.
+  const uint32_t qb0 = 16u * q;
+  const uint32_t nch16 = nch >> 4, nrem = nch & 15u;
+  for (; p < p1; p += pstep) {
+    const uint32_t tw[16] = {nt[0].x, nt[0].y, nt[0].z, nt[0].w, nt[1].x, nt[1].y, nt[1].z, nt[1].w,
+                             nt[2].x, nt[2].y, nt[2].z, nt[2].w, nt[3].x, nt[3].y, nt[3].z, nt[3].w};
+    const uint64_t pn = p + pstep;
+    if (pn < p1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) nt[k] = tv4[4 * pn + k];
     }
-    if (lane_live) *reinterpret_cast<uint4*>(ys + p * lam + off) = acc;
+    uint32_t acc[4] = {cst.x, cst.y, cst.z, cst.w};
+    uint32_t tq[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tq[k] = tw[k];
+    // Full groups of 16 chunks (4 t words): fully unrolled, constant LDS offsets.
+    const char* gb = reinterpret_cast<const char*>(G);
+    uint32_t qb = qb0;
+    for (uint32_t g16 = 0; g16 < nch16; ++g16) {
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j += 2) {
+        uint4 b[2];
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+          const uint32_t cc = j + h;
+          if (TW == 256) {
+            const uint32_t a = __builtin_amdgcn_perm(tq[cc >> 2], qb, 0x0c020000u | ((4u + (cc & 3u)) << 8));
+            b[h] = *reinterpret_cast<const uint4*>(gb + a + cc * 4096u);
+          } else {
+            const uint32_t e = (tq[cc >> 2] >> (8u * (cc & 3u))) & 15u;
+            b[h] = G[((16u * g16 + cc) * 16u + e) * LP + q];
+          }
+        }
+        acc[0] = xor3(acc[0], b[0].x, b[1].x);
+        acc[1] = xor3(acc[1], b[0].y, b[1].y);
+        acc[2] = xor3(acc[2], b[0].z, b[1].z);
+        acc[3] = xor3(acc[3], b[0].w, b[1].w);
+      }
+#pragma unroll
+      for (int k = 0; k < 12; ++k) tq[k] = tq[k + 4];  // word queue: no dynamic register indexing
+      qb += 0x10000u;
+    }
+    // Remaining nch % 16 chunks.
+#pragma unroll
+    for (uint32_t cc = 0; cc < 15; ++cc) {
+      if (cc < nrem) {
+        const uint32_t e = (tq[cc >> 2] >> (8u * (cc & 3u))) & 15u;
+        const uint4 b = G[((16u * nch16 + cc) * 16u + e) * LP + q];
+        acc[0] ^= b.x; acc[1] ^= b.y; acc[2] ^= b.z; acc[3] ^= b.w;
+      }
+    }
+    if (lane_live) *reinterpret_cast<uint4*>(ys + p * lam + off) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
   }
 }
 

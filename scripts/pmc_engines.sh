@@ -9,6 +9,7 @@ case $SET in
   a) C="SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT";;
   b) C="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_ANY SQ_INST_LEVEL_LDS SQ_LDS_CMD_FIFO_FULL SQ_IFETCH GRBM_GUI_ACTIVE";;
 esac
+WL=${WORKLOAD:-c3}
 for m in $MODES; do
-  timeout -s KILL 120 rocprofv3 --pmc $C -d $OUT/m$m$SET -o pmc -- python bench.py --steps 2 --warmup 1 --no-cpu --eval-mode $m --points $PTS > $OUT/m$m$SET.log 2>&1 || exit 1
+  timeout -s KILL 120 rocprofv3 --pmc $C -d $OUT/m$m$SET -o pmc -- python bench.py --workload $WL --steps 2 --warmup 1 --no-cpu --eval-mode $m --points $PTS > $OUT/m$m$SET.log 2>&1 || exit 1
 done

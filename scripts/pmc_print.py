@@ -11,6 +11,6 @@ for d in sorted(glob.glob(os.path.join(sys.argv[1], "*/"))):
         agg = defaultdict(lambda: defaultdict(list))
         for k, cn, v in c.execute("select kernel_name, counter_name, value from counters_collection"):
             if "k_eval" in k:
-                agg[k.split("(")[0].split("::")[-1][:40]][cn].append(v)
+                agg[k.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:40]][cn].append(v)
         for k, cs in agg.items():
             print(os.path.basename(d.rstrip("/")), k, {cn: "%.4g" % (sum(v) / len(v)) for cn, v in sorted(cs.items())})
