@@ -53,10 +53,16 @@ def hybrid_peak() -> float:
 
 ENGINE = {0: "stream", 1: "ttable", 2: "bitsliced", 3: "hybrid", 4: "stream"}
 KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "bitsliced": "k_eval16_bs",
-          "stream": "k_eval16_stream"}
+          "stream": "k_eval16_stream", "mmo": "k_eval16_mmo"}
+
+
+# MMO (AES-128, kernels_mmo.h): 10 rounds x 16 lookups + 11 round-key ds_read_b128 (16 lanes/clk) per block
+PEAK_MMO_BLOCKS = CUS * CLK_HZ / (160 / 32 + 11 / 16)
 
 
 def engine_peak(engine: str) -> float:
+    if engine == "mmo":
+        return PEAK_MMO_BLOCKS
     if engine in ("ttable", "stream"):
         return PEAK_TT_BLOCKS
     if engine == "bitsliced":
@@ -138,13 +144,13 @@ def gen_points(m: int, n_bytes: int, rank: int, seed: int) -> torch.Tensor:
 
 
 def cpu_baseline(keys, n_bytes, lam, cwb_h: bytes, s0: bytes, xs_sample: np.ndarray, ys_gpu: np.ndarray,
-                 target_s: float):
+                 target_s: float, prg_kind: str = "hirose"):
     """Time the C++-free C restatement of the reference eval (oracle, AES-NI,
     one pthread per core over contiguous point chunks like rayon) on this host.
     Bounded: calibrate on a small slice, then run ~target_s of CPU work."""
     from oracle import oracle as O
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    P = O.OraclePrg(keys, lam)
+    P = (O.OracleMmoPrg if prg_kind == "mmo" else O.OraclePrg)(keys, lam)
     k = O.OracleKey(n_bytes, lam)
     n = 8 * n_bytes
     k.cw_s[:] = np.frombuffer(cwb_h[:n * lam], np.uint8).reshape(n, lam)
@@ -177,8 +183,12 @@ def run_eval(args, world, rank):
     m = args.points
     rng = np.random.default_rng(0xDCF0001)
     # benches/dcf_batch_eval.rs:7 uses 2 AES keys at LAMBDA = 16; benches/dcf_large_lambda.rs:10 uses 2048.
-    keys = [rng.bytes(32) for _ in range(2 if lam == 16 else 2048)]
-    prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
+    if args.prg == "mmo":  # Aes128MatyasMeyerOseasPrg (north_star's PRG; not in the reference): 4 AES-128 keys
+        keys = [rng.bytes(16) for _ in range(4)]
+        prg = dcf_amd.Aes128MatyasMeyerOseasPrg(keys, lam, device=torch.cuda.current_device())
+    else:
+        keys = [rng.bytes(32) for _ in range(2 if lam == 16 else 2048)]
+        prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
     prg.set_eval_mode(args.eval_mode)
     if args.hybrid_split is not None:
         prg.set_hybrid_split(args.hybrid_split, args.hybrid_mem)
@@ -216,9 +226,11 @@ def run_eval(args, world, rank):
     engine = ENGINE[args.eval_mode] if lam == 16 else "ttable"
     if engine in ("hybrid", "bitsliced") and nb > 16:
         engine = "ttable"
+    if args.prg == "mmo":
+        engine = "mmo"
     # Blocks the dominant kernel actually encrypts per eval: the reference count, except the
     # stream engine, which encrypts B on every level and A on left (x bit 0) levels only.
-    exec_bpe = (8 * nb + zero_bits(xs) / m) if engine == "stream" else bpe
+    exec_bpe = (8 * nb + zero_bits(xs) / m) if engine == "stream" else bpe  # mmo: 2 AES-128 per level
     per_gpu_blocks = m * exec_bpe / kern_s
     kernel = KERNEL[engine] if lam == 16 else "k_eval_wide_head+k_eval_wide_tail"
     peak = engine_peak(engine)
@@ -226,15 +238,16 @@ def run_eval(args, world, rank):
         "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"{args.workload.upper()}: N={nb} ({8 * nb}-bit x), lambda={lam}, Aes256HirosePrg "
+        "config": {"workload": f"{args.workload.upper()}: N={nb} ({8 * nb}-bit x), lambda={lam}, "
+                               f"{'Aes128MatyasMeyerOseasPrg' if args.prg == 'mmo' else 'Aes256HirosePrg'} "
                                f"({len(keys)} AES keys), 1 key, {m} points/GPU in HBM, party 0, eval only",
                    "n_bytes": nb, "lambda": lam, "points_per_gpu": m, "global_points": m * world,
                    "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
         "aes_blocks_per_s": value * bpe,
         "roofline": {
-            "bound": "lds" if engine in ("ttable", "stream") else ("valu" if engine == "bitsliced" else "lds+valu"),
+            "bound": "lds" if engine in ("ttable", "stream", "mmo") else ("valu" if engine == "bitsliced" else "lds+valu"),
             "kernel": kernel, "engine": engine,
-            "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-256 blocks/s",
+            "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-128 blocks/s" if engine == "mmo" else "G AES-256 blocks/s",
             "frac": per_gpu_blocks / peak, "traffic": pmc_traffic(kernel, m, nb, lam),
             "algorithmic_bytes": m * (nb + lam), "kernel_ms": kern_s * 1e3,
             "hbm_GBps": m * (nb + lam) / kern_s / 1e9,
@@ -254,7 +267,7 @@ def run_eval(args, world, rank):
         ys_h = ys[:ns].cpu().numpy()
         cwb_h = cwb.cpu().numpy().tobytes()
         out["cpu_baseline"] = cpu_baseline(keys, nb, lam, cwb_h, seeds[0].cpu().numpy().tobytes(), xs_h, ys_h,
-                                           args.cpu_seconds)
+                                           args.cpu_seconds, args.prg)
     return out
 
 
@@ -316,6 +329,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--eval-mode", type=int, default=0, help="AES engine: 0 auto, 1 T-table, 2 bitsliced, 3 hybrid, 4 stream")
+    ap.add_argument("--prg", default="hirose", choices=["hirose", "mmo"],
+                    help="hirose: the reference's Aes256HirosePrg; mmo: Aes128MatyasMeyerOseasPrg (lambda = 16)")
     ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves per workgroup")
     ap.add_argument("--hybrid-mem", type=int, default=1, help="hybrid: 1 = 16 waves + scratch slabs, 0 = 12 waves")
     args = ap.parse_args()
@@ -335,8 +350,9 @@ def main():
         args.points = args.points or (1 << 28)
     world, rank, _ = dist_setup(args.gpus)
     out = run_c5(args, world, rank) if args.workload == "c5" else run_eval(args, world, rank)
-    if args.workload != "c3":
-        out["metric"] = f"DCF evals/sec, workload {args.workload.upper()} (not the BASELINE.json headline config)"
+    if args.workload != "c3" or args.prg != "hirose":
+        out["metric"] = (f"DCF evals/sec, workload {args.workload.upper()}, {args.prg} PRG "
+                         "(not the BASELINE.json headline config)")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

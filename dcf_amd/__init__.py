@@ -7,6 +7,7 @@ of include/dcf_hip.h).  This package is the host-side mirror of the crate's
 """
 from ._lib import DcfError, LIB_PATH, load  # noqa: F401
 from .dcf import (  # noqa: F401
+    Aes128MatyasMeyerOseasPrg,
     Aes256HirosePrg,
     BoundState,
     CmpFn,
@@ -20,6 +21,6 @@ from .dcf import (  # noqa: F401
 )
 
 __all__ = [
-    "Aes256HirosePrg", "BoundState", "CmpFn", "Cw", "DcfImpl", "Share", "DcfError",
+    "Aes128MatyasMeyerOseasPrg", "Aes256HirosePrg", "BoundState", "CmpFn", "Cw", "DcfImpl", "Share", "DcfError",
     "cwb_bytes", "cwb_np1_offset", "cwb_to_share", "share_to_cwb", "load", "LIB_PATH",
 ]

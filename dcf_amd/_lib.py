@@ -27,7 +27,7 @@ ERRORS = {
 
 # Every symbol the header declares (tests check the library exports all of them).
 EXPORTS = [
-    "dcf_version", "dcf_last_error", "dcf_hirose_prg_new", "dcf_prg_free", "dcf_prg_lambda", "dcf_prg_set_eval_mode",
+    "dcf_version", "dcf_last_error", "dcf_hirose_prg_new", "dcf_mmo_prg_new", "dcf_prg_kind", "dcf_prg_free", "dcf_prg_lambda", "dcf_prg_set_eval_mode",
     "dcf_prg_set_hybrid_split",
     "dcf_cwb_bytes", "dcf_cwb_np1_offset", "dcf_gen", "dcf_eval", "dcf_prg_gen",
     "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device", "dcf_eval_full_domain_device",
@@ -65,6 +65,8 @@ def load(path: str = LIB_PATH):
         "dcf_version": ([], ctypes.c_char_p),
         "dcf_last_error": ([], ctypes.c_char_p),
         "dcf_hirose_prg_new": ([u8p, sz, sz, i, ctypes.POINTER(vp)], i),
+        "dcf_mmo_prg_new": ([u8p, sz, sz, i, ctypes.POINTER(vp)], i),
+        "dcf_prg_kind": ([vp], i),
         "dcf_prg_free": ([vp], None),
         "dcf_prg_lambda": ([vp], sz),
         "dcf_prg_set_eval_mode": ([vp, i], i),

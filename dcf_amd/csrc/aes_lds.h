@@ -71,6 +71,28 @@ void aes256_expand_words(const uint8_t key[32], RoundKeys* rk) {
                ((uint32_t)b[4 * i + 3] << 24);
 }
 
+// AES-128 key expansion (FIPS-197 §5.2, Nk = 4): 44 words = 11 round keys.
+void aes128_expand_words(const uint8_t key[16], uint32_t w[44]) {
+  uint8_t b[176];
+  memcpy(b, key, 16);
+  uint8_t rcon = 1;
+  for (int i = 4; i < 44; i++) {
+    uint8_t t[4] = {b[4 * i - 4], b[4 * i - 3], b[4 * i - 2], b[4 * i - 1]};
+    if (i % 4 == 0) {
+      const uint8_t t0 = t[0];
+      t[0] = (uint8_t)(g_sbox[t[1]] ^ rcon);
+      t[1] = g_sbox[t[2]];
+      t[2] = g_sbox[t[3]];
+      t[3] = g_sbox[t0];
+      rcon = gmul(rcon, 2);
+    }
+    for (int k = 0; k < 4; k++) b[4 * i + k] = (uint8_t)(b[4 * (i - 4) + k] ^ t[k]);
+  }
+  for (int i = 0; i < 44; i++)
+    w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+           ((uint32_t)b[4 * i + 3] << 24);
+}
+
 // ------------------------------------------------------------------------
 // Device: LDS T-tables and AES-256
 // ------------------------------------------------------------------------
@@ -151,6 +173,60 @@ __device__ __forceinline__ void aes256_tt(uint32_t (&st)[NB][4], const RoundKeys
       const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
       o[b][j] = xor3(lo, hi, rk.w[56 + j]);
     }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+}
+
+// NB independent AES-128 encryptions (10 rounds), each under its own key
+// schedule read from LDS: rk[b] points at 11 uint4 round keys (per lane, so a
+// lane may pick its schedule; lanes reading the same schedule broadcast).
+template <int NB>
+__device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* const (&rk)[NB], const uint32_t* lds,
+                                          uint32_t lc) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint4 k = rk[b][0];
+    st[b][0] ^= k.x; st[b][1] ^= k.y; st[b][2] ^= k.z; st[b][3] ^= k.w;
+  }
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    uint32_t o[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint4 k = rk[b][r];
+      const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+        const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+        const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+        const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+        o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+  uint32_t o[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint4 k = rk[b][10];
+    const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+      const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+      const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+      const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+      const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
+      const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
+      o[b][j] = xor3(lo, hi, kw[j]);
+    }
+  }
 #pragma unroll
   for (int b = 0; b < NB; ++b)
 #pragma unroll

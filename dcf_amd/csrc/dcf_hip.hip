@@ -35,6 +35,7 @@
 #include "kernels_wide.h"
 #include "kernels_bs.h"
 #include "kernels_stream.h"
+#include "kernels_mmo.h"
 
 namespace {
 
@@ -85,11 +86,13 @@ struct DevBuf {
 }  // namespace
 
 struct dcf_prg {
+  int kind = 0;               // 0: Aes256HirosePrg (prg.rs), 1: Aes128MatyasMeyerOseasPrg (kernels_mmo.h)
   int device = 0;
   int cus = 256;
   size_t lambda = 0;
   size_t cipher_n = 0;
   std::vector<RoundKeys> rk;  // Aes256::new per key (prg.rs:28-31)
+  uint4* d_rk128 = nullptr;   // MMO: AES-128 schedules of ciphers 0..3 (4 x 11 round keys)
   uint32_t* d_tab = nullptr;  // T0..T3 (4 KiB) on the device
   uint4* d_km = nullptr;      // bitsliced round-key masks of cipher 0 (15 x 4 x 8 uint4)
   uint8_t* d_ws = nullptr;    // stream-ordered scratch (LAMBDA >= 32 paths)
@@ -230,12 +233,50 @@ int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int 
   return DCF_OK;
 }
 
+int dcf_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int device, dcf_prg** out) {
+  if (!keys || !out) return fail(DCF_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (lambda == 0 || lambda % 16 != 0) return fail(DCF_ERR_LAMBDA, "lambda must be a positive multiple of 16");
+  if (lambda != 16) return fail(DCF_ERR_UNSUPPORTED, "Aes128MatyasMeyerOseasPrg: lambda = 16 only");
+  if (cipher_n < 4 * (lambda / 16)) return fail(DCF_ERR_CIPHER_N, "MMO PRG needs 4 * lambda / 16 AES-128 keys");
+  std::call_once(g_aes_once, aes_init_tables);
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(DCF_ERR_ARG, "bad device ordinal");
+  DeviceGuard dg(device);
+  if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
+  dcf_prg* p = new dcf_prg();
+  p->kind = 1;
+  p->device = device;
+  p->lambda = lambda;
+  p->cipher_n = cipher_n;
+  p->eval_mode = DCF_EVAL_TTABLE;
+  std::vector<uint32_t> w(4 * 44);
+  for (size_t i = 0; i < 4; i++) aes128_expand_words(keys + 16 * i, w.data() + 44 * i);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    p->cus = prop.multiProcessorCount;
+  hipError_t e = hipMalloc(&p->d_tab, sizeof(g_tab));
+  if (e == hipSuccess) e = hipMemcpy(p->d_tab, g_tab, sizeof(g_tab), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&p->d_rk128, w.size() * 4);
+  if (e == hipSuccess) e = hipMemcpy(p->d_rk128, w.data(), w.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    dcf_prg_free(p);
+    return fail(DCF_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e));
+  }
+  *out = p;
+  return DCF_OK;
+}
+
+int dcf_prg_kind(const dcf_prg* p) { return p ? p->kind : -1; }
+
 void dcf_prg_free(dcf_prg* p) {
   if (!p) return;
   {
     DeviceGuard dg(p->device);
     if (p->d_tab) (void)hipFree(p->d_tab);
     if (p->d_km) (void)hipFree(p->d_km);
+    if (p->d_rk128) (void)hipFree(p->d_rk128);
     if (p->d_ws) (void)hipFree(p->d_ws);
     if (p->d_ctr) (void)hipFree(p->d_ctr);
     if (p->d_slabs) (void)hipFree(p->d_slabs);
@@ -274,6 +315,14 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
   uint8_t* cwv = cwb_out + n * num_keys * lam;
   uint8_t* cwt = cwb_out + 2 * n * num_keys * lam;
   uint8_t* np1 = cwb_out + dcf_cwb_np1_offset(n_bytes, lam, num_keys);
+  if (p->kind == 1) {  // Aes128MatyasMeyerOseasPrg (LAMBDA = 16)
+    hipLaunchKernelGGL(k_gen16_mmo, dim3((unsigned)grid_for(num_keys, p->cus)), dim3(kBlock), 0, (hipStream_t)stream,
+                       p->d_tab, p->d_rk128, alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1,
+                       (uint32_t)bound, (uint32_t)n_bytes, (uint64_t)num_keys, (uint4*)cws, (uint4*)cwv, cwt,
+                       (uint4*)np1);
+    HIP_TRY(hipGetLastError());
+    return DCF_OK;
+  }
   if (lam > 16) {  // one workgroup per key, keys in chunks (scratch 3*LAMBDA per key)
     hipStream_t st = (hipStream_t)stream;
     const uint64_t chunk = num_keys < kGenChunk ? num_keys : kGenChunk;
@@ -320,6 +369,18 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   const uint4* np1 = (const uint4*)(cwb + dcf_cwb_np1_offset(n_bytes, lam, num_keys));
   const dim3 grid((unsigned)grid_for(total, p->cus)), block(kBlock);
   hipStream_t st = (hipStream_t)stream;
+  if (p->kind == 1) {  // MMO: lockstep, two blocks per level (the side's s and v), any engine setting
+#define DCF_MMO(MODE)                                                                                          \
+  hipLaunchKernelGGL(k_eval16_mmo<MODE>, grid, block, 0, st, p->d_tab, p->d_rk128, cws, cwv, cwt, np1,            \
+                     (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk, \
+                     (uint4*)ys)
+    if (num_keys == 1) DCF_MMO(0);
+    else if (ppk % 64 == 0) DCF_MMO(1);
+    else DCF_MMO(2);
+#undef DCF_MMO
+    HIP_TRY(hipGetLastError());
+    return DCF_OK;
+  }
   const bool bs_ok = (num_keys == 1 && n_bytes <= 16);
   int mode = p->eval_mode;
   // Auto: one key -> the stream engine (T-table, right steps encrypt B only; C3: 407 M
@@ -554,8 +615,13 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   HIP_TRY(hipGetLastError());
   for (uint32_t lev = 0; lev < nlev; ++lev) {
     const uint64_t parents = 1ull << lev;
-    hipLaunchKernelGGL(k_fd_level16, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
-                       p->rk[0], cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b, (uint4*)ys);
+    if (p->kind == 1)
+      hipLaunchKernelGGL(k_fd_level16_mmo, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                         p->d_rk128, cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b,
+                         (uint4*)ys);
+    else
+      hipLaunchKernelGGL(k_fd_level16, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                         p->rk[0], cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b, (uint4*)ys);
     HIP_TRY(hipGetLastError());
     std::swap(s_a, s_b);
     std::swap(v_a, v_b);
@@ -626,7 +692,10 @@ int dcf_prg_gen(dcf_prg* p, const uint8_t* seeds, size_t m, uint8_t* out) {
   HIP_TRY(s.alloc(m * lam));
   HIP_TRY(o.alloc(m * row));
   HIP_TRY(hipMemcpy(s.p, seeds, m * lam, hipMemcpyHostToDevice));
-  if (lam == 16)
+  if (p->kind == 1)
+    hipLaunchKernelGGL(k_prg16_mmo, dim3((unsigned)grid_for(m, p->cus)), dim3(kBlock), 0, nullptr, p->d_tab,
+                       p->d_rk128, (const uint4*)s.p, (uint64_t)m, (uint8_t*)o.p);
+  else if (lam == 16)
     hipLaunchKernelGGL(k_prg16, dim3((unsigned)grid_for(m, p->cus)), dim3(kBlock), 0, nullptr, p->d_tab, p->rk[0],
                        (const uint4*)s.p, (uint64_t)m, (uint8_t*)o.p);
   else

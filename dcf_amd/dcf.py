@@ -8,6 +8,7 @@ Same names, argument meaning and error behaviour as the Rust crate
   trait Dcf<N, LAMBDA> { gen, eval }  lib.rs:24-35   DcfImpl.gen / DcfImpl.eval
   struct CmpFn { alpha, beta }        lib.rs:41-46   CmpFn
   trait Prg / Aes256HirosePrg::new    lib.rs:52, prg.rs:27  Aes256HirosePrg(keys, lam)
+  Aes128MatyasMeyerOseasPrg (north_star; not in the crate)  Aes128MatyasMeyerOseasPrg(keys, lam)
   DcfImpl::new(prg)                   lib.rs:74      DcfImpl(n_bytes, lam, prg)
   struct Cw { s, v, tl, tr }          lib.rs:209     Cw
   struct Share { s0s, cws, cw_np1 }   lib.rs:275     Share
@@ -181,8 +182,33 @@ class Aes256HirosePrg:
         return res
 
 
+class Aes128MatyasMeyerOseasPrg(Aes256HirosePrg):
+    """`Aes128MatyasMeyerOseasPrg::<LAMBDA, CIPHER_N>::new(keys)`, the PRG BASELINE.json's
+    north_star names, resident on one GPU.  The reference crate has no such PRG, so its
+    definition is ours (include/dcf_hip.h, dcf_mmo_prg_new; parity unpinned):
+    out_b = AES128_{keys[b]}(seed) ^ seed for b = s_L, v_L, s_R, v_R; t from bit 0 of
+    byte 0 of s_L / s_R; bit 0 of the last byte cleared (prg.rs:63-68's convention).
+
+    keys: CIPHER_N >= 4 16-byte AES-128 keys; LAMBDA = 16.
+    """
+
+    def __init__(self, keys: Sequence[bytes], lam: int = 16, device: int = 0):
+        keys = [bytes(k) for k in keys]
+        if any(len(k) != 16 for k in keys):
+            raise ValueError("AES-128 keys are 16 bytes")
+        L = _lib.load()
+        blob = b"".join(keys)
+        h = ctypes.c_void_p()
+        check(L.dcf_mmo_prg_new(_ptr(blob), len(keys), lam, device, ctypes.byref(h)))
+        self._h = h
+        self.lam = lam
+        self.cipher_n = len(keys)
+        self.device = device
+
+
 class DcfImpl:
-    """`DcfImpl<N, LAMBDA, Aes256HirosePrg>` (lib.rs:63-205) on MI355X."""
+    """`DcfImpl<N, LAMBDA, P>` (lib.rs:63-205) on MI355X, P = Aes256HirosePrg or
+    Aes128MatyasMeyerOseasPrg."""
 
     def __init__(self, n_bytes: int, lam: int, prg: Aes256HirosePrg):
         if prg.lam != lam:

@@ -112,6 +112,41 @@ class Aes256HirosePrg final : public Prg<LAMBDA> {
   dcf_prg* h_ = nullptr;
 };
 
+// Aes128MatyasMeyerOseasPrg<LAMBDA, CIPHER_N>::new(keys): the PRG BASELINE.json's
+// north_star names (not in the reference crate; definition in dcf_hip.h,
+// dcf_mmo_prg_new; parity unpinned).  CIPHER_N >= 4 AES-128 keys, LAMBDA = 16.
+template <size_t LAMBDA, size_t CIPHER_N>
+class Aes128MatyasMeyerOseasPrg final : public Prg<LAMBDA> {
+ public:
+  explicit Aes128MatyasMeyerOseasPrg(const std::array<const std::array<uint8_t, 16>*, CIPHER_N>& keys,
+                                     int device = 0) {
+    std::vector<uint8_t> blob(16 * CIPHER_N);
+    for (size_t i = 0; i < CIPHER_N; ++i) std::memcpy(blob.data() + 16 * i, keys[i]->data(), 16);
+    check(dcf_mmo_prg_new(blob.data(), CIPHER_N, LAMBDA, device, &h_));
+  }
+  ~Aes128MatyasMeyerOseasPrg() override { dcf_prg_free(h_); }
+  Aes128MatyasMeyerOseasPrg(const Aes128MatyasMeyerOseasPrg&) = delete;
+  Aes128MatyasMeyerOseasPrg& operator=(const Aes128MatyasMeyerOseasPrg&) = delete;
+
+  PrgOut<LAMBDA> gen(const std::array<uint8_t, LAMBDA>& seed) const override {
+    std::vector<uint8_t> out(4 * LAMBDA + 2);
+    check(dcf_prg_gen(h_, seed.data(), 1, out.data()));
+    PrgOut<LAMBDA> r;
+    auto slice = [&](size_t i) {
+      std::array<uint8_t, LAMBDA> a;
+      std::memcpy(a.data(), out.data() + i * LAMBDA, LAMBDA);
+      return a;
+    };
+    r[0] = std::make_tuple(slice(0), slice(1), out[4 * LAMBDA] != 0);
+    r[1] = std::make_tuple(slice(2), slice(3), out[4 * LAMBDA + 1] != 0);
+    return r;
+  }
+  dcf_prg* handle() const override { return h_; }
+
+ private:
+  dcf_prg* h_ = nullptr;
+};
+
 // `Dcf<N, LAMBDA>` (lib.rs:24-35).
 template <size_t N, size_t LAMBDA>
 class Dcf {

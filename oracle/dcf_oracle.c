@@ -8,6 +8,11 @@
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
  * it; the product library never links or calls it.
  *
+ * Also restated: the Aes128MatyasMeyerOseasPrg that BASELINE.json's north_star
+ * names.  The reference has no such PRG, so its definition is ours (see
+ * include/dcf_hip.h, dcf_mmo_prg_new) and its parity is UNPINNED by the
+ * reference; AES-128 itself is pinned by FIPS-197 C.1 in tests/.
+ *
  * Parity anchors (the Rust crate cannot be built here: no cargo/rustc, nightly
  * features, un-vendored deps — see DESIGN.md "Oracle"):
  *   - AES-256 arithmetic: third-party crate `aes` ^0.8.3 (Cargo.toml:36, version
@@ -129,6 +134,52 @@ void orc_aes256_encrypt_portable(const uint8_t rk[240], const uint8_t in[16], ui
   memcpy(out, s, 16);
 }
 
+/* AES-128 key expansion (FIPS-197 §5.2, Nk = 4): 11 round keys = 176 bytes. */
+void orc_aes128_expand(const uint8_t key[16], uint8_t rk[176]) {
+  ensure_sbox();
+  memcpy(rk, key, 16);
+  uint8_t rcon = 1;
+  for (int i = 4; i < 44; i++) {
+    uint8_t t[4];
+    memcpy(t, rk + 4 * (i - 1), 4);
+    if (i % 4 == 0) {
+      uint8_t t0 = t[0];
+      t[0] = (uint8_t)(SBOX[t[1]] ^ rcon);
+      t[1] = SBOX[t[2]];
+      t[2] = SBOX[t[3]];
+      t[3] = SBOX[t0];
+      rcon = gf_mul(rcon, 2);
+    }
+    for (int k = 0; k < 4; k++) rk[4 * i + k] = (uint8_t)(rk[4 * (i - 4) + k] ^ t[k]);
+  }
+}
+
+/* Portable AES-128 block encryption (FIPS-197 §5.1, Nr = 10). */
+void orc_aes128_encrypt_portable(const uint8_t rk[176], const uint8_t in[16], uint8_t out[16]) {
+  uint8_t s[16], t[16];
+  for (int i = 0; i < 16; i++) s[i] = (uint8_t)(in[i] ^ rk[i]);
+  for (int round = 1; round <= 10; round++) {
+    for (int i = 0; i < 16; i++) s[i] = SBOX[s[i]];
+    for (int c = 0; c < 4; c++)
+      for (int r = 0; r < 4; r++) t[r + 4 * c] = s[r + 4 * ((c + r) & 3)];
+    memcpy(s, t, 16);
+    if (round != 10)
+      for (int c = 0; c < 4; c++) aes_mix_column(s + 4 * c);
+    for (int i = 0; i < 16; i++) s[i] ^= rk[16 * round + i];
+  }
+  memcpy(out, s, 16);
+}
+
+#if defined(__x86_64__)
+__attribute__((target("aes,sse2"))) static void aes128_encrypt_ni(const uint8_t rk[176], const uint8_t* in,
+                                                                   uint8_t* out) {
+  __m128i a = _mm_xor_si128(_mm_loadu_si128((const __m128i*)in), _mm_loadu_si128((const __m128i*)rk));
+  for (int r = 1; r < 10; r++) a = _mm_aesenc_si128(a, _mm_loadu_si128((const __m128i*)(rk + 16 * r)));
+  a = _mm_aesenclast_si128(a, _mm_loadu_si128((const __m128i*)(rk + 160)));
+  _mm_storeu_si128((__m128i*)out, a);
+}
+#endif
+
 #if defined(__x86_64__)
 __attribute__((target("aes,sse2"))) static void aes256_encrypt2_ni(const uint8_t rk[240], const uint8_t* in0,
                                                                     const uint8_t* in1, uint8_t* out0,
@@ -161,8 +212,9 @@ static int cpu_has_aesni(void) { return 0; }
 typedef struct {
   size_t lambda;
   size_t cipher_n;
-  uint8_t* rk; /* cipher_n * 240 bytes: Aes256::new per key, prg.rs:27-33 */
+  uint8_t* rk; /* Hirose: cipher_n * 240 bytes (Aes256::new per key, prg.rs:27-33); MMO: cipher_n * 176 */
   int use_ni;
+  int kind;    /* 0 = Aes256HirosePrg, 1 = Aes128MatyasMeyerOseasPrg */
 } orc_prg;
 
 /* Aes256HirosePrg::new (prg.rs:27-33).  The reference panics on
@@ -191,6 +243,30 @@ int orc_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int allow_n
   return ORC_OK;
 }
 
+/* Aes128MatyasMeyerOseasPrg::<LAMBDA, CIPHER_N>::new: CIPHER_N AES-128 keys,
+ * CIPHER_N >= 4 * LAMBDA / 16 (one key per 16-byte block of each of the four
+ * outputs). */
+int orc_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int allow_ni, orc_prg** out) {
+  if (!keys || !out) return ORC_ERR_ARG;
+  if (lambda == 0 || lambda % 16 != 0) return ORC_ERR_LAMBDA;
+  if (cipher_n < 4 * (lambda / 16)) return ORC_ERR_CIPHER_N;
+  ensure_sbox();
+  orc_prg* p = (orc_prg*)calloc(1, sizeof(orc_prg));
+  if (!p) return ORC_ERR_ARG;
+  p->lambda = lambda;
+  p->cipher_n = cipher_n;
+  p->kind = 1;
+  p->rk = (uint8_t*)malloc(cipher_n * 176);
+  if (!p->rk) {
+    free(p);
+    return ORC_ERR_ARG;
+  }
+  for (size_t i = 0; i < cipher_n; i++) orc_aes128_expand(keys + 16 * i, p->rk + 176 * i);
+  p->use_ni = allow_ni && cpu_has_aesni();
+  *out = p;
+  return ORC_OK;
+}
+
 void orc_prg_free(orc_prg* p) {
   if (!p) return;
   free(p->rk);
@@ -212,11 +288,40 @@ static void enc2(const orc_prg* p, size_t ci, const uint8_t* in0, const uint8_t*
   orc_aes256_encrypt_portable(rk, in1, out1);
 }
 
+/* Aes128MatyasMeyerOseasPrg::gen: out_b = AES128_{k[b * LAMBDA/16 + j]}(seed_j) ^ seed_j
+ * per 16-byte block j, b = s_L, v_L, s_R, v_R; t_L / t_R = Lsb0 bit 0 of byte 0 of
+ * s_L / s_R before the clear; bit 0 of byte LAMBDA-1 cleared in all four (the
+ * convention of prg.rs:63-68). */
+static void mmo_gen(const orc_prg* p, const uint8_t* seed, uint8_t* sl, uint8_t* vl, int* tl, uint8_t* sr,
+                    uint8_t* vr, int* tr) {
+  const size_t lam = p->lambda, nb = lam / 16;
+  uint8_t* outs[4] = {sl, vl, sr, vr};
+  for (size_t b = 0; b < 4; b++)
+    for (size_t j = 0; j < nb; j++) {
+      const uint8_t* rk = p->rk + 176 * (b * nb + j);
+      uint8_t* o = outs[b] + 16 * j;
+#if defined(__x86_64__)
+      if (p->use_ni)
+        aes128_encrypt_ni(rk, seed + 16 * j, o);
+      else
+#endif
+        orc_aes128_encrypt_portable(rk, seed + 16 * j, o);
+      for (int k = 0; k < 16; k++) o[k] ^= seed[16 * j + k]; /* Matyas-Meyer-Oseas: E_k(m) ^ m */
+    }
+  *tl = sl[0] & 1;
+  *tr = sr[0] & 1;
+  for (int b = 0; b < 4; b++) outs[b][lam - 1] &= 0xfe;
+}
+
 /* Aes256HirosePrg::gen (prg.rs:42-73).
  * scratch: 5*lambda bytes.  out: sl, vl, sr, vr (lambda bytes each), tl, tr. */
 static void prg_gen(const orc_prg* p, const uint8_t* seed, uint8_t* scratch, uint8_t* sl, uint8_t* vl, int* tl,
                     uint8_t* sr, uint8_t* vr, int* tr) {
   const size_t lam = p->lambda;
+  if (p->kind == 1) {
+    mmo_gen(p, seed, sl, vl, tl, sr, vr, tr);
+    return;
+  }
   uint8_t* seed_p = scratch; /* prg.rs:44: seed ^ c(), c() = 0xff.. (prg.rs:36-38) */
   for (size_t i = 0; i < lam; i++) seed_p[i] = (uint8_t)(seed[i] ^ 0xff);
   /* prg.rs:45-46: result_buf0 = [[0; L]; 2], result_buf1 = [[0; L]; 2]

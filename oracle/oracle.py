@@ -42,6 +42,12 @@ def lib():
         u8p = ctypes.POINTER(ctypes.c_uint8)
         L.orc_prg_new.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(P)]
         L.orc_prg_new.restype = ctypes.c_int
+        L.orc_mmo_prg_new.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(P)]
+        L.orc_mmo_prg_new.restype = ctypes.c_int
+        L.orc_aes128_expand.argtypes = [u8p, u8p]
+        L.orc_aes128_expand.restype = None
+        L.orc_aes128_encrypt_portable.argtypes = [u8p, u8p, u8p]
+        L.orc_aes128_encrypt_portable.restype = None
         L.orc_prg_free.argtypes = [P]
         L.orc_prg_free.restype = None
         L.orc_prg_uses_aesni.argtypes = [P]
@@ -80,20 +86,33 @@ def aes256_encrypt(key: bytes, block: bytes) -> bytes:
     return out.tobytes()
 
 
+def aes128_encrypt(key: bytes, block: bytes) -> bytes:
+    rk = np.zeros(176, np.uint8)
+    lib().orc_aes128_expand(_p(_u8(key)), _p(rk))
+    out = np.zeros(16, np.uint8)
+    lib().orc_aes128_encrypt_portable(_p(rk), _p(_u8(block)), _p(out))
+    return out.tobytes()
+
+
 class OraclePrg:
     """Aes256HirosePrg<LAMBDA, CIPHER_N> (prg.rs:22-74)."""
+    KEY_BYTES = 32
 
     def __init__(self, keys, lam: int, allow_aesni: bool = True):
         keys = [bytes(k) for k in keys]
-        assert all(len(k) == 32 for k in keys)
+        assert all(len(k) == self.KEY_BYTES for k in keys)
         self.lam = lam
         self.cipher_n = len(keys)
         self._keys = _u8(b"".join(keys))
         h = ctypes.c_void_p()
-        rc = lib().orc_prg_new(_p(self._keys), self.cipher_n, lam, int(allow_aesni), ctypes.byref(h))
+        rc = self._new(_p(self._keys), self.cipher_n, lam, int(allow_aesni), ctypes.byref(h))
         if rc != 0:
-            raise ValueError(f"orc_prg_new failed rc={rc}")
+            raise ValueError(f"prg constructor failed rc={rc}")
         self._h = h
+
+    @staticmethod
+    def _new(*args):
+        return lib().orc_prg_new(*args)
 
     @property
     def uses_aesni(self) -> bool:
@@ -113,6 +132,16 @@ class OraclePrg:
         assert rc == 0
         return [(outs[0].tobytes(), outs[1].tobytes(), bool(t[0])),
                 (outs[2].tobytes(), outs[3].tobytes(), bool(t[1]))]
+
+
+class OracleMmoPrg(OraclePrg):
+    """Aes128MatyasMeyerOseasPrg<LAMBDA, CIPHER_N> (BASELINE.json north_star; not in the
+    reference, parity unpinned): CIPHER_N >= 4 * LAMBDA / 16 AES-128 keys."""
+    KEY_BYTES = 16
+
+    @staticmethod
+    def _new(*args):
+        return lib().orc_mmo_prg_new(*args)
 
 
 class OracleKey:

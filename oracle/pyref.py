@@ -25,6 +25,7 @@ def _libcrypto():
         c.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
         c.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
         c.EVP_aes_256_ecb.restype = ctypes.c_void_p
+        c.EVP_aes_128_ecb.restype = ctypes.c_void_p
         c.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p,
                                          ctypes.c_char_p]
         c.EVP_CIPHER_CTX_set_padding.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -36,11 +37,12 @@ def _libcrypto():
 
 class Aes256Ecb:
     def __init__(self, key: bytes):
-        assert len(key) == 32
+        assert len(key) in (16, 32)
         c = _libcrypto()
         self._c = c
         self._ctx = c.EVP_CIPHER_CTX_new()
-        assert c.EVP_EncryptInit_ex(self._ctx, c.EVP_aes_256_ecb(), None, key, None) == 1
+        cipher = c.EVP_aes_256_ecb() if len(key) == 32 else c.EVP_aes_128_ecb()
+        assert c.EVP_EncryptInit_ex(self._ctx, cipher, None, key, None) == 1
         c.EVP_CIPHER_CTX_set_padding(self._ctx, 0)
 
     def encrypt(self, data: bytes) -> bytes:
@@ -87,6 +89,30 @@ class HirosePrg:
         for b in buf0 + buf1:
             b[lam - 1] &= 0xFE
         return [(bytes(buf0[0]), bytes(buf1[0]), bit0), (bytes(buf0[1]), bytes(buf1[1]), bit1)]
+
+
+class MmoPrg:
+    """Aes128MatyasMeyerOseasPrg (ours; the reference has none): out_b = AES128_{k_b}(seed) ^ seed
+    blockwise for b = s_L, v_L, s_R, v_R; t from bit 0 of byte 0 of s_L / s_R; the last
+    byte's bit 0 cleared as in prg.rs:63-68."""
+
+    def __init__(self, keys, lam: int):
+        self.lam = lam
+        self.ciphers = [Aes256Ecb(bytes(k)) for k in keys]  # 16-byte keys -> AES-128
+
+    def gen(self, seed: bytes):
+        lam, nb = self.lam, self.lam // 16
+        outs = []
+        for b in range(4):
+            o = bytearray()
+            for j in range(nb):
+                blk = seed[16 * j:16 * (j + 1)]
+                o += _xor(self.ciphers[b * nb + j].encrypt(blk), blk)
+            outs.append(o)
+        tl, tr = bool(outs[0][0] & 1), bool(outs[2][0] & 1)
+        for o in outs:
+            o[lam - 1] &= 0xFE
+        return [(bytes(outs[0]), bytes(outs[1]), tl), (bytes(outs[2]), bytes(outs[3]), tr)]
 
 
 def _bit_msb0(b: bytes, i: int) -> bool:

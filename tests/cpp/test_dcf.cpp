@@ -3,6 +3,7 @@
 // thread_rng() seeds are replaced by fixed bytes; a golden PRG row pins bits.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <string>
 
@@ -41,7 +42,8 @@ static const Bytes16 SEED = hex<16>("2a4c8f2579125a942a458f242b4e4819");  // prg
 using Prg16 = dcf::Aes256HirosePrg<16, 2>;
 using Dcf16 = dcf::DcfImpl<16, 16, Prg16>;
 
-static void eval_both(const Dcf16& d, const dcf::Share<16>& k, std::vector<Bytes16>& ys0, std::vector<Bytes16>& ys1) {
+template <class DcfT>
+static void eval_both(const DcfT& d, const dcf::Share<16>& k, std::vector<Bytes16>& ys0, std::vector<Bytes16>& ys1) {
   dcf::Share<16> k0 = k, k1 = k;
   k0.s0s = {k.s0s[0]};  // lib.rs:382-385
   k1.s0s = {k.s0s[1]};
@@ -58,9 +60,9 @@ static void eval_both(const Dcf16& d, const dcf::Share<16>& k, std::vector<Bytes
   d.eval(true, k1, xs, y1p);
 }
 
-static void reconstruction(dcf::BoundState bound, const int expect[5]) {
-  Prg16 prg({&KEY0, &KEY1});
-  Dcf16 d(prg);
+template <class PrgT>
+static void reconstruction(const PrgT& prg, dcf::BoundState bound, const int expect[5]) {
+  dcf::DcfImpl<16, 16, PrgT> d(prg);
   for (int trial = 0; trial < 3; ++trial) {
     Bytes16 s0{}, s1{};
     for (int i = 0; i < 16; ++i) {
@@ -83,16 +85,22 @@ static void reconstruction(dcf::BoundState bound, const int expect[5]) {
 }
 
 int main() {
+  Prg16 prg({&KEY0, &KEY1});
+  // The same two reference tests over the MMO PRG (north_star; keys = halves of KEYS).
+  std::array<uint8_t, 16> mk[4];
+  for (int i = 0; i < 4; ++i) std::memcpy(mk[i].data(), (i < 2 ? KEY0 : KEY1).data() + 16 * (i & 1), 16);
+  dcf::Aes128MatyasMeyerOseasPrg<16, 4> mmo({&mk[0], &mk[1], &mk[2], &mk[3]});
   {  // test_dcf_gen_then_eval_ok (lib.rs:372-395)
     const int expect[5] = {1, 1, 0, 0, 0};
-    reconstruction(dcf::BoundState::LtBeta, expect);
+    reconstruction(prg, dcf::BoundState::LtBeta, expect);
+    reconstruction(mmo, dcf::BoundState::LtBeta, expect);
   }
   {  // test_dcf_gen_gt_beta_then_eval_ok (lib.rs:397-420)
     const int expect[5] = {0, 0, 0, 1, 1};
-    reconstruction(dcf::BoundState::GtBeta, expect);
+    reconstruction(prg, dcf::BoundState::GtBeta, expect);
+    reconstruction(mmo, dcf::BoundState::GtBeta, expect);
   }
   {  // test_prg_gen_not_zeros (prg.rs:86-96) + golden row (tests/golden/prg16.json rows[0])
-    Prg16 prg({&KEY0, &KEY1});
     auto out = prg.gen(SEED);
     for (int i = 0; i < 2; ++i) {
       CHECK(std::get<0>(out[i]) != Bytes16{});
@@ -102,7 +110,6 @@ int main() {
     if (want) CHECK(std::get<0>(out[0]) == hex<16>(want));
   }
   {  // panics of the reference become exceptions
-    Prg16 prg({&KEY0, &KEY1});
     Dcf16 d(prg);
     Bytes16 s0{}, s1{};
     auto k = d.gen(dcf::CmpFn<16, 16>{ALPHAS[0], BETA}, {&s0, &s1}, dcf::BoundState::LtBeta);

@@ -61,18 +61,26 @@ def sha(b: bytes) -> str:
     return hashlib.sha256(b).hexdigest()
 
 
-def dcf_case(name, keys, lam, n_bytes, alpha, beta, s0s, bound, xs, full=True):
+FIPS197_C1 = {
+    "key": bytes(range(16)).hex(),
+    "pt": "00112233445566778899aabbccddeeff",
+    "ct": "69c4e0d86a7b0430d8cdb78070b4c55a",
+}
+
+
+def dcf_case(name, keys, lam, n_bytes, alpha, beta, s0s, bound, xs, full=True, mmo=False):
     """Run gen + eval of both parties on both restatements; return a fixture dict."""
-    P = O.OraclePrg(keys, lam)
+    OP, RP = (O.OracleMmoPrg, R.MmoPrg) if mmo else (O.OraclePrg, R.HirosePrg)
+    P = OP(keys, lam)
     k = O.gen(P, alpha, beta, s0s[0], s0s[1], bound)
     xa = np.frombuffer(b"".join(xs), np.uint8).reshape(len(xs), n_bytes)
     y0 = O.eval_(P, 0, k, s0s[0], xa, nthreads=4)
     y1 = O.eval_(P, 1, k, s0s[1], xa, nthreads=4)
     # portable AES path must agree with AES-NI
-    Pp = O.OraclePrg(keys, lam, allow_aesni=False)
+    Pp = OP(keys, lam, allow_aesni=False)
     assert (O.eval_(Pp, 0, k, s0s[0], xa[:4]) == y0[:4]).all()
     # independent restatement (small cases in full, large ones on a prefix)
-    Q = R.HirosePrg(keys, lam)
+    Q = RP(keys, lam)
     if lam * n_bytes <= 256:
         cws, np1 = R.gen(Q, alpha, beta, s0s, bound)
         assert np1 == k.cw_np1.tobytes()
@@ -105,8 +113,47 @@ def dcf_case(name, keys, lam, n_bytes, alpha, beta, s0s, bound, xs, full=True):
     return d
 
 
+def mmo_vectors():
+    """Aes128MatyasMeyerOseasPrg fixtures.  PARITY UNPINNED: the reference has no MMO
+    PRG (its definition is ours, include/dcf_hip.h); these vectors pin our GPU path
+    to two agreeing CPU restatements and AES-128 to FIPS-197 C.1."""
+    kat = [FIPS197_C1]
+    for i in range(8):
+        key, pt = detbytes(f"aes128/key/{i}", 16), detbytes(f"aes128/pt/{i}", 16)
+        ct = R.Aes256Ecb(key).encrypt(pt)  # 16-byte key -> EVP aes-128-ecb
+        assert O.aes128_encrypt(key, pt) == ct
+        kat.append({"key": key.hex(), "pt": pt.hex(), "ct": ct.hex()})
+    assert O.aes128_encrypt(bytes(range(16)), bytes.fromhex(FIPS197_C1["pt"])).hex() == FIPS197_C1["ct"]
+    keys = [detbytes(f"mmo16/key/{i}", 16) for i in range(4)]
+    P, Q = O.OracleMmoPrg(keys, 16), R.MmoPrg(keys, 16)
+    rows = []
+    for i in range(32):
+        sd = detbytes(f"mmo16/seed/{i}", 16)
+        g = P.gen(sd)
+        assert g == Q.gen(sd)
+        (sl, vl, tl), (sr, vr, tr) = g
+        rows.append({"seed": sd.hex(), "sl": sl.hex(), "vl": vl.hex(), "tl": tl, "sr": sr.hex(), "vr": vr.hex(),
+                     "tr": tr})
+    cases = []
+    for nb, bound in ((16, 0), (16, 1), (4, 0), (3, 1)):
+        alpha = detbytes(f"mmo/n{nb}/alpha", nb)
+        xs = [alpha] + [detbytes(f"mmo/n{nb}/x/{i}", nb) for i in range(47)]
+        cases.append(dcf_case(f"mmo_n{nb}_{'lt' if bound == 0 else 'gt'}", keys, 16, nb, alpha,
+                              detbytes(f"mmo/n{nb}/beta", 16),
+                              [detbytes(f"mmo/n{nb}/s0/0", 16), detbytes(f"mmo/n{nb}/s0/1", 16)], bound, xs,
+                              mmo=True))
+    return {"parity": "unpinned: no MMO PRG in the reference; C oracle == Python/libcrypto restatement",
+            "aes128_kat": kat, "keys": [k.hex() for k in keys], "prg_rows": rows, "cases": cases}
+
+
 def main():
-    out = {}
+    if sys.argv[1:] == ["--mmo"]:
+        with open(os.path.join(HERE, "mmo16.json"), "w") as f:
+            json.dump(mmo_vectors(), f, indent=1)
+            f.write("\n")
+        print("wrote mmo16")
+        return
+    out = {"mmo16": mmo_vectors()}
     # AES-256 known answers: FIPS-197 C.3 + libcrypto on derived keys/blocks
     kat = [FIPS197_C3]
     for i in range(8):
