@@ -179,11 +179,15 @@ __device__ __forceinline__ void aes256_tt(uint32_t (&st)[NB][4], const RoundKeys
     for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
 }
 
-// NB independent AES-128 encryptions (10 rounds), each under its own key
-// schedule read from LDS: rk[b] points at 11 uint4 round keys (per lane, so a
-// lane may pick its schedule; lanes reading the same schedule broadcast).
-template <int NB>
-__device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* const (&rk)[NB], const uint32_t* lds,
+// NB independent AES encryptions with NR rounds (10: AES-128, 14: AES-256), each
+// under its own key schedule read from LDS: rk[b] points at NR + 1 uint4 round
+// keys (per lane, so a lane may pick its schedule; lanes reading the same
+// schedule broadcast).
+// LATE_KEYS: each round's key read waits (through an empty asm) for the previous
+// round's state, so the compiler cannot hoist all the key reads up front (for
+// kernels that are short of VGPRs; costs one v_add per round and block).
+template <int NR, int NB, bool LATE_KEYS = false>
+__device__ __forceinline__ void aes_tt_lk(uint32_t (&st)[NB][4], const uint4* const (&rk)[NB], const uint32_t* lds,
                                           uint32_t lc) {
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -191,11 +195,13 @@ __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* co
     st[b][0] ^= k.x; st[b][1] ^= k.y; st[b][2] ^= k.z; st[b][3] ^= k.w;
   }
 #pragma unroll
-  for (int r = 1; r < 10; ++r) {
+  for (int r = 1; r < NR; ++r) {
     uint32_t o[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const uint4 k = rk[b][r];
+      uint32_t z = 0u;
+      if (LATE_KEYS) asm volatile("" : "+v"(z) : "v"(st[b][0]));
+      const uint4 k = rk[b][r + z];
       const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -214,7 +220,7 @@ __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* co
   uint32_t o[NB][4];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const uint4 k = rk[b][10];
+    const uint4 k = rk[b][NR];
     const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -231,6 +237,12 @@ __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* co
   for (int b = 0; b < NB; ++b)
 #pragma unroll
     for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+}
+
+template <int NB>
+__device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* const (&rk)[NB], const uint32_t* lds,
+                                          uint32_t lc) {
+  aes_tt_lk<10, NB>(st, rk, lds, lc);
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }

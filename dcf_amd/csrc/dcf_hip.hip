@@ -36,6 +36,7 @@
 #include "kernels_bs.h"
 #include "kernels_stream.h"
 #include "kernels_mmo.h"
+#include "kernels_wide_stream.h"
 
 namespace {
 
@@ -93,6 +94,9 @@ struct dcf_prg {
   size_t cipher_n = 0;
   std::vector<RoundKeys> rk;  // Aes256::new per key (prg.rs:28-31)
   uint4* d_rk128 = nullptr;   // MMO: AES-128 schedules of ciphers 0..3 (4 x 11 round keys)
+  uint4* d_rk2 = nullptr;     // LAMBDA >= 32 stream head: AES-256 schedules of ciphers 0 and 17
+  uint8_t* d_dig = nullptr;   // LAMBDA >= 32 stream head: compact CW digest of the current key
+  uint32_t dig_levels = 0;
   uint32_t* d_tab = nullptr;  // T0..T3 (4 KiB) on the device
   uint4* d_km = nullptr;      // bitsliced round-key masks of cipher 0 (15 x 4 x 8 uint4)
   uint8_t* d_ws = nullptr;    // stream-ordered scratch (LAMBDA >= 32 paths)
@@ -132,7 +136,7 @@ int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, cons
   const size_t lds = (size_t)nch * 16 * TW;
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail<TW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const dim3 grid((unsigned)((lam - 32 + TW - 1) / TW), (unsigned)((cnt + kTailPts - 1) / kTailPts));
+  const dim3 grid((unsigned)((lam + TW - 1) / TW), (unsigned)((cnt + kTailPts - 1) / kTailPts));
   hipLaunchKernelGGL(k_eval_wide_tail<TW>, grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key, tvec,
                      cnt, kTailPts, ys);
   HIP_TRY(hipGetLastError());
@@ -157,7 +161,38 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = (m - off < chunk) ? m - off : chunk;
     const dim3 grid((unsigned)grid_for(cnt, p->cus));
-    if (lam == 32)
+    if (p->eval_mode != DCF_EVAL_TTABLE) {  // stream head: 2.5 AES blocks per level instead of 4
+      if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
+      HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+      if (!p->d_rk2) {  // round keys of ciphers 0 and 17 (2 x 15 x 16 B), read into LDS by the kernel
+        HIP_TRY(hipMalloc(&p->d_rk2, 2 * sizeof(RoundKeys)));
+        HIP_TRY(hipMemcpy(p->d_rk2, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(p->d_rk2 + 15, &p->rk[17], sizeof(RoundKeys), hipMemcpyHostToDevice));
+      }
+      if (off == 0) {  // CW digest of this key (bytes [0,32) of each level's cw_s / cw_v, and cw_t)
+        if (p->dig_levels < nlev) {
+          if (p->d_dig) {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipFree(p->d_dig));
+          }
+          HIP_TRY(hipMalloc(&p->d_dig, (size_t)nlev * 65));
+          p->dig_levels = nlev;
+        }
+        hipLaunchKernelGGL(k_cw_digest, dim3((4 * nlev + 255) / 256), dim3(256), 0, st, cws, cwv, cwt, nlev, lam, K,
+                           key, (uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64);
+        HIP_TRY(hipGetLastError());
+      }
+      const uint64_t units = (cnt + kStreamUnit - 1) / kStreamUnit;
+      uint64_t blocks = (units + 15) / 16;
+      if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
+#define DCF_WHS(MH)                                                                                            \
+  hipLaunchKernelGGL((k_eval_wide_head_stream<2, MH>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab,     \
+                     p->d_rk2, (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
+                     lam, K, key, cnt, p->d_ctr, ys + off * lam, tvec)
+      if (lam == 32) DCF_WHS(true);
+      else DCF_WHS(false);
+#undef DCF_WHS
+    } else if (lam == 32)
       hipLaunchKernelGGL(k_eval_wide_head<true>, grid, dim3(kBlock), 0, st, p->d_tab, p->rk[0], p->rk[17], cws, cwv,
                          cwt, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes, lam, K, key, cnt,
                          ys + off * lam, tvec);
@@ -277,6 +312,8 @@ void dcf_prg_free(dcf_prg* p) {
     if (p->d_tab) (void)hipFree(p->d_tab);
     if (p->d_km) (void)hipFree(p->d_km);
     if (p->d_rk128) (void)hipFree(p->d_rk128);
+    if (p->d_rk2) (void)hipFree(p->d_rk2);
+    if (p->d_dig) (void)hipFree(p->d_dig);
     if (p->d_ws) (void)hipFree(p->d_ws);
     if (p->d_ctr) (void)hipFree(p->d_ctr);
     if (p->d_slabs) (void)hipFree(p->d_slabs);

@@ -1,0 +1,243 @@
+// kernels_wide_stream.h — LAMBDA >= 32 eval head with per-lane AES block
+// scheduling.  Included by dcf_hip.hip only (after kernels_stream.h).
+//
+// The head walks bytes [0,32) of the state (kernels_wide.h).  Per level the PRG
+// (prg.rs:42-73 at LAMBDA >= 32) encrypts four blocks, but a step needs only
+//   left  (x bit 0): B = E0(~s[0:16]) (v_L) and A = E0(s[0:16]) (s_L, t_L)
+//   right (x bit 1): B (t_R = lsb(B ^ ~s)[0]), D = E17(~s[16:32]) (v_R), C = E17(s[16:32]) (s_R)
+// i.e. 2.5 blocks per level on average instead of 4.  As in kernels_stream.h
+// each lane runs two points and each AES slot encrypts the next block its point
+// needs, in the order B, A (left) or B, D, C (right).  A slot's cipher is chosen
+// per lane: the schedules of ciphers 0 and 17 sit in LDS beside the T-tables and
+// each round reads the lane's key with one ds_read_b128 (as kernels_mmo.h does;
+// key words in SGPRs would need a v_mov per use for the per-lane select).
+// Outputs (y[0:32) and the t-vector for the tail) are identical to
+// k_eval_wide_head's.
+#pragma once
+
+#include "aes_lds.h"
+
+namespace {
+
+template <int NS>
+struct WideLane {
+  uint32_t s[NS][8], v[NS][8];           // bytes [0,32) of the seed and of the v accumulator
+  uint32_t t[NS], ph[NS], lev[NS], cur[NS], tR[NS], tacc[NS];
+  uint32_t pt[NS];                       // point index within this launch (<= 2^20); x row = xs + pt * N
+  bool alive[NS];
+};
+
+template <int NS>
+__device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, const uint8_t* __restrict__ s0p,
+                                           uint32_t party, const uint8_t* __restrict__ xs, uint32_t nbytes) {
+  const uint4* s4 = reinterpret_cast<const uint4*>(s0p);  // k.s0s[0] (lib.rs:168), L2-resident
+  const uint4 a = s4[0], b = s4[1];
+  L.s[i][0] = a.x; L.s[i][1] = a.y; L.s[i][2] = a.z; L.s[i][3] = a.w;
+  L.s[i][4] = b.x; L.s[i][5] = b.y; L.s[i][6] = b.z; L.s[i][7] = b.w;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) L.v[i][j] = 0u;
+  L.t[i] = party;
+  L.tacc[i] = party;  // row 0 of the t-vector is t_0 = party
+  L.tR[i] = 0u;
+  L.ph[i] = 0u;
+  L.lev[i] = 0u;
+  L.pt[i] = p;
+  L.alive[i] = true;
+  // x bits are needed before the next AES (they pick its block): one 32-bit word
+  // per 32 levels, the first one here.
+  L.cur[i] = load_bits32(xs + (uint64_t)p * nbytes, 0, nbytes);
+}
+
+template <int NS>
+__device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, uint64_t& unext, uint64_t& uend,
+                                            bool& exhausted, uint32_t* __restrict__ ctr, uint64_t nunits,
+                                            uint64_t count, const uint8_t* __restrict__ s0p, uint32_t party,
+                                            const uint8_t* __restrict__ xs, uint32_t nbytes) {
+  uint64_t need = __ballot(mine);
+  while (need) {
+    if (unext >= uend && !exhausted) {
+      const uint32_t u = dequeue_unit(ctr);
+      if (u >= nunits) {
+        exhausted = true;
+      } else {
+        unext = (uint64_t)u * kStreamUnit;
+        uend = min(unext + kStreamUnit, count);
+      }
+    }
+    if (exhausted && unext >= uend) {
+      if (mine) {
+        L.alive[i] = false;
+        L.lev[i] = 0u;  // keep the idle stream's CW loads in bounds
+      }
+      return;
+    }
+    const uint32_t rank = lane_rank(need);
+    const bool take = mine && (uint64_t)rank < uend - unext;
+    if (take) wide_start<NS>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes);
+    const uint64_t taken = __ballot(take);
+    unext += (uint64_t)__popcll(taken);
+    need &= ~taken;
+    mine = mine && !take;
+  }
+}
+
+// Compact CW digest of key `key` for the stream head: dig[4 l .. 4 l + 4) = cw_s[l][0:32) |
+// cw_v[l][0:32), dig_t[l] = cw_t[l].
+__global__ void k_cw_digest(const uint8_t* __restrict__ cw_s, const uint8_t* __restrict__ cw_v,
+                            const uint8_t* __restrict__ cw_t, const uint32_t nlev, const uint32_t lam,
+                            const uint64_t num_keys, const uint64_t key, uint4* __restrict__ dig,
+                            uint8_t* __restrict__ dig_t) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4 * nlev) return;
+  const uint32_t l = i >> 2, q = i & 3u;
+  const uint64_t ci = (uint64_t)l * num_keys + key;
+  const uint8_t* src = (q < 2 ? cw_s : cw_v) + ci * lam + 16u * (q & 1u);
+  dig[i] = *reinterpret_cast<const uint4*>(src);
+  if (q == 0) dig_t[l] = cw_t[ci];
+}
+
+// Single key `key` of a num_keys-key CWB; count <= 2^20 points per launch.
+template <int NS, bool MASK_HEAD>
+__global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
+    const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
+    const uint8_t* __restrict__ dig_t, const uint8_t* __restrict__ cw_np1,
+    const uint8_t* __restrict__ s0p, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint32_t lam, const uint64_t num_keys, const uint64_t key, const uint64_t count, uint32_t* __restrict__ ctr,
+    uint8_t* __restrict__ ys, uint32_t* __restrict__ tvec) {
+  __shared__ uint32_t lds[kLdsWords];
+  // Schedules of cipher 0 (slots 0..14) and cipher 17 (slots 23..37): 23 slots apart,
+  // so lanes reading the two never share a ds_read_b128 bank group.
+  __shared__ uint4 rks[23 + 15];
+  if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
+  lds_fill_tables(lds, tab);  // its barrier also publishes rks
+  const uint32_t lc = lane_const();
+  const uint32_t nlev = 8u * nbytes;
+  const uint64_t nunits = (count + kStreamUnit - 1) / kStreamUnit;
+  const uint32_t mlast = MASK_HEAD ? kMaskLast : 0xFFFFFFFFu;  // LAMBDA == 32: byte 31 is the cleared byte
+  uint64_t unext = 0, uend = 0;
+  bool exhausted = false;
+  WideLane<NS> L;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    L.alive[i] = false;
+    L.lev[i] = 0u;
+    L.ph[i] = 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i)
+    wide_refill<NS>(L, i, true, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes);
+
+  for (;;) {
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) any = any || L.alive[i];
+    if (!__ballot(any)) break;
+    // Block of this step: B (ph 0), then A (ph 1, left) or D (ph 1, right), C (ph 2).
+    uint32_t st[NS][4];
+    const uint4* rk[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
+      const uint32_t hi = (ph != 0u) & xb;                            // D or C: bytes [16,32), cipher 17
+      const uint32_t inv = 0u - ((ph == 0u) | ((ph == 1u) & xb));    // B or D: ~s
+      rk[i] = rks + 23u * hi;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[i][j] = (hi ? L.s[i][4 + j] : L.s[i][j]) ^ inv;
+    }
+    aes_tt_lk<14, NS>(st, rk, lds, lc);
+    // Correction words, needed only on the step that ends a level: bytes [0,32) of cw_s /
+    // cw_v from the compact per-key digest (64 B per level, 8 KiB, L1-resident; the CWB
+    // rows are LAMBDA bytes apart, one cache line per lane), loaded after the AES so
+    // they are not live across it.
+    uint4 cs[NS][2], cv[NS][2];
+    uint32_t ct[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
+      const bool end = L.alive[i] && (((ph == 1u) & (xb == 0u)) | (ph == 2u));
+      cs[i][0] = cs[i][1] = cv[i][0] = cv[i][1] = make_uint4(0u, 0u, 0u, 0u);
+      ct[i] = 0u;
+      if (end) {
+        const uint4* d4 = dig + 4u * L.lev[i];
+        cs[i][0] = d4[0]; cs[i][1] = d4[1];
+        cv[i][0] = d4[2]; cv[i][1] = d4[3];
+        ct[i] = dig_t[L.lev[i]];
+      }
+    }
+
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
+      const bool live = L.alive[i];
+      const uint32_t mB = 0u - (uint32_t)(live & (ph == 0u));
+      const uint32_t mA = 0u - (uint32_t)(live & (ph == 1u) & (xb == 0u));
+      const uint32_t mD = 0u - (uint32_t)(live & (ph == 1u) & (xb == 1u));
+      const uint32_t mC = 0u - (uint32_t)(live & (ph == 2u));
+      const uint32_t mBl = mB & (xb - 1u);  // B on a left step: v_L[0:16) = B ^ ~s
+      const uint32_t adv = (mA | mC) & 1u;   // this step finishes the level
+      const uint32_t am = 0u - adv, tm = 0u - L.t[i];
+      // d = E(in) ^ in: the PRG output block (prg.rs:57-62)
+      uint32_t d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t hi = (ph != 0u) & xb;
+        const uint32_t inv = 0u - ((ph == 0u) | ((ph == 1u) & xb));
+        d[j] = st[i][j] ^ ((hi ? L.s[i][4 + j] : L.s[i][j]) ^ inv);
+      }
+      L.tR[i] = mB ? (d[0] & 1u) : L.tR[i];  // t_R = lsb(B ^ ~s)[0] (prg.rs:64)
+      const uint32_t tb = ((mA ? d[0] : L.tR[i]) & 1u) ^ (L.t[i] & (ct[i] >> xb) & 1u);  // lib.rs:179-180
+      const uint32_t csw[8] = {cs[i][0].x, cs[i][0].y, cs[i][0].z, cs[i][0].w,
+                               cs[i][1].x, cs[i][1].y, cs[i][1].z, cs[i][1].w};
+      const uint32_t cvw[8] = {cv[i][0].x, cv[i][0].y, cv[i][0].z, cv[i][0].w,
+                               cv[i][1].x, cv[i][1].y, cv[i][1].z, cv[i][1].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // bytes [0,16): AES on the left branch only
+        // v ^= v_hat: B ^ ~s (left, at the B step) or ~s (right, at the C step); then t*cw.v
+        L.v[i][j] ^= (mBl & d[j]) ^ (mC & ~L.s[i][j]) ^ (am & tm & cvw[j]);
+        const uint32_t sn = mA ? d[j] : L.s[i][j];
+        L.s[i][j] = adv ? (sn ^ (tm & csw[j])) : L.s[i][j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // bytes [16,32): AES on the right branch only
+        const uint32_t msk = (j == 3) ? mlast : 0xFFFFFFFFu;
+        L.v[i][4 + j] ^= (((mD & d[j]) ^ (mA & ~L.s[i][4 + j])) & msk) ^ (am & tm & cvw[4 + j]);
+        const uint32_t sn = (mC ? d[j] : L.s[i][4 + j]) & msk;
+        L.s[i][4 + j] = adv ? (sn ^ (tm & csw[4 + j])) : L.s[i][4 + j];
+      }
+      L.t[i] = adv ? tb : L.t[i];
+      L.ph[i] = mB ? 1u : (mD ? 2u : 0u);
+      // t-vector: row r = lev + 1 gets t_r (byte r >> 2, bit r & 3), as k_eval_wide_head writes it
+      const uint32_t r = L.lev[i] + adv;
+      L.tacc[i] |= (am & L.t[i]) << (8u * ((r >> 2) & 3u) + (r & 3u));
+      uint32_t* trow = tvec + (uint64_t)L.pt[i] * kTWords;
+      const bool pdone = adv && r == nlev;
+      if (adv && ((r & 15u) == 15u || pdone)) {
+        trow[r >> 4] = L.tacc[i];
+        L.tacc[i] = 0u;
+      }
+      L.cur[i] <<= adv;
+      if (adv && (r & 31u) == 0u && r < nlev) L.cur[i] = load_bits32(xs + (uint64_t)L.pt[i] * nbytes, r >> 5, nbytes);
+      L.lev[i] = r;
+      if (pdone) {  // y[0:32) = v ^ s ^ t * cw_np1 (lib.rs:192)
+        const uint4* np4 = reinterpret_cast<const uint4*>(cw_np1 + key * lam);
+        const uint4 n0 = np4[0], n1 = np4[1];
+        const uint32_t nw[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+        const uint32_t tn = 0u - L.t[i];
+        uint32_t y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = L.v[i][j] ^ L.s[i][j] ^ (tn & nw[j]);
+        uint4* y4 = reinterpret_cast<uint4*>(ys + (uint64_t)L.pt[i] * lam);
+        y4[0] = make_uint4(y[0], y[1], y[2], y[3]);
+        y4[1] = make_uint4(y[4], y[5], y[6], y[7]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const bool done = L.alive[i] && L.lev[i] == nlev;
+      if (__ballot(done))
+        wide_refill<NS>(L, i, done, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes);
+    }
+  }
+}
+
+}  // namespace
