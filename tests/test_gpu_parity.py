@@ -227,13 +227,16 @@ def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P, mode):
         assert not (y0h[::P] ^ y1h[::P]).any()
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("lam,nb,m", [(32, 2, 70), (48, 3, 65), (64, 16, 33), (112, 4, 130), (1024, 2, 40),
-                                      (4096, 16, 12)])
-def test_wide_eval_random_vs_oracle(dcf, lam, nb, m):
-    """LAMBDA >= 32: head/tail kernels vs the literal oracle, both parties, both bounds."""
+                                      (4096, 16, 12), (272, 5, 600)])
+def test_wide_eval_random_vs_oracle(dcf, lam, nb, m, mode):
+    """LAMBDA >= 32: head/tail kernels vs the literal oracle, both parties, both bounds.
+    mode 0: stream head (default), mode 1: lockstep T-table head."""
     rng = np.random.default_rng(lam * 7 + nb)
     keys = [rng.bytes(32) for _ in range(18)]
     prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    prg.set_eval_mode(mode)
     d = dcf.DcfImpl(nb, lam, prg)
     for bound in (0, 1):
         alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
