@@ -424,6 +424,27 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   // evals/s vs 353 M hybrid, 332 M T-table).  Many keys -> lockstep T-table, whose waves
   // share one key's CWs through scalar loads (C5: 264 M vs 206 M evals/s with streams,
   // whose lanes sit on different levels and miss L1 on the level-major CW layout).
+  // Small batches (fewer points than two per lane of the GPU) are latency-bound: one
+  // point's 8N levels run back to back, so the lockstep walk (A and B of a level in
+  // one AES pass: 8N passes) beats the stream engine (~12N passes), and the points are
+  // spread over every CU with workgroups just big enough (C1, 100k points: 3.2 -> see
+  // DESIGN.md).
+  if (mode == DCF_EVAL_AUTO && total < (uint64_t)p->cus * kBlock * 2) {
+    uint64_t threads = (total + p->cus - 1) / p->cus;
+    threads = ((threads + 63) / 64) * 64;
+    if (threads > (uint64_t)kBlock) threads = kBlock;
+    const dim3 g2((unsigned)((total + threads - 1) / threads)), b2((unsigned)threads);
+#define DCF_SMALL(MODE)                                                                                           \
+  hipLaunchKernelGGL(k_eval16<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s,    \
+                     (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk, (uint4*)ys,          \
+                     (uint32_t*)nullptr)
+    if (num_keys == 1) DCF_SMALL(0);
+    else if (ppk % 64 == 0) DCF_SMALL(1);
+    else DCF_SMALL(2);
+#undef DCF_SMALL
+    HIP_TRY(hipGetLastError());
+    return DCF_OK;
+  }
   if (mode == DCF_EVAL_AUTO) mode = (num_keys == 1) ? DCF_EVAL_STREAM : DCF_EVAL_TTABLE;
   // Single-key T-table eval also runs in the hybrid kernel, with every wave on
   // the T-table engine: its 512-point work units measured 13 % faster than
@@ -496,18 +517,19 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     else
       hipLaunchKernelGGL(k_eval16_bs<false>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
                          (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
-  } else if (num_keys == 1)
-    hipLaunchKernelGGL(k_eval16<0>, grid, block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
-                       (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)1, (uint64_t)ppk,
-                       (uint4*)ys);
-  else if (ppk % 64 == 0)
-    hipLaunchKernelGGL(k_eval16<1>, grid, block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
-                       (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,
-                       (uint64_t)ppk, (uint4*)ys);
-  else
-    hipLaunchKernelGGL(k_eval16<2>, grid, block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
-                       (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,
-                       (uint64_t)ppk, (uint4*)ys);
+  } else {  // lockstep T-table, 64-point units from the work counter
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+    if ((total + 63) / 64 > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "more than 2^32 64-point units");
+#define DCF_TT(MODE)                                                                                         \
+  hipLaunchKernelGGL(k_eval16<MODE>, grid, block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,               \
+                     (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk, \
+                     (uint4*)ys, p->d_ctr)
+    if (num_keys == 1) DCF_TT(0);
+    else if (ppk % 64 == 0) DCF_TT(1);
+    else DCF_TT(2);
+#undef DCF_TT
+  }
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }

@@ -70,18 +70,31 @@ __device__ __forceinline__ uint4 tt_eval_one(const uint32_t* lds, uint32_t lc, c
                     v[3] ^ s[3] ^ (tm & np.w));
 }
 
+// Work distribution: with ctr == nullptr a grid-stride loop (small batches: every
+// wave runs once); otherwise waves take 64-point units from the counter, so the
+// waves of a CU drift apart and their AES rounds do not hit the LDS in lockstep
+// bursts (C5: see DESIGN.md).
+__device__ __forceinline__ uint64_t next_wave_base(uint32_t* __restrict__ ctr, uint64_t base, uint64_t stride) {
+  if (!ctr) return base + stride;
+  uint32_t u = 0;
+  if ((threadIdx.x & 63u) == 0) u = atomicAdd(ctr, 1u);
+  return (uint64_t)__builtin_amdgcn_readfirstlane(u) * 64u;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock, 1) void k_eval16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
-    const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys) {
+    const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys, uint32_t* __restrict__ ctr) {
   __shared__ uint32_t lds[kLdsWords];
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
   const uint64_t total = num_keys * points_per_key;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += stride) {
+  const uint64_t first = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+  for (uint64_t base = ctr ? next_wave_base(ctr, 0, 0) : first; base < total;
+       base = next_wave_base(ctr, base, stride)) {
     const uint64_t g = base + (threadIdx.x & 63u);
     const bool live = g < total;
     const uint64_t gg = live ? g : total - 1;
