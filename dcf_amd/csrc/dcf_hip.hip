@@ -96,6 +96,8 @@ struct dcf_prg {
   uint4* d_rk128 = nullptr;   // MMO: AES-128 schedules of ciphers 0..3 (4 x 11 round keys)
   uint4* d_rk2 = nullptr;     // LAMBDA >= 32 stream head: AES-256 schedules of ciphers 0 and 17
   uint8_t* d_dig = nullptr;   // LAMBDA >= 32 stream head: compact CW digest of the current key
+  uint8_t* d_kdig = nullptr;  // LAMBDA = 16 multi-key stream eval: key-major CW digest
+  size_t kdig_bytes = 0;
   uint32_t dig_levels = 0;
   uint32_t* d_tab = nullptr;  // T0..T3 (4 KiB) on the device
   uint4* d_km = nullptr;      // bitsliced round-key masks of cipher 0 (15 x 4 x 8 uint4)
@@ -314,6 +316,7 @@ void dcf_prg_free(dcf_prg* p) {
     if (p->d_rk128) (void)hipFree(p->d_rk128);
     if (p->d_rk2) (void)hipFree(p->d_rk2);
     if (p->d_dig) (void)hipFree(p->d_dig);
+    if (p->d_kdig) (void)hipFree(p->d_kdig);
     if (p->d_ws) (void)hipFree(p->d_ws);
     if (p->d_ctr) (void)hipFree(p->d_ctr);
     if (p->d_slabs) (void)hipFree(p->d_slabs);
@@ -445,7 +448,9 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     HIP_TRY(hipGetLastError());
     return DCF_OK;
   }
-  if (mode == DCF_EVAL_AUTO) mode = (num_keys == 1) ? DCF_EVAL_STREAM : DCF_EVAL_TTABLE;
+  if (mode == DCF_EVAL_AUTO) mode = (num_keys == 1 || n_bytes <= 32) ? DCF_EVAL_STREAM : DCF_EVAL_TTABLE;
+  if (mode == DCF_EVAL_STREAM && num_keys > 1 && n_bytes > 32)
+    return fail(DCF_ERR_UNSUPPORTED, "multi-key stream eval: N <= 32");
   // Single-key T-table eval also runs in the hybrid kernel, with every wave on
   // the T-table engine: its 512-point work units measured 13 % faster than
   // k_eval16<0>'s grid-stride loop (r01 sweep, 331.7 vs 292 M evals/s).
@@ -496,9 +501,29 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     uint64_t blocks = (units + 15) / 16;
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
     const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16, multi = num_keys > 1;
+    const uint4* scs = cws;
+    const uint8_t* sct = cwt;
+    if (multi) {  // key-major digest of the K keys (kernels_stream.h)
+      const size_t need = (size_t)num_keys * n * 33;
+      if (p->kdig_bytes < need) {
+        if (p->d_kdig) {
+          HIP_TRY(hipStreamSynchronize(st));
+          HIP_TRY(hipFree(p->d_kdig));
+          p->d_kdig = nullptr;
+          p->kdig_bytes = 0;
+        }
+        HIP_TRY(hipMalloc(&p->d_kdig, need));
+        p->kdig_bytes = need;
+      }
+      hipLaunchKernelGGL(k_cw_keymajor, dim3((unsigned)((num_keys + 15) / 16)), dim3(256), 0, st, cws, cwv, cwt,
+                         (uint32_t)n, (uint64_t)num_keys, (uint4*)p->d_kdig, p->d_kdig + (size_t)num_keys * n * 32);
+      HIP_TRY(hipGetLastError());
+      scs = (const uint4*)p->d_kdig;
+      sct = p->d_kdig + (size_t)num_keys * n * 32;
+    }
 #define DCF_STREAM(XR, MK)                                                                                    \
-  hipLaunchKernelGGL((k_eval16_stream<2, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], cws, \
-                     cwv, cwt, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,  \
+  hipLaunchKernelGGL((k_eval16_stream<2, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], scs, \
+                     cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,  \
                      (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys)
     if (xreg && multi) DCF_STREAM(true, true);
     else if (xreg) DCF_STREAM(true, false);

@@ -13,13 +13,18 @@
 // one wave sit on different levels, so correction words are per-lane vector
 // loads (L1/L2-resident: 4.2 KB per key) instead of scalar loads.
 //
+// Multi-key (MULTI): lanes on different levels of one key would each touch a
+// different line of the level-major CWB (K * 16 B apart), so the host first
+// builds a key-major digest — dig[key][level] = cw_s | cw_v (32 B), dig_t[key][level]
+// — and the kernel reads a key's 4 KiB contiguously (k_cw_keymajor below).
+//
 // Work: each wave takes kStreamUnit consecutive points at a time from one
 // global counter and hands them to its finished streams (wave-aggregated, in
 // uniform control flow), so a wave's x reads and y writes stay within a few KiB;
 // a stream with nothing left goes idle and the wave exits when all its streams
 // are idle.  (A static strided assignment of points to streams measured 25 %
 // slower: scattered 16-byte x reads and y writes.)  Multi-key (MULTI): point p
-// belongs to key p / points_per_key; CW index = level * K + key.
+// belongs to key p / points_per_key; CW index = key * 8N + level into the digest.
 #pragma once
 
 #include "aes_lds.h"
@@ -55,7 +60,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
   L.t[i] = party;  // lib.rs:169
   L.ph[i] = 0u;
   L.lev[i] = 0u;
-  L.ci[i] = k;
+  L.ci[i] = k * (8u * nbytes);  // key-major digest row (MULTI); level 0 of the single key otherwise
   L.key[i] = k;
   L.pt[i] = p;
   L.alive[i] = true;
@@ -112,6 +117,37 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
   }
 }
 
+// Key-major CW digest for the multi-key stream engine: one workgroup per 16 keys
+// stages their 8N levels through LDS so both the level-major reads (16 keys x 16 B
+// per row) and the key-major writes (4 KiB per key) are contiguous.
+__global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
+                                                     const uint8_t* __restrict__ cw_t, const uint32_t nlev,
+                                                     const uint64_t num_keys, uint4* __restrict__ dig,
+                                                     uint8_t* __restrict__ dig_t) {
+  __shared__ uint4 sh[16 * 256 * 2];  // [key][level][s|v], nlev <= 256
+  __shared__ uint8_t sht[16 * 256];
+  const uint64_t k0 = (uint64_t)blockIdx.x * 16;
+  const uint32_t nk = (uint32_t)min<uint64_t>(16, num_keys - k0);
+  for (uint32_t it = threadIdx.x; it < nlev * 16; it += blockDim.x) {
+    const uint32_t l = it >> 4, kk = it & 15u;
+    if (kk < nk) {
+      const uint64_t src = (uint64_t)l * num_keys + k0 + kk;
+      sh[(kk * 256 + l) * 2] = cw_s[src];
+      sh[(kk * 256 + l) * 2 + 1] = cw_v[src];
+      sht[kk * 256 + l] = cw_t[src];
+    }
+  }
+  __syncthreads();
+  for (uint32_t it = threadIdx.x; it < nk * nlev * 2; it += blockDim.x) {
+    const uint32_t kk = it / (nlev * 2), r = it % (nlev * 2);
+    dig[(k0 + kk) * nlev * 2 + r] = sh[kk * 512 + r];
+  }
+  for (uint32_t it = threadIdx.x; it < nk * nlev; it += blockDim.x) {
+    const uint32_t kk = it / nlev, l = it % nlev;
+    dig_t[(k0 + kk) * nlev + l] = sht[kk * 256 + l];
+  }
+}
+
 template <int NS, bool XREG, bool MULTI, int WG = kBlock>
 __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
@@ -124,7 +160,6 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
   const uint64_t nunits = (total + kStreamUnit - 1) / kStreamUnit;
-  const uint64_t K = MULTI ? num_keys : 1;
   uint64_t unext = 0, uend = 0;
   bool exhausted = false;
   const uint4 s0v = s0s[0];
@@ -150,8 +185,13 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     uint32_t ct[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      cs[i] = cw_s[L.ci[i]];
-      cv[i] = cw_v[L.ci[i]];
+      if (MULTI) {  // cw_s = digest (2 uint4 per level), cw_t = digest t bytes
+        cs[i] = cw_s[2 * L.ci[i]];
+        cv[i] = cw_s[2 * L.ci[i] + 1];
+      } else {
+        cs[i] = cw_s[L.ci[i]];
+        cv[i] = cw_v[L.ci[i]];
+      }
       ct[i] = cw_t[L.ci[i]];
     }
     // Slot i encrypts ~s (B) in phase 0 and s (A) in phase 1.
@@ -210,7 +250,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
       else if (bnd && nl < nlev)
         L.cur[i] = load_bits32(L.xp[i], nl >> 5, nbytes);
       L.lev[i] = nl;
-      L.ci[i] += adv ? K : 0;
+      L.ci[i] += adv;
     }
     // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.
 #pragma unroll
