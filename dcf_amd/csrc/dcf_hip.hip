@@ -377,10 +377,17 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
     }
     return DCF_OK;
   }
+  // Large batches: 64-key units from the work counter (waves drift apart, as in k_eval16).
+  uint32_t* ctr = nullptr;
+  if (num_keys >= (uint64_t)p->cus * kBlock * 2 && (num_keys + 63) / 64 <= 0xFFFFFFFFull) {
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), (hipStream_t)stream));
+    ctr = p->d_ctr;
+  }
   hipLaunchKernelGGL(k_gen16, dim3((unsigned)grid_for(num_keys, p->cus)), dim3(kBlock), 0, (hipStream_t)stream,
                      p->d_tab, p->rk[0], alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1,
                      (uint32_t)bound, (uint32_t)n_bytes, (uint64_t)num_keys, (uint4*)cws, (uint4*)cwv, cwt,
-                     (uint4*)np1);
+                     (uint4*)np1, ctr);
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }

@@ -115,14 +115,16 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ alpha,
     const uint4* __restrict__ beta, const uint4* __restrict__ s0_0, const uint4* __restrict__ s0_1,
     const uint32_t bound, const uint32_t nbytes, const uint64_t num_keys, uint4* __restrict__ cw_s,
-    uint4* __restrict__ cw_v, uint8_t* __restrict__ cw_t, uint4* __restrict__ cw_np1) {
+    uint4* __restrict__ cw_v, uint8_t* __restrict__ cw_t, uint4* __restrict__ cw_np1, uint32_t* __restrict__ ctr) {
   __shared__ uint32_t lds[kLdsWords];
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
   const uint32_t nchunk = (nbytes + 3u) >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < num_keys; base += stride) {
+  const uint64_t first = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+  for (uint64_t base = ctr ? next_wave_base(ctr, 0, 0) : first; base < num_keys;
+       base = next_wave_base(ctr, base, stride)) {
     const uint64_t g = base + (threadIdx.x & 63u);
     const bool live = g < num_keys;
     const uint64_t k = live ? g : num_keys - 1;

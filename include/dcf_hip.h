@@ -39,8 +39,10 @@
  * keeps no reference to caller buffers once the stream has passed the call.
  * Host entry points take host pointers and are synchronous.
  *
- * Threading: one dcf_prg may be used by one host thread at a time; distinct
- * dcf_prg objects are independent.  Multi-GPU = one process (or one dcf_prg)
+ * Threading: one dcf_prg may be used by one host thread at a time, and its
+ * device calls must not overlap on different streams (its work counter and
+ * scratch buffers are per dcf_prg; calls queued on one stream are fine);
+ * distinct dcf_prg objects are independent.  Multi-GPU = one process (or one dcf_prg)
  * per device; the path shards by points/keys with no collective.
  */
 #ifndef DCF_HIP_H

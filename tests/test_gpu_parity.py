@@ -327,3 +327,41 @@ def test_full_domain_eval_vs_oracle(dcf, nb, lam):
     a = int.from_bytes(alpha, "big")
     rec = ys[0] ^ ys[1]
     assert not rec[a:].any() and (rec[:a] == np.frombuffer(beta, np.uint8)).all()
+
+
+@pytest.mark.parametrize("nb", [2, 16])
+def test_gen_batch_large_counter_path(dcf, nb):
+    """>= 2^19 keys: batched gen takes 64-key units from the work counter; the multi-key
+    eval runs the stream engine over the key-major digest.  A sample of keys vs the oracle."""
+    import torch
+    K, P = 600_000 if nb == 2 else 540_000, 1
+    rng = np.random.default_rng(4242 + nb)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, Po = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    d = dcf.DcfImpl(nb, 16, prg)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(nb)
+    r = lambda *s: torch.randint(0, 256, s, dtype=torch.uint8, device="cuda", generator=g)  # noqa: E731
+    alpha, beta, s0, s1, xs = r(K, nb), r(K, 16), r(K, 16), r(K, 16), r(K * P, nb)
+    cwb = d.gen_batch_device(alpha, beta, s0, s1, dcf.BoundState.LtBeta)
+    y0 = d.eval_multikey_device(False, cwb, s0, xs, P)
+    y1 = d.eval_multikey_device(True, cwb, s1, xs, P)
+    torch.cuda.synchronize()
+    n = 8 * nb
+    cw = cwb.cpu().numpy()
+    cws = cw[:n * K * 16].reshape(n, K, 16)
+    A, B, S0, S1, X = (t.cpu().numpy() for t in (alpha, beta, s0, s1, xs))
+    Y0, Y1 = y0.cpu().numpy(), y1.cpu().numpy()
+    for key in sorted(set([0, K - 1] + list(rng.integers(0, K, 24)))):
+        ok = O.gen(Po, A[key].tobytes(), B[key].tobytes(), S0[key].tobytes(), S1[key].tobytes(), 0)
+        assert np.array_equal(cws[:, key], ok.cw_s), key
+        assert np.array_equal(Y0[key:key + 1], O.eval_(Po, 0, ok, S0[key].tobytes(), X[key:key + 1]))
+        assert np.array_equal(Y1[key:key + 1], O.eval_(Po, 1, ok, S1[key].tobytes(), X[key:key + 1]))
+    # reconstruction on every key: y0 ^ y1 = beta * [x < alpha]
+    diff = X != A
+    first = np.where(diff.any(1), diff.argmax(1), nb)
+    lt = np.zeros(K, bool)
+    has = first < nb
+    lt[has] = X[has, first[has]] < A[has, first[has]]
+    rec = Y0 ^ Y1
+    assert np.array_equal(rec[lt], B[lt]) and not rec[~lt].any()
