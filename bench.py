@@ -93,6 +93,26 @@ def blocks_per_eval(n_bytes: int, lam: int) -> int:
     return (2 if lam == 16 else 4) * 8 * n_bytes
 
 
+HBM_WRITE_BPS = 8.0e12  # MI355X_MICROARCH.md HBM peak (a sequential fill measures 6.9 TB/s, scripts/hbm_write_bw.py)
+
+
+def wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine):
+    """LAMBDA >= 32 (C4): head and tail run back to back, so the bound is the sum of the
+    head's AES time at the T-table LDS peak and the output's HBM write time."""
+    t_aes = m * exec_bpe / PEAK_TT_BLOCKS
+    t_out = m * lam / HBM_WRITE_BPS
+    peak = m / (t_aes + t_out)
+    achieved = m / kern_s
+    return {"bound": "lds+hbm", "kernel": kernel, "engine": engine, "achieved": achieved / 1e6,
+            "peak": peak / 1e6, "unit": "M evals/s", "frac": achieved / peak, "traffic": None,
+            "algorithmic_bytes": m * (nb + lam), "kernel_ms": kern_s * 1e3, "hbm_GBps": m * (nb + lam) / kern_s / 1e9,
+            "executed_blocks_per_eval": exec_bpe, "reference_blocks_per_eval": bpe,
+            "aes_blocks_per_s_executed": m * exec_bpe / kern_s,
+            "note": "peak = 1 / (executed AES-256 blocks per eval / 87.8 G blocks/s (T-table LDS bound) + "
+                    "LAMBDA bytes per eval / 8 TB/s HBM write): the head (AES walk over bytes [0,32)) and the tail "
+                    "(GF(2) combination writing bytes [32, LAMBDA)) run back to back"}
+
+
 def zero_bits(xs: torch.Tensor) -> int:
     """Number of 0 bits in the points = left steps = the A blocks the stream engine
     encrypts on top of one B block per level (kernels_stream.h)."""
@@ -231,8 +251,15 @@ def run_eval(args, world, rank):
     # Blocks the dominant kernel actually encrypts per eval: the reference count, except the
     # stream engine, which encrypts B on every level and A on left (x bit 0) levels only.
     exec_bpe = (8 * nb + zero_bits(xs) / m) if engine == "stream" else bpe  # mmo: 2 AES-128 per level
+    if lam > 16:
+        # LAMBDA >= 32: the stream head encrypts B, A (left) or B, D, C (right) per level, and the
+        # tail writes LAMBDA - 32 output bytes per eval: time bound = AES (LDS) + output (HBM write).
+        engine = "stream-head" if args.eval_mode != 1 else "ttable"
+        if engine == "stream-head":
+            exec_bpe = 3 * 8 * nb - zero_bits(xs) / m
     per_gpu_blocks = m * exec_bpe / kern_s
-    kernel = KERNEL[engine] if lam == 16 else "k_eval_wide_head+k_eval_wide_tail"
+    kernel = KERNEL.get(engine, "k_eval16") if lam == 16 else (
+        "k_eval_wide_head_stream+k_eval_wide_tail" if engine == "stream-head" else "k_eval_wide_head+k_eval_wide_tail")
     peak = engine_peak(engine)
     out = {
         "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
@@ -244,7 +271,7 @@ def run_eval(args, world, rank):
                    "n_bytes": nb, "lambda": lam, "points_per_gpu": m, "global_points": m * world,
                    "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
         "aes_blocks_per_s": value * bpe,
-        "roofline": {
+        "roofline": wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine) if lam > 16 else {
             "bound": "lds" if engine in ("ttable", "stream", "mmo") else ("valu" if engine == "bitsliced" else "lds+valu"),
             "kernel": kernel, "engine": engine,
             "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-128 blocks/s" if engine == "mmo" else "G AES-256 blocks/s",
