@@ -200,27 +200,23 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
   // the head and are skipped): unaligned 256-byte pieces split cache lines between
   // neighbouring tiles and measured 20 % slower HBM writes.
   const uint32_t byte0 = (uint32_t)blockIdx.x * TW;
-  // singles and zero entries
-  for (uint32_t it = threadIdx.x; it < nch * 16u * LP; it += blockDim.x) {
-    const uint32_t q = it % LP, e = (it / LP) & 15u, c = it / (LP * 16);
-    uint4 val = make_uint4(0u, 0u, 0u, 0u);
-    if (e && !(e & (e - 1))) val = w_row_piece(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, 4 * c + (31 - __clz(e)),
-                         byte0 + 16 * q);
-    if (!e || !(e & (e - 1))) G[it] = val;
-  }
-  __syncthreads();
-  for (uint32_t it = threadIdx.x; it < nch * 16u * LP; it += blockDim.x) {
-    const uint32_t q = it % LP, e = (it / LP) & 15u, c = it / (LP * 16);
-    if (e & (e - 1)) {
-      uint4 a = make_uint4(0u, 0u, 0u, 0u);
+  // Tables: one thread per (chunk, piece) loads its chunk's 4 W-row pieces (all
+  // loads in flight at once) and writes the 16 XOR combinations; one barrier.
+  for (uint32_t it = threadIdx.x; it < nch * LP; it += blockDim.x) {
+    const uint32_t qq = it % LP, c = it / LP;
+    uint4 w[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (e & (1u << k)) {
-          const uint4 b = G[(c * 16 + (1u << k)) * LP + q];
-          a.x ^= b.x; a.y ^= b.y; a.z ^= b.z; a.w ^= b.w;
-        }
-      G[it] = a;
+    for (int k = 0; k < 4; ++k) w[k] = w_row_piece(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, 4 * c + k, byte0 + 16 * qq);
+    uint4* dst = G + (c * 16) * LP + qq;
+    uint4 e[16];
+    e[0] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int x = 1; x < 16; ++x) {  // e[x] = e[x without its lowest bit] ^ w[lowest bit]
+      const uint4 a0 = e[x & (x - 1)], b0 = w[__builtin_ctz(x)];
+      e[x] = make_uint4(a0.x ^ b0.x, a0.y ^ b0.y, a0.z ^ b0.z, a0.w ^ b0.w);
     }
+#pragma unroll
+    for (int x = 0; x < 16; ++x) dst[x * LP] = e[x];
   }
   __syncthreads();
   const uint32_t q = threadIdx.x % LP;
