@@ -215,11 +215,21 @@ def run_eval(args, world, rank):
     d = dcf_amd.DcfImpl(nb, lam, prg)
     cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002)
     s0 = seeds[0].contiguous()
+    s1 = seeds[1].contiguous()
     xs = gen_points(m, nb, rank, 0xDCF0003)
     ys = torch.empty((m, lam), dtype=torch.uint8, device="cuda")
+    # C1 (benches/dcf_batch_eval.rs shape) evaluates both parties per step.
+    parties = 2 if args.workload == "c1" else 1
+    ys1 = torch.empty_like(ys) if parties == 2 else None
+
+    def step():
+        d.eval_device(False, cwb, s0, xs, ys)
+        if parties == 2:
+            d.eval_device(True, cwb, s1, xs, ys1)
+
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
-        d.eval_device(False, cwb, s0, xs, ys)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -228,19 +238,19 @@ def run_eval(args, world, rank):
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        d.eval_device(False, cwb, s0, xs, ys)
+        step()
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # one k_eval16 launch per step
+    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps / parties  # per eval launch
     t = torch.tensor([wall], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
-    total_evals = m * world * args.steps
+    total_evals = m * world * args.steps * parties
     value = total_evals / wall
     bpe = blocks_per_eval(nb, lam)
     engine = ENGINE[args.eval_mode] if lam == 16 else "ttable"
@@ -267,7 +277,8 @@ def run_eval(args, world, rank):
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"{args.workload.upper()}: N={nb} ({8 * nb}-bit x), lambda={lam}, "
                                f"{'Aes128MatyasMeyerOseasPrg' if args.prg == 'mmo' else 'Aes256HirosePrg'} "
-                               f"({len(keys)} AES keys), 1 key, {m} points/GPU in HBM, party 0, eval only",
+                               f"({len(keys)} AES keys), 1 key, {m} points/GPU in HBM, "
+                               f"{'both parties' if parties == 2 else 'party 0'}, eval only",
                    "n_bytes": nb, "lambda": lam, "points_per_gpu": m, "global_points": m * world,
                    "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
         "aes_blocks_per_s": value * bpe,

@@ -245,6 +245,78 @@ __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* co
   aes_tt_lk<10, NB>(st, rk, lds, lc);
 }
 
+// ------------------------------------------------------------------------
+// Two-table variant (64 KiB of LDS instead of 128: room for two 640-thread
+// workgroups per CU).  Only T0 and T2 are stored, 32 replicas each, at
+//   addr(T, b, lane) = b * 256 + (T >> 1) * 128 + (lane & 31) * 4   (T in {0, 2});
+// T1 = rotl8(T0) and T3 = rotl8(T2), and rotation distributes over XOR, so a
+// column is T0[a] ^ T2[d] ^ rotl8(T0[c] ^ T2[e]) ^ rk: 4 lookups, 4 VALU.
+// ------------------------------------------------------------------------
+constexpr int kLdsWords2 = 16384;  // 64 KiB
+
+__device__ __forceinline__ void lds_fill_tables2(uint32_t* lds, const uint32_t* __restrict__ tab) {
+  for (int idx = threadIdx.x; idx < kLdsWords2; idx += blockDim.x) {
+    const int b = idx >> 6, half = (idx >> 5) & 1;
+    lds[idx] = tab[(2 * half) * 256 + b];
+  }
+  __syncthreads();
+}
+
+// Lookup of T0 (H = 0) or T2 (H = 1) at state byte K of w.
+template <int H, int K>
+__device__ __forceinline__ uint32_t lk2(const uint32_t* lds, uint32_t w, uint32_t lc) {
+  constexpr uint32_t sel = (H ? 1u : 0u) | ((4u + K) << 8) | (0x0cu << 16) | (0x0cu << 24);
+  const uint32_t addr = __builtin_amdgcn_perm(w, lc, sel);
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + addr);
+}
+
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+
+template <int NB>
+__device__ __forceinline__ void aes256_tt2(uint32_t (&st)[NB][4], const RoundKeys& rk, const uint32_t* lds,
+                                           uint32_t lc) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] ^= rk.w[j];
+#pragma unroll
+  for (int r = 1; r < 14; ++r) {
+    uint32_t o[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t a = lk2<0, 0>(lds, st[b][j], lc);            // T0[byte 0 of col j]
+        const uint32_t c = lk2<0, 1>(lds, st[b][(j + 1) & 3], lc);  // T1 = rotl8(T0)
+        const uint32_t d = lk2<1, 2>(lds, st[b][(j + 2) & 3], lc);  // T2
+        const uint32_t e = lk2<1, 3>(lds, st[b][(j + 3) & 3], lc);  // T3 = rotl8(T2)
+        o[b][j] = xor3(a, d, rotl8(c ^ e)) ^ rk.w[4 * r + j];
+      }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+  // Final round: S(x) is byte 1 of T0[x].
+  uint32_t o[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t a = lk2<0, 0>(lds, st[b][j], lc);
+      const uint32_t c = lk2<0, 1>(lds, st[b][(j + 1) & 3], lc);
+      const uint32_t d = lk2<0, 2>(lds, st[b][(j + 2) & 3], lc);
+      const uint32_t e = lk2<0, 3>(lds, st[b][(j + 3) & 3], lc);
+      const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0501u);  // byte0 = S(a), byte1 = S(c)
+      const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x05010c0cu);  // byte2 = S(d), byte3 = S(e)
+      o[b][j] = xor3(lo, hi, rk.w[56 + j]);
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+}
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }
 
 // 32 bits of a byte string starting at byte 4c, Msb0 order (lib.rs:106,181),

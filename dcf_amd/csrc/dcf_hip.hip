@@ -532,6 +532,15 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   hipLaunchKernelGGL((k_eval16_stream<2, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], scs, \
                      cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,  \
                      (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys)
+#ifdef DCF_STREAM_TT2
+    if (xreg && !multi) {
+      uint64_t b2 = (units + 9) / 10;
+      if (b2 > 2 * (uint64_t)p->cus) b2 = 2 * (uint64_t)p->cus;
+      hipLaunchKernelGGL((k_eval16_stream<2, true, false, 640, true>), dim3((unsigned)b2), dim3(640), 0, st, p->d_tab,
+                         p->rk[0], scs, cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes,
+                         (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys);
+    } else
+#endif
     if (xreg && multi) DCF_STREAM(true, true);
     else if (xreg) DCF_STREAM(true, false);
     else if (multi) DCF_STREAM(false, true);

@@ -148,15 +148,19 @@ __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ c
   }
 }
 
-template <int NS, bool XREG, bool MULTI, int WG = kBlock>
+// TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.
+template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false>
 __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
     uint4* __restrict__ ys) {
-  __shared__ uint32_t lds[kLdsWords];
-  lds_fill_tables(lds, tab);
+  __shared__ uint32_t lds[TT2 ? kLdsWords2 : kLdsWords];
+  if (TT2)
+    lds_fill_tables2(lds, tab);
+  else
+    lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
   const uint64_t nunits = (total + kStreamUnit - 1) / kStreamUnit;
@@ -202,7 +206,10 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[i][j] = L.s[i][j] ^ inv;
     }
-    aes256_tt<NS>(st, rk, lds, lc);
+    if (TT2)
+      aes256_tt2<NS>(st, rk, lds, lc);
+    else
+      aes256_tt<NS>(st, rk, lds, lc);
     // Pin the CW loads above the update: without this the compiler sinks the
     // cw_t load into the (divergent) level-done path and waits on it there.
 #pragma unroll
