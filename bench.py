@@ -355,12 +355,90 @@ def run_c5(args, world, rank):
             "config": {"workload": f"C5: {K} keys x {P} points per GPU, N={nb}, lambda={lam}"}}
 
 
+def run_fd(args, world, rank):
+    """Full-domain eval: y for every x in [0, 2^(8N)), N = 4 by default
+    (the 32-bit fixed-point shape: 2^32 outputs, 64 GiB), party 0, one key.  Ranks
+    evaluate the same key (replicas: the tree expansion has no point slice to shard)."""
+    nb, lam = args.n_bytes, 16
+    rng = np.random.default_rng(0xDCF0001)
+    mmo = args.prg == "mmo"
+    if mmo:
+        keys = [rng.bytes(16) for _ in range(4)]
+        prg = dcf_amd.Aes128MatyasMeyerOseasPrg(keys, lam, device=torch.cuda.current_device())
+    else:
+        keys = [rng.bytes(32) for _ in range(2)]
+        prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
+    prg_name = "Aes128MatyasMeyerOseasPrg" if mmo else "Aes256HirosePrg"
+    d = dcf_amd.DcfImpl(nb, lam, prg)
+    cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002)
+    s0 = seeds[0].contiguous()
+    npts = 1 << (8 * nb)
+    ys = torch.empty((npts, lam), dtype=torch.uint8, device="cuda")
+    for _ in range(args.warmup):
+        d.eval_full_domain_device(False, cwb, s0, ys)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        d.eval_full_domain_device(False, cwb, s0, ys)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
+    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    value = npts * world * args.steps / wall
+    # one PRG call per internal node of the tree: A, B (Hirose) or 4 AES-128 blocks (MMO)
+    blocks = (4 if mmo else 2) * (npts - 1)
+    peak = PEAK_MMO_BLOCKS if mmo else PEAK_TT_BLOCKS
+    # a sample against the oracle (checker only): the first and last 4096 outputs
+    out = {"metric": f"DCF full-domain evals/sec, N={nb} (not the BASELINE.json headline config)", "value": value,
+           "unit": "evals/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "u8", "data": "synthetic",
+           "config": {"workload": f"FD: full domain 2^{8 * nb} points, N={nb}, lambda={lam}, {prg_name}, 1 key, "
+                                  f"party 0; replicas on {world} GPU(s)"},
+           "roofline": {"bound": "lds", "engine": "ttable",
+                        "kernel": ("k_fd_level16_mmo (8N launches)" if mmo
+                                   else "k_fd_level16 (8N-3 launches) + k_fd_tail16<3>"),
+                        "achieved": blocks / kern_s / 1e9, "peak": peak / 1e9,
+                        "unit": f"G AES-{128 if mmo else 256} blocks/s", "frac": blocks / kern_s / peak, "kernel_ms": kern_s * 1e3,
+                        "note": (f"{4 if mmo else 2} AES blocks per internal node (both children from one PRG "
+                                 f"call), about {4 if mmo else 2} per leaf, vs {4 if mmo else 2} x 8N per point "
+                                 "for pointwise eval")}}
+    if rank == 0 and not args.no_cpu:
+        from oracle import oracle as O
+        P = (O.OracleMmoPrg if mmo else O.OraclePrg)(keys, lam)
+        cw = cwb.cpu().numpy().tobytes()
+        k = O.OracleKey(nb, lam)
+        n = 8 * nb
+        k.cw_s[:] = np.frombuffer(cw[:n * lam], np.uint8).reshape(n, lam)
+        k.cw_v[:] = np.frombuffer(cw[n * lam:2 * n * lam], np.uint8).reshape(n, lam)
+        k.cw_t[:] = np.frombuffer(cw[2 * n * lam:2 * n * lam + n], np.uint8)
+        off = dcf_amd.cwb_np1_offset(nb, lam, 1)
+        k.cw_np1[:] = np.frombuffer(cw[off:off + lam], np.uint8)
+        idx = np.concatenate([np.arange(4096), np.arange(npts - 4096, npts)])
+        xs = np.array([list(int(i).to_bytes(nb, "big")) for i in idx], np.uint8)
+        want = O.eval_(P, 0, k, seeds[0].cpu().numpy().tobytes(), xs, nthreads=8)
+        got = ys[torch.from_numpy(idx).cuda()].cpu().numpy()
+        out["matches_oracle_sample"] = bool(np.array_equal(got, want))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5", "fd"])
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--n-bytes", type=int, default=None)
@@ -379,6 +457,8 @@ def main():
     elif args.workload == "c2":  # 32-bit input
         args.n_bytes = args.n_bytes or 4
         args.points = args.points or (1 << 24)
+    elif args.workload == "fd":  # full domain of a 32-bit input
+        args.n_bytes = args.n_bytes or 4
     elif args.workload == "c4":  # benches/dcf_large_lambda.rs:10-11 shape, 2^22 points per GPU
         args.n_bytes = args.n_bytes or 16
         args.points = args.points or (1 << 22)
@@ -387,8 +467,13 @@ def main():
         args.n_bytes = args.n_bytes or 16
         args.points = args.points or (1 << 28)
     world, rank, _ = dist_setup(args.gpus)
-    out = run_c5(args, world, rank) if args.workload == "c5" else run_eval(args, world, rank)
-    if args.workload != "c3" or args.prg != "hirose":
+    if args.workload == "c5":
+        out = run_c5(args, world, rank)
+    elif args.workload == "fd":
+        out = run_fd(args, world, rank)
+    else:
+        out = run_eval(args, world, rank)
+    if args.workload != "fd" and (args.workload != "c3" or args.prg != "hirose"):
         out["metric"] = (f"DCF evals/sec, workload {args.workload.upper()}, {args.prg} PRG "
                          "(not the BASELINE.json headline config)")
     if rank == 0:

@@ -694,12 +694,20 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
     HIP_TRY(hipStreamSynchronize(st));  // xs is freed on return
     return DCF_OK;
   }
-  // Two ping-pong node buffers of 2^(n-1) nodes: s (16 B), v (16 B), t (1 B).
-  const uint64_t maxnodes = npts / 2;
+  // Two ping-pong node buffers: s (16 B), v (16 B), t (1 B) per node.  With the
+  // Hirose PRG the last kFdTail levels run in registers (k_fd_tail16), so the widest
+  // node level in HBM is 2^(n - kFdTail).
+  constexpr uint32_t kFdTail = 3;
+  const bool fused = p->kind == 0 && nlev > kFdTail;
+  const uint64_t maxnodes = fused ? (npts >> kFdTail) : npts / 2;
   const size_t nodeb = 33;
-  int rc = ensure_ws(p, 2 * maxnodes * nodeb + 64, st);
+  // + one work counter per launch (64-node units, see next_wave_base) after the nodes
+  const size_t ctr_off = (2 * maxnodes * nodeb + 64 + 255) & ~(size_t)255;
+  int rc = ensure_ws(p, ctr_off + 64 * sizeof(uint32_t), st);
   if (rc) return rc;
   uint8_t* w = p->d_ws;
+  uint32_t* ctrs = (uint32_t*)(w + ctr_off);
+  HIP_TRY(hipMemsetAsync(ctrs, 0, 64 * sizeof(uint32_t), st));
   uint4* s_a = (uint4*)w;
   uint4* v_a = s_a + maxnodes;
   uint8_t* t_a = (uint8_t*)(v_a + maxnodes);
@@ -713,19 +721,27 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   const uint4* np1 = (const uint4*)(cwb + dcf_cwb_np1_offset(n_bytes, lam, 1));
   hipLaunchKernelGGL(k_fd_root16, dim3(1), dim3(64), 0, st, (const uint4*)s0, (uint32_t)party, s_a, v_a, t_a);
   HIP_TRY(hipGetLastError());
-  for (uint32_t lev = 0; lev < nlev; ++lev) {
+  const uint32_t lev_end = fused ? nlev - kFdTail : nlev;
+  for (uint32_t lev = 0; lev < lev_end; ++lev) {
     const uint64_t parents = 1ull << lev;
     if (p->kind == 1)
       hipLaunchKernelGGL(k_fd_level16_mmo, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
                          p->d_rk128, cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b,
-                         (uint4*)ys);
+                         (uint4*)ys, ctrs + lev);
     else
       hipLaunchKernelGGL(k_fd_level16, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
-                         p->rk[0], cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b, (uint4*)ys);
+                         p->rk[0], cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b, (uint4*)ys,
+                         ctrs + lev);
     HIP_TRY(hipGetLastError());
     std::swap(s_a, s_b);
     std::swap(v_a, v_b);
     std::swap(t_a, t_b);
+  }
+  if (fused) {
+    const uint64_t nodes = 1ull << lev_end;
+    hipLaunchKernelGGL(k_fd_tail16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63);
+    HIP_TRY(hipGetLastError());
   }
   return DCF_OK;
 }

@@ -81,6 +81,19 @@ __device__ __forceinline__ uint64_t next_wave_base(uint32_t* __restrict__ ctr, u
   return (uint64_t)__builtin_amdgcn_readfirstlane(u) * 64u;
 }
 
+// Units of 64 * U consecutive items for kernels with little work per item (the
+// full-domain levels: one PRG call per node): a wave walks its unit 64 items at a
+// time and takes the next unit from ctr, so one atomic covers U wave iterations.
+// Start with base = ~0.
+template <uint32_t U>
+__device__ __forceinline__ uint64_t next_unit_base(uint32_t* __restrict__ ctr, uint64_t base) {
+  if (base != ~0ull && ((base >> 6) + 1) % U != 0) return base + 64;
+  uint32_t u = 0;
+  if ((threadIdx.x & 63u) == 0) u = atomicAdd(ctr, 1u);
+  return (uint64_t)__builtin_amdgcn_readfirstlane(u) * 64u * U;
+}
+constexpr uint32_t kFdUnit = 16;
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock, 1) void k_eval16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
@@ -260,7 +273,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint32_t lev, const uint32_t nlev, const uint64_t nparents, const uint4* __restrict__ s_in,
     const uint4* __restrict__ v_in, const uint8_t* __restrict__ t_in, uint4* __restrict__ s_out,
-    uint4* __restrict__ v_out, uint8_t* __restrict__ t_out, uint4* __restrict__ ys) {
+    uint4* __restrict__ v_out, uint8_t* __restrict__ t_out, uint4* __restrict__ ys, uint32_t* __restrict__ ctr) {
   __shared__ uint32_t lds[kLdsWords];
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
@@ -270,7 +283,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
   const uint32_t npw[4] = {np.x, np.y, np.z, np.w};
   const bool last = lev + 1 == nlev;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < nparents; base += stride) {
+  for (uint64_t base = next_unit_base<kFdUnit>(ctr, ~0ull); base < nparents;
+       base = next_unit_base<kFdUnit>(ctr, base)) {
     const uint64_t j = base + (threadIdx.x & 63u);
     const bool live = j < nparents;
     const uint64_t jj = live ? j : nparents - 1;
@@ -310,6 +324,95 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
       v_out[2 * j + 1] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
       t_out[2 * j] = (uint8_t)tl;
       t_out[2 * j + 1] = (uint8_t)tr;
+    }
+  }
+}
+
+// Last D levels of the full-domain expansion in registers: one lane per node at
+// level nlev - D expands its 2^D leaves (2^D - 1 PRG calls) and writes their y
+// contiguously (2^D x 16 B), so the two largest node levels never go to HBM.
+template <int D>
+__global__ __launch_bounds__(kBlock, 1) void k_fd_tail16(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
+    const uint32_t lev0, const uint64_t nnodes, const uint4* __restrict__ s_in, const uint4* __restrict__ v_in,
+    const uint8_t* __restrict__ t_in, uint4* __restrict__ ys, uint32_t* __restrict__ ctr) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint4 np = cw_np1[0];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = next_unit_base<kFdUnit>(ctr, ~0ull); base < nnodes;
+       base = next_unit_base<kFdUnit>(ctr, base)) {
+    const uint64_t j = base + (threadIdx.x & 63u);
+    const bool live = j < nnodes;
+    const uint64_t jj = live ? j : nnodes - 1;
+    // nodes of the current level: ns/nv (4 words each), nt; level d has 2^d nodes
+    uint32_t ns[1 << (D - 1)][4], nv[1 << (D - 1)][4], nt[1 << (D - 1)];
+    {
+      const uint4 sv = s_in[jj], vv = v_in[jj];
+      ns[0][0] = sv.x; ns[0][1] = sv.y; ns[0][2] = sv.z; ns[0][3] = sv.w;
+      nv[0][0] = vv.x; nv[0][1] = vv.y; nv[0][2] = vv.z; nv[0][3] = vv.w;
+      nt[0] = t_in[jj];
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const uint32_t lev = lev0 + d;
+      const uint4 cs = cw_s[lev], cv = cw_v[lev];
+      const uint32_t ct = cw_t[lev];
+      const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+      uint32_t cs2[1 << (D - 1)][4], cv2[1 << (D - 1)][4], ct2[1 << (D - 1)];  // next level (d < D - 1)
+#pragma unroll
+      for (int i = (1 << d) - 1; i >= 0; --i) {  // descending: children 2i, 2i+1 overwrite nothing unread
+        uint32_t st[2][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          st[0][k] = ns[i][k];
+          st[1][k] = ~ns[i][k];
+        }
+        aes256_tt<2>(st, rk, lds, lc);  // A, B: both children (lib.rs:176-189 with x bit 0 / 1)
+        const uint32_t tm = 0u - nt[i];
+        uint32_t sl[4], vl[4], sr[4], vr[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t msk = (k == 3) ? kMaskLast : 0xFFFFFFFFu;
+          sl[k] = ((st[0][k] ^ ns[i][k]) & msk) ^ (tm & csw[k]);
+          sr[k] = (ns[i][k] & msk) ^ (tm & csw[k]);
+          vl[k] = nv[i][k] ^ ((st[1][k] ^ ~ns[i][k]) & msk) ^ (tm & cvw[k]);
+          vr[k] = nv[i][k] ^ ((~ns[i][k]) & msk) ^ (tm & cvw[k]);
+        }
+        const uint32_t tl = ((st[0][0] ^ ns[i][0]) & 1u) ^ (nt[i] & ct & 1u);
+        const uint32_t tr = ((st[1][0] ^ ~ns[i][0]) & 1u) ^ (nt[i] & (ct >> 1) & 1u);
+        if (d == D - 1) {  // leaves: y = v ^ s ^ t * cw_np1 (lib.rs:192)
+          if (live) {
+            const uint32_t ml = 0u - tl, mr = 0u - tr;
+            uint4* y = ys + (jj << D) + 2 * i;
+            y[0] = make_uint4(vl[0] ^ sl[0] ^ (ml & np.x), vl[1] ^ sl[1] ^ (ml & np.y), vl[2] ^ sl[2] ^ (ml & np.z),
+                              vl[3] ^ sl[3] ^ (ml & np.w));
+            y[1] = make_uint4(vr[0] ^ sr[0] ^ (mr & np.x), vr[1] ^ sr[1] ^ (mr & np.y), vr[2] ^ sr[2] ^ (mr & np.z),
+                              vr[3] ^ sr[3] ^ (mr & np.w));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            cs2[2 * i][k] = sl[k]; cv2[2 * i][k] = vl[k];
+            cs2[2 * i + 1][k] = sr[k]; cv2[2 * i + 1][k] = vr[k];
+          }
+          ct2[2 * i] = tl;
+          ct2[2 * i + 1] = tr;
+        }
+      }
+      if (d < D - 1) {
+#pragma unroll
+        for (int i = 0; i < (2 << d); ++i) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            ns[i][k] = cs2[i][k];
+            nv[i][k] = cv2[i][k];
+          }
+          nt[i] = ct2[i];
+        }
+      }
     }
   }
 }

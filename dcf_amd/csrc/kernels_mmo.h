@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16_mmo(
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint32_t lev, const uint32_t nlev, const uint64_t nparents, const uint4* __restrict__ s_in,
     const uint4* __restrict__ v_in, const uint8_t* __restrict__ t_in, uint4* __restrict__ s_out,
-    uint4* __restrict__ v_out, uint8_t* __restrict__ t_out, uint4* __restrict__ ys) {
+    uint4* __restrict__ v_out, uint8_t* __restrict__ t_out, uint4* __restrict__ ys, uint32_t* __restrict__ ctr) {
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint4 rks[4 * kMmoRk];
   lds_fill_rk128(rks, rk128);
@@ -240,7 +240,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16_mmo(
   const uint32_t npw[4] = {np.x, np.y, np.z, np.w};
   const bool last = lev + 1 == nlev;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < nparents; base += stride) {
+  for (uint64_t base = next_unit_base<kFdUnit>(ctr, ~0ull); base < nparents;
+       base = next_unit_base<kFdUnit>(ctr, base)) {
     const uint64_t j = base + (threadIdx.x & 63u);
     const bool live = j < nparents;
     const uint64_t jj = live ? j : nparents - 1;
