@@ -115,7 +115,7 @@ namespace {
 
 constexpr uint64_t kWideChunk = 1ull << 20;   // points per head/tail pass (t-vector scratch 64 MiB)
 constexpr uint64_t kGenChunk = 4096;          // keys per wide-gen launch (scratch 3*LAMBDA per key)
-constexpr uint32_t kTailPts = 4096;          // points per tail workgroup
+constexpr uint32_t kTailPts = 4096;          // points per tail workgroup (one table build each)
 
 int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
   if (p->ws_bytes >= bytes) return DCF_OK;
@@ -130,16 +130,16 @@ int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
   return DCF_OK;
 }
 
-template <int TW>
+template <int TW, int NCH = 0>
 int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
                 uint32_t lam, uint64_t K, uint64_t key, const uint32_t* tvec, uint64_t cnt, uint8_t* ys,
                 hipStream_t st) {
   const uint32_t nch = (nlev + 1 + 3) / 4;
   const size_t lds = (size_t)nch * 16 * TW;
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail<TW>),
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail<TW, NCH>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const dim3 grid((unsigned)((lam + TW - 1) / TW), (unsigned)((cnt + kTailPts - 1) / kTailPts));
-  hipLaunchKernelGGL(k_eval_wide_tail<TW>, grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key, tvec,
+  hipLaunchKernelGGL((k_eval_wide_tail<TW, NCH>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key, tvec,
                      cnt, kTailPts, ys);
   HIP_TRY(hipGetLastError());
   return DCF_OK;
@@ -204,7 +204,8 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
                          ys + off * lam, tvec);
     HIP_TRY(hipGetLastError());
     if (lam > 32) {
-      rc = (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st)
+      rc = (nch == 33) ? launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st)
+         : (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st)
                        : launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st);
       if (rc) return rc;
     }
@@ -501,6 +502,9 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     else DCF_HYB(false, false);
 #undef DCF_HYB
   } else if (mode == DCF_EVAL_STREAM) {
+#ifndef DCF_STREAM_NS
+#define DCF_STREAM_NS 2  // streams per lane
+#endif
     if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
     HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
     const uint64_t units = (total + kStreamUnit - 1) / kStreamUnit;
@@ -529,7 +533,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
       sct = p->d_kdig + (size_t)num_keys * n * 32;
     }
 #define DCF_STREAM(XR, MK)                                                                                    \
-  hipLaunchKernelGGL((k_eval16_stream<2, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], scs, \
+  hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], scs, \
                      cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,  \
                      (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys)
 #ifdef DCF_STREAM_TT2

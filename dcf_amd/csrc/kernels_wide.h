@@ -178,13 +178,91 @@ __device__ __forceinline__ uint4 w_row_piece(const uint8_t* __restrict__ cw_s, c
   return w;
 }
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// 16 bytes at an LDS byte address: ds_read takes the address as is (a generic
+// pointer into an extern __shared__ array costs a v_add of the array base per read).
+__device__ __forceinline__ uint4 lds_load16(uint32_t a) {
+  const u32x4_t v = *(__attribute__((address_space(3))) const u32x4_t*)(size_t)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void tail_load_t(uint4 (&d)[4], const uint4* __restrict__ tv4, uint64_t pp, uint64_t p1) {
+  pp = min<uint64_t>(pp, p1 - 1);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = tv4[4 * pp + k];
+}
+
+// One 16-byte piece of y for the point whose t-vector is t: cst ^ XOR over chunks c of
+// G[c][t nibble c] (four-Russians, see k_eval_wide_tail).
+template <int TW, int LP, int NCH>
+__device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst, const char* gb, const uint4* G,
+                                            uint32_t q, uint32_t nch16_rt, uint32_t nrem_rt) {
+  // NCH > 0: chunk count fixed at compile time (fully unrolled; N = 16 has 33 chunks)
+  const uint32_t nch16 = NCH > 0 ? (uint32_t)NCH / 16u : nch16_rt;
+  const uint32_t nrem = NCH > 0 ? (uint32_t)NCH % 16u : nrem_rt;
+  uint32_t acc[4] = {cst.x, cst.y, cst.z, cst.w};
+  uint32_t tq[16] = {t[0].x, t[0].y, t[0].z, t[0].w, t[1].x, t[1].y, t[1].z, t[1].w,
+                     t[2].x, t[2].y, t[2].z, t[2].w, t[3].x, t[3].y, t[3].z, t[3].w};
+  // Row read of chunk c: G + c * 16 * TW + e * TW + q * 16 bytes.  At TW = 256 one
+  // v_perm builds e * 256 + q * 16 (+ 64 KiB per group of 16 chunks) from the t byte
+  // and a lane constant, and c * 4096 mod 64 KiB rides in the ds_read offset field.
+  uint32_t qb = 16u * q;
+  for (uint32_t g16 = 0; g16 < nch16; ++g16) {  // full groups of 16 chunks (4 t words)
+#pragma unroll
+    for (uint32_t j = 0; j < 16; j += 2) {
+      uint4 b[2];
+#pragma unroll
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t cc = j + h;
+        if (TW == 256) {
+          const uint32_t a = __builtin_amdgcn_perm(tq[cc >> 2], qb, 0x0c020000u | ((4u + (cc & 3u)) << 8));
+          b[h] = lds_load16(a + cc * 4096u);  // G sits at LDS address 0 (checked in the kernel)
+        } else {
+          const uint32_t e = (tq[cc >> 2] >> (8u * (cc & 3u))) & 15u;
+          b[h] = G[((16u * g16 + cc) * 16u + e) * LP + q];
+        }
+      }
+      acc[0] = xor3(acc[0], b[0].x, b[1].x);
+      acc[1] = xor3(acc[1], b[0].y, b[1].y);
+      acc[2] = xor3(acc[2], b[0].z, b[1].z);
+      acc[3] = xor3(acc[3], b[0].w, b[1].w);
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) tq[k] = tq[k + 4];  // word queue: no dynamic register indexing
+    qb += 0x10000u;
+  }
+#pragma unroll
+  for (uint32_t cc = 0; cc < 15; ++cc) {  // remaining nch % 16 chunks
+    if (cc < nrem) {
+      const uint32_t e = (tq[cc >> 2] >> (8u * (cc & 3u))) & 15u;
+      const uint4 b = G[((16u * nch16 + cc) * 16u + e) * LP + q];
+      acc[0] ^= b.x; acc[1] ^= b.y; acc[2] ^= b.z; acc[3] ^= b.w;
+    }
+  }
+  return make_uint4(acc[0], acc[1], acc[2], acc[3]);
+}
+
+// Non-temporal (written once, never re-read here: measured 4 % faster) buffer store of
+// a y piece; `kill` != 0 puts the lane's offset past num_records, which drops it.
+template <int LP>
+__device__ __forceinline__ void tail_store(uint8_t* ys, uint64_t pw, uint32_t pin, uint32_t lam, uint32_t off,
+                                           uint32_t kill, uint4 y) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t base = (uint64_t)(uintptr_t)(ys + pw * lam);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  uint8_t* wb = reinterpret_cast<uint8_t*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(wb, (short)0, (int)((64 / LP) * lam), 0x00020000);
+  const u32x4 v = {y.x, y.y, y.z, y.w};
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (pin * lam + off) | kill, 0, 2 /* nt */);
+}
+
 // ------------------------------------------------------------------------
 // Tail: y[32 + TW*tile .. +TW) for a range of points.  LP = TW/16 lanes per
 // point, each owns one 16-byte piece.  LDS: G[chunk][nibble][LP] uint4,
 // G[c][e] = XOR of W rows 4c+k over the set bits k of e.  All LP lanes of a
 // point read one contiguous TW-byte entry -> conflict-free ds_read_b128.
 // ------------------------------------------------------------------------
-template <int TW>
+template <int TW, int NCH = 0>
 __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __restrict__ cw_s,
                                                             const uint8_t* __restrict__ cw_v,
                                                             const uint8_t* __restrict__ cw_np1,
@@ -195,6 +273,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
                                                             uint8_t* __restrict__ ys) {
   constexpr int LP = TW / 16;
   extern __shared__ uint4 G[];
+  if (TW == 256 && (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)G != 0u) __builtin_trap();
   const uint32_t nrows = nlev + 1, nch = (nrows + 3) >> 2;
   // Tiles are aligned to TW bytes of the output row (tile 0's first 32 bytes belong to
   // the head and are skipped): unaligned 256-byte pieces split cache lines between
@@ -230,75 +309,36 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
   const uint64_t p0 = (uint64_t)blockIdx.y * pts_per_block;
   const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
   const uint32_t pstep = blockDim.x / LP;
-  // The point's t-vector (64 B) is loaded one point ahead, so the LDS row reads
-  // of a point never wait on a global load.
-  uint64_t p = p0 + threadIdx.x / LP;
+  const uint32_t pin = (threadIdx.x & 63u) / LP;  // the lane's point among the wave's 64 / LP
+  // t-vectors (64 B per point) are loaded two points ahead into ping-pong registers,
+  // clamped instead of guarded, and the y store below is unconditional too: with no
+  // branch around any vector-memory instruction the compiler counts vmcnt exactly and
+  // waits for the t-vector loads only, never for an older non-temporal y store.
   const uint4* tv4 = reinterpret_cast<const uint4*>(tvec);
-  uint4 nt[4] = {};
-  if (p < p1) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) nt[k] = tv4[4 * p + k];
-  }
-  // Row read of chunk c: G + c * 16 * TW + e * TW + q * 16 bytes.  At TW = 256 one
-  // v_perm builds e * 256 + q * 16 (+ 64 KiB for c >= 16) from the t byte and a lane
-  // constant, and c * 4096 mod 64 KiB rides in the ds_read offset field.
-  const uint32_t qb0 = 16u * q;
+  uint64_t p = p0 + threadIdx.x / LP;
+  uint4 ta[4], tb[4];
+  tail_load_t(ta, tv4, p, p1);
+  tail_load_t(tb, tv4, p + pstep, p1);
+  const char* gb = reinterpret_cast<const char*>(G);
   const uint32_t nch16 = nch >> 4, nrem = nch & 15u;
-  for (; p < p1; p += pstep) {
-    const uint32_t tw[16] = {nt[0].x, nt[0].y, nt[0].z, nt[0].w, nt[1].x, nt[1].y, nt[1].z, nt[1].w,
-                             nt[2].x, nt[2].y, nt[2].z, nt[2].w, nt[3].x, nt[3].y, nt[3].z, nt[3].w};
-    const uint64_t pn = p + pstep;
-    if (pn < p1) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) nt[k] = tv4[4 * pn + k];
+  // Buffer store: base = the wave's first point row, dead lanes get an offset past
+  // num_records (the store drops it).  4 points x LAMBDA bytes <= 4 GiB.
+  const uint32_t dead = 0x80000000u;
+  for (;;) {
+    if (p >= p1) break;
+    {
+      const uint4 y = tail_piece<TW, LP, NCH>(ta, cst, gb, G, q, nch16, nrem);
+      tail_load_t(ta, tv4, p + 2 * pstep, p1);
+      tail_store<LP>(ys, p - pin, pin, lam, off, lane_live ? 0u : dead, y);
     }
-    uint32_t acc[4] = {cst.x, cst.y, cst.z, cst.w};
-    uint32_t tq[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) tq[k] = tw[k];
-    // Full groups of 16 chunks (4 t words): fully unrolled, constant LDS offsets.
-    const char* gb = reinterpret_cast<const char*>(G);
-    uint32_t qb = qb0;
-    for (uint32_t g16 = 0; g16 < nch16; ++g16) {
-#pragma unroll
-      for (uint32_t j = 0; j < 16; j += 2) {
-        uint4 b[2];
-#pragma unroll
-        for (uint32_t h = 0; h < 2; ++h) {
-          const uint32_t cc = j + h;
-          if (TW == 256) {
-            const uint32_t a = __builtin_amdgcn_perm(tq[cc >> 2], qb, 0x0c020000u | ((4u + (cc & 3u)) << 8));
-            b[h] = *reinterpret_cast<const uint4*>(gb + a + cc * 4096u);
-          } else {
-            const uint32_t e = (tq[cc >> 2] >> (8u * (cc & 3u))) & 15u;
-            b[h] = G[((16u * g16 + cc) * 16u + e) * LP + q];
-          }
-        }
-        acc[0] = xor3(acc[0], b[0].x, b[1].x);
-        acc[1] = xor3(acc[1], b[0].y, b[1].y);
-        acc[2] = xor3(acc[2], b[0].z, b[1].z);
-        acc[3] = xor3(acc[3], b[0].w, b[1].w);
-      }
-#pragma unroll
-      for (int k = 0; k < 12; ++k) tq[k] = tq[k + 4];  // word queue: no dynamic register indexing
-      qb += 0x10000u;
+    p += pstep;
+    if (p >= p1) break;
+    {
+      const uint4 y = tail_piece<TW, LP, NCH>(tb, cst, gb, G, q, nch16, nrem);
+      tail_load_t(tb, tv4, p + 2 * pstep, p1);
+      tail_store<LP>(ys, p - pin, pin, lam, off, lane_live ? 0u : dead, y);
     }
-    // Remaining nch % 16 chunks.
-#pragma unroll
-    for (uint32_t cc = 0; cc < 15; ++cc) {
-      if (cc < nrem) {
-        const uint32_t e = (tq[cc >> 2] >> (8u * (cc & 3u))) & 15u;
-        const uint4 b = G[((16u * nch16 + cc) * 16u + e) * LP + q];
-        acc[0] ^= b.x; acc[1] ^= b.y; acc[2] ^= b.z; acc[3] ^= b.w;
-      }
-    }
-    if (lane_live) {  // written once, never re-read here: non-temporal (measured 4 % faster)
-      uint32_t* yo = reinterpret_cast<uint32_t*>(ys + p * lam + off);
-      __builtin_nontemporal_store(acc[0], yo);
-      __builtin_nontemporal_store(acc[1], yo + 1);
-      __builtin_nontemporal_store(acc[2], yo + 2);
-      __builtin_nontemporal_store(acc[3], yo + 3);
-    }
+    p += pstep;
   }
 }
 
