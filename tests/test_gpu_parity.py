@@ -229,10 +229,12 @@ def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P, mode):
 
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("lam,nb,m", [(32, 2, 70), (48, 3, 65), (64, 16, 33), (112, 4, 130), (1024, 2, 40),
-                                      (4096, 16, 12), (272, 5, 600)])
+                                      (4096, 16, 12), (272, 5, 600), (512, 16, 5000), (16384, 16, 150)])
 def test_wide_eval_random_vs_oracle(dcf, lam, nb, m, mode):
     """LAMBDA >= 32: head/tail kernels vs the literal oracle, both parties, both bounds.
-    mode 0: stream head (default), mode 1: lockstep T-table head."""
+    mode 0: stream head (default), mode 1: lockstep T-table head.  N = 16 runs the
+    compile-time 33-chunk tail; 5000 points cross tail workgroups (4096 points each)
+    and the two-ahead t-vector prefetch, 16384 covers 64 tiles per point."""
     rng = np.random.default_rng(lam * 7 + nb)
     keys = [rng.bytes(32) for _ in range(18)]
     prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
