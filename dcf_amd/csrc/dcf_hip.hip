@@ -113,7 +113,7 @@ struct dcf_prg {
 
 namespace {
 
-constexpr uint64_t kWideChunk = 1ull << 20;   // points per head/tail pass (t-vector scratch 64 MiB)
+constexpr uint64_t kWideChunk = 1ull << 22;   // points per head/tail pass (t-vector scratch 256 MiB)
 constexpr uint64_t kGenChunk = 4096;          // keys per wide-gen launch (scratch 3*LAMBDA per key)
 constexpr uint32_t kTailPts = 4096;          // points per tail workgroup (one table build each)
 
@@ -187,12 +187,18 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
       const uint64_t units = (cnt + kStreamUnit - 1) / kStreamUnit;
       uint64_t blocks = (units + 15) / 16;
       if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
-#define DCF_WHS(MH)                                                                                            \
-  hipLaunchKernelGGL((k_eval_wide_head_stream<2, MH>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab,     \
+#ifndef DCF_WHS_NS
+#define DCF_WHS_NS 1  // points per lane (2 spills: 128 VGPRs)
+#endif
+#define DCF_WHS(MH, XR)                                                                                        \
+  hipLaunchKernelGGL((k_eval_wide_head_stream<DCF_WHS_NS, MH, XR>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab,     \
                      p->d_rk2, (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
                      lam, K, key, cnt, p->d_ctr, ys + off * lam, tvec)
-      if (lam == 32) DCF_WHS(true);
-      else DCF_WHS(false);
+      const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16;
+      if (lam == 32 && xreg) DCF_WHS(true, true);
+      else if (lam == 32) DCF_WHS(true, false);
+      else if (xreg) DCF_WHS(false, true);
+      else DCF_WHS(false, false);
 #undef DCF_WHS
     } else if (lam == 32)
       hipLaunchKernelGGL(k_eval_wide_head<true>, grid, dim3(kBlock), 0, st, p->d_tab, p->rk[0], p->rk[17], cws, cwv,

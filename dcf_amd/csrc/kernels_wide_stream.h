@@ -23,11 +23,12 @@ template <int NS>
 struct WideLane {
   uint32_t s[NS][8], v[NS][8];           // bytes [0,32) of the seed and of the v accumulator
   uint32_t t[NS], ph[NS], lev[NS], cur[NS], tR[NS], tacc[NS];
+  uint32_t xq[NS][3];                    // XREG: the point's next raw x words (byte-swapped on use)
   uint32_t pt[NS];                       // point index within this launch (<= 2^20); x row = xs + pt * N
   bool alive[NS];
 };
 
-template <int NS>
+template <int NS, bool XREG>
 __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, const uint8_t* __restrict__ s0p,
                                            uint32_t party, const uint8_t* __restrict__ xs, uint32_t nbytes) {
   const uint4* s4 = reinterpret_cast<const uint4*>(s0p);  // k.s0s[0] (lib.rs:168), L2-resident
@@ -44,11 +45,26 @@ __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, c
   L.pt[i] = p;
   L.alive[i] = true;
   // x bits are needed before the next AES (they pick its block): one 32-bit word
-  // per 32 levels, the first one here.
-  L.cur[i] = load_bits32(xs + (uint64_t)p * nbytes, 0, nbytes);
+  // per 32 levels.  XREG (N % 4 == 0, N <= 16): all of x now, queued, so a level
+  // crossing 32 bits never waits on a load.
+  const uint8_t* row = xs + (uint64_t)p * nbytes;
+  if (XREG) {
+    uint32_t w[4];
+    if (nbytes == 16) {
+      const uint4 x = *reinterpret_cast<const uint4*>(row);
+      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = (4u * k < nbytes) ? reinterpret_cast<const uint32_t*>(row)[k] : 0u;
+    }
+    L.cur[i] = bswap32(w[0]);
+    L.xq[i][0] = w[1]; L.xq[i][1] = w[2]; L.xq[i][2] = w[3];
+  } else {
+    L.cur[i] = load_bits32(row, 0, nbytes);
+  }
 }
 
-template <int NS>
+template <int NS, bool XREG>
 __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, uint64_t& unext, uint64_t& uend,
                                             bool& exhausted, uint32_t* __restrict__ ctr, uint64_t nunits,
                                             uint64_t count, const uint8_t* __restrict__ s0p, uint32_t party,
@@ -73,7 +89,7 @@ __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, u
     }
     const uint32_t rank = lane_rank(need);
     const bool take = mine && (uint64_t)rank < uend - unext;
-    if (take) wide_start<NS>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes);
+    if (take) wide_start<NS, XREG>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes);
     const uint64_t taken = __ballot(take);
     unext += (uint64_t)__popcll(taken);
     need &= ~taken;
@@ -97,7 +113,7 @@ __global__ void k_cw_digest(const uint8_t* __restrict__ cw_s, const uint8_t* __r
 }
 
 // Single key `key` of a num_keys-key CWB; count <= 2^20 points per launch.
-template <int NS, bool MASK_HEAD>
+template <int NS, bool MASK_HEAD, bool XREG>
 __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
     const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
     const uint8_t* __restrict__ dig_t, const uint8_t* __restrict__ cw_np1,
@@ -125,30 +141,18 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
   }
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    wide_refill<NS>(L, i, true, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes);
+    wide_refill<NS, XREG>(L, i, true, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes);
 
   for (;;) {
     bool any = false;
 #pragma unroll
     for (int i = 0; i < NS; ++i) any = any || L.alive[i];
     if (!__ballot(any)) break;
-    // Block of this step: B (ph 0), then A (ph 1, left) or D (ph 1, right), C (ph 2).
-    uint32_t st[NS][4];
-    const uint4* rk[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
-      const uint32_t hi = (ph != 0u) & xb;                            // D or C: bytes [16,32), cipher 17
-      const uint32_t inv = 0u - ((ph == 0u) | ((ph == 1u) & xb));    // B or D: ~s
-      rk[i] = rks + 23u * hi;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st[i][j] = (hi ? L.s[i][4 + j] : L.s[i][j]) ^ inv;
-    }
-    aes_tt_lk<14, NS>(st, rk, lds, lc);
     // Correction words, needed only on the step that ends a level: bytes [0,32) of cw_s /
     // cw_v from the compact per-key digest (64 B per level, 8 KiB, L1-resident; the CWB
-    // rows are LAMBDA bytes apart, one cache line per lane), loaded after the AES so
-    // they are not live across it.
+    // rows are LAMBDA bytes apart, one cache line per lane).  Issued before the AES and
+    // pinned after it, so they are waited on long after the last y / t-vector stores
+    // (vmcnt is in order: a load issued after a store cannot be waited on alone).
     uint4 cs[NS][2], cv[NS][2];
     uint32_t ct[NS];
 #pragma unroll
@@ -164,7 +168,25 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
         ct[i] = dig_t[L.lev[i]];
       }
     }
-
+    // Block of this step: B (ph 0), then A (ph 1, left) or D (ph 1, right), C (ph 2).
+    uint32_t st[NS][4];
+    const uint4* rk[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
+      const uint32_t hi = (ph != 0u) & xb;                            // D or C: bytes [16,32), cipher 17
+      const uint32_t inv = 0u - ((ph == 0u) | ((ph == 1u) & xb));    // B or D: ~s
+      rk[i] = rks + 23u * hi;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[i][j] = (hi ? L.s[i][4 + j] : L.s[i][j]) ^ inv;
+    }
+    aes_tt_lk<14, NS>(st, rk, lds, lc);
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+      asm volatile("" : "+v"(cs[i][0].x), "+v"(cs[i][0].y), "+v"(cs[i][0].z), "+v"(cs[i][0].w), "+v"(cs[i][1].x),
+                   "+v"(cs[i][1].y), "+v"(cs[i][1].z), "+v"(cs[i][1].w), "+v"(cv[i][0].x), "+v"(cv[i][0].y),
+                   "+v"(cv[i][0].z), "+v"(cv[i][0].w), "+v"(cv[i][1].x), "+v"(cv[i][1].y), "+v"(cv[i][1].z),
+                   "+v"(cv[i][1].w), "+v"(ct[i]));
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
@@ -216,7 +238,14 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
         L.tacc[i] = 0u;
       }
       L.cur[i] <<= adv;
-      if (adv && (r & 31u) == 0u && r < nlev) L.cur[i] = load_bits32(xs + (uint64_t)L.pt[i] * nbytes, r >> 5, nbytes);
+      if (XREG) {  // next x word from the queue at a 32-level boundary
+        const bool nw = adv && (r & 31u) == 0u;
+        L.cur[i] = nw ? bswap32(L.xq[i][0]) : L.cur[i];
+        L.xq[i][0] = nw ? L.xq[i][1] : L.xq[i][0];
+        L.xq[i][1] = nw ? L.xq[i][2] : L.xq[i][1];
+      } else if (adv && (r & 31u) == 0u && r < nlev) {
+        L.cur[i] = load_bits32(xs + (uint64_t)L.pt[i] * nbytes, r >> 5, nbytes);
+      }
       L.lev[i] = r;
       if (pdone) {  // y[0:32) = v ^ s ^ t * cw_np1 (lib.rs:192)
         const uint4* np4 = reinterpret_cast<const uint4*>(cw_np1 + key * lam);
@@ -235,7 +264,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
       if (__ballot(done))
-        wide_refill<NS>(L, i, done, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes);
+        wide_refill<NS, XREG>(L, i, done, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes);
     }
   }
 }
