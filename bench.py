@@ -52,7 +52,7 @@ def hybrid_peak() -> float:
 
 
 ENGINE = {0: "stream", 1: "ttable", 2: "bitsliced", 3: "hybrid", 4: "stream"}
-KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "bitsliced": "k_eval16_bs",
+KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "ttable-small": "k_eval16", "bitsliced": "k_eval16_bs",
           "stream": "k_eval16_stream", "mmo": "k_eval16_mmo"}
 
 
@@ -63,7 +63,7 @@ PEAK_MMO_BLOCKS = CUS * CLK_HZ / (160 / 32 + 11 / 16)
 def engine_peak(engine: str) -> float:
     if engine == "mmo":
         return PEAK_MMO_BLOCKS
-    if engine in ("ttable", "stream"):
+    if engine in ("ttable", "ttable-small", "stream"):
         return PEAK_TT_BLOCKS
     if engine == "bitsliced":
         return VALU_OPS / BS_VALU_PER_BLOCK
@@ -258,6 +258,8 @@ def run_eval(args, world, rank):
         engine = "ttable"
     if args.prg == "mmo":
         engine = "mmo"
+    elif args.eval_mode == 0 and lam == 16 and m < CUS * 1024 * 2:
+        engine = "ttable-small"  # auto mode's small-batch path: lockstep walk (dcf_hip.hip eval_launch)
     # Blocks the dominant kernel actually encrypts per eval: the reference count, except the
     # stream engine, which encrypts B on every level and A on left (x bit 0) levels only.
     exec_bpe = (8 * nb + zero_bits(xs) / m) if engine == "stream" else bpe  # mmo: 2 AES-128 per level
@@ -283,7 +285,7 @@ def run_eval(args, world, rank):
                    "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
         "aes_blocks_per_s": value * bpe,
         "roofline": wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine) if lam > 16 else {
-            "bound": "lds" if engine in ("ttable", "stream", "mmo") else ("valu" if engine == "bitsliced" else "lds+valu"),
+            "bound": "lds" if engine in ("ttable", "ttable-small", "stream", "mmo") else ("valu" if engine == "bitsliced" else "lds+valu"),
             "kernel": kernel, "engine": engine,
             "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-128 blocks/s" if engine == "mmo" else "G AES-256 blocks/s",
             "frac": per_gpu_blocks / peak, "traffic": pmc_traffic(kernel, m, nb, lam),
