@@ -113,14 +113,19 @@ def wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine):
                     "(GF(2) combination writing bytes [32, LAMBDA)) run back to back"}
 
 
-def zero_bits(xs: torch.Tensor) -> int:
+def zero_bits(xs: torch.Tensor, skip_bits: int = 0) -> int:
     """Number of 0 bits in the points = left steps = the A blocks the stream engine
-    encrypts on top of one B block per level (kernels_stream.h)."""
+    encrypts on top of one B block per level (kernels_stream.h), not counting each
+    point's first `skip_bits` (Msb0) bits: the levels a shared-prefix table covers."""
     lut = torch.tensor([8 - bin(i).count("1") for i in range(256)], dtype=torch.int32, device=xs.device)
-    flat = xs.reshape(-1)
+    x2 = xs.reshape(xs.shape[0], -1)
+    full, part = skip_bits // 8, skip_bits % 8
     tot = 0
-    for off in range(0, flat.numel(), 1 << 26):
-        tot += int(lut[flat[off:off + (1 << 26)].to(torch.int64)].sum().item())
+    for off in range(0, x2.shape[0], 1 << 22):
+        c = x2[off:off + (1 << 22)].to(torch.int64)
+        tot += int(lut[c[:, full:]].sum().item())
+        if part:  # the partial byte's first `part` bits are covered by the prefix
+            tot -= int(lut[c[:, full] >> (8 - part)].sum().item()) - (8 - part) * c.shape[0]
     return tot
 
 
@@ -212,6 +217,8 @@ def run_eval(args, world, rank):
     prg.set_eval_mode(args.eval_mode)
     if args.hybrid_split is not None:
         prg.set_hybrid_split(args.hybrid_split, args.hybrid_mem)
+    prg.set_prefix_levels(args.prefix)
+    pfx = prg.eval_prefix_levels(nb, 1, m)  # shared-prefix depth this eval uses (0 = none)
     d = dcf_amd.DcfImpl(nb, lam, prg)
     cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002)
     s0 = seeds[0].contiguous()
@@ -227,29 +234,41 @@ def run_eval(args, world, rank):
         if parties == 2:
             d.eval_device(True, cwb, s1, xs, ys1)
 
-    stream = torch.cuda.current_stream()
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps / parties  # per eval launch
-    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
+    def timed(steps):
+        """(wall seconds max over ranks, seconds per eval call on the launch stream)"""
+        stream = torch.cuda.current_stream()
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(steps):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        w = time.perf_counter() - t0
+        t = torch.tensor([w], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), ev0.elapsed_time(ev1) / 1e3 / steps / parties
+
+    wall, kern_s = timed(args.steps)
+    no_prefix = None
+    if pfx and not args.no_compare:
+        # the same batch without the shared-prefix table (each point walks all 8N levels)
+        prg.set_prefix_levels(0)
+        w0, k0 = timed(args.steps)
+        prg.set_prefix_levels(args.prefix)
+        no_prefix = {"value": m * world * args.steps * parties / w0, "kernel_ms": k0 * 1e3,
+                     "executed_blocks_per_eval": 8 * nb + zero_bits(xs) / m,
+                     "speedup": w0 / wall}
     total_evals = m * world * args.steps * parties
     value = total_evals / wall
     bpe = blocks_per_eval(nb, lam)
@@ -262,7 +281,10 @@ def run_eval(args, world, rank):
         engine = "ttable-small"  # auto mode's small-batch path: lockstep walk (dcf_hip.hip eval_launch)
     # Blocks the dominant kernel actually encrypts per eval: the reference count, except the
     # stream engine, which encrypts B on every level and A on left (x bit 0) levels only.
-    exec_bpe = (8 * nb + zero_bits(xs) / m) if engine == "stream" else bpe  # mmo: 2 AES-128 per level
+    # With a shared-prefix table of depth D a point walks levels D..8N-1 only, and the
+    # table costs 2 blocks per node of the top tree (2^(D+1) - 2), spread over the batch.
+    exec_bpe = ((8 * nb - pfx) + zero_bits(xs, pfx) / m + (2 ** (pfx + 1) - 2) / m) if engine == "stream" \
+        else bpe  # mmo: 2 AES-128 per level
     if lam > 16:
         # LAMBDA >= 32: the stream head encrypts B, A (left) or B, D, C (right) per level, and the
         # tail writes LAMBDA - 32 output bytes per eval: time bound = AES (LDS) + output (HBM write).
@@ -293,8 +315,10 @@ def run_eval(args, world, rank):
             "hbm_GBps": m * (nb + lam) / kern_s / 1e9,
             "ttable_only_peak": PEAK_TT_BLOCKS / 1e9,
             "executed_blocks_per_eval": exec_bpe, "reference_blocks_per_eval": bpe,
+            "prefix_levels": pfx, "no_prefix": no_prefix,
             "note": "achieved = AES-256 blocks the kernel encrypts per second (stream engine: B every "
-                    "level + A on left levels; other engines: the reference count, 2 per level); "
+                    "level + A on left levels, below a shared-prefix table of prefix_levels levels built "
+                    "inside the timed call and counted; other engines: the reference count, 2 per level); "
                     "aes_blocks_per_s above uses the reference count.  Peak per GPU at 2.4 GHz: T-table "
                     "engines LDS-bound (32 ds_read_b32 lookups/clk/CU, 224 per block), bitsliced VALU-bound "
                     "(128 lane-ops/clk/CU, ~800 per block); hybrid = LDS-saturating T-table + bitsliced on "
@@ -449,6 +473,9 @@ def main():
     ap.add_argument("--eval-mode", type=int, default=0, help="AES engine: 0 auto, 1 T-table, 2 bitsliced, 3 hybrid, 4 stream")
     ap.add_argument("--prg", default="hirose", choices=["hirose", "mmo"],
                     help="hirose: the reference's Aes256HirosePrg; mmo: Aes128MatyasMeyerOseasPrg (lambda = 16)")
+    ap.add_argument("--prefix", type=int, default=-1,
+                    help="shared-prefix table depth for single-key eval: -1 auto (library default), 0 off")
+    ap.add_argument("--no-compare", action="store_true", help="skip the no-prefix comparison timing")
     ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves per workgroup")
     ap.add_argument("--hybrid-mem", type=int, default=1, help="hybrid: 1 = 16 waves + scratch slabs, 0 = 12 waves")
     args = ap.parse_args()

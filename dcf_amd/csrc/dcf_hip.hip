@@ -18,6 +18,7 @@
 // per lookup; 16 lookups per round.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -107,6 +108,9 @@ struct dcf_prg {
   void* d_slabs = nullptr;    // per-wave s/v slabs of the hybrid kernel (MEM variant)
   size_t slab_bytes = 0;
   int eval_mode = DCF_EVAL_AUTO;
+  int prefix_levels = -1;     // shared-prefix table depth for single-key stream eval: -1 auto, 0 off
+  uint8_t* d_pfx = nullptr;   // its two node buffers (s, v, t per node) + work counters
+  size_t pfx_bytes = 0;
   int hybrid_tt_waves = 13;   // T-table waves per hybrid workgroup (r01 sweep: 13 of 16 best)
   int hybrid_mem = 1;         // 1: 16-wave workgroups with s/v slabs; 0: 12 waves, s/v in registers
 };
@@ -127,6 +131,69 @@ int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
   }
   HIP_TRY(hipMalloc(&p->d_ws, bytes));
   p->ws_bytes = bytes;
+  return DCF_OK;
+}
+
+// Shared-prefix depth for a single-key stream eval of `total` points (kernels_stream.h
+// PrefixTable): the top tree has 2^D nodes (33 B each, built with 2^(D+1) AES blocks)
+// and saves every point D levels.  Auto: D = log2(total) - 1 (table build < 1 block per
+// point), at most 24 (a 553 MB table), none below 8, always < 8N.  Measured (r01i,
+// C2: 2^24 points, N = 4): D = 12 / 16 / 20 / 24 -> 2.00 / 2.29 / 2.62 / 2.83 G evals/s
+// (1.44 without); C3 (2^28, N = 16): D = 16 / 24 -> 450 / 477 M (397 M without).
+constexpr uint32_t kPrefixMax = 24;
+uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
+  if (p->kind != 0 || p->lambda != 16 || num_keys != 1 || p->prefix_levels == 0) return 0;
+  uint32_t d;
+  if (p->prefix_levels > 0) {
+    d = (uint32_t)p->prefix_levels;
+  } else {
+    const uint32_t lg = 63u - (uint32_t)__builtin_clzll(total | 1u);
+    d = lg > 1u ? lg - 1u : 0u;
+    if (d < 8u) return 0;
+  }
+  d = std::min(d, kPrefixMax);
+  return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
+}
+
+// Expand the top `levels` levels of the key's tree (s = s0, v = 0, t = party at the
+// root; k_fd_level16 per level, as the full-domain eval does) into p->d_pfx.
+int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const uint4* cwv, const uint8_t* cwt,
+                 const uint4* np1, const uint8_t* s0, uint32_t levels, PrefixTable* out, hipStream_t st) {
+  const uint64_t maxnodes = 1ull << levels;
+  const size_t nodeb = 33, half = (maxnodes * nodeb + 255) & ~(size_t)255;
+  const size_t need = 2 * half + 64 * sizeof(uint32_t);
+  if (p->pfx_bytes < need) {
+    if (p->d_pfx) {
+      HIP_TRY(hipStreamSynchronize(st));
+      HIP_TRY(hipFree(p->d_pfx));
+      p->d_pfx = nullptr;
+      p->pfx_bytes = 0;
+    }
+    HIP_TRY(hipMalloc(&p->d_pfx, need));
+    p->pfx_bytes = need;
+  }
+  uint4* s_a = (uint4*)p->d_pfx;
+  uint4* v_a = s_a + maxnodes;
+  uint8_t* t_a = (uint8_t*)(v_a + maxnodes);
+  uint4* s_b = (uint4*)(p->d_pfx + half);
+  uint4* v_b = s_b + maxnodes;
+  uint8_t* t_b = (uint8_t*)(v_b + maxnodes);
+  uint32_t* ctrs = (uint32_t*)(p->d_pfx + 2 * half);
+  HIP_TRY(hipMemsetAsync(ctrs, 0, 64 * sizeof(uint32_t), st));
+  hipLaunchKernelGGL(k_fd_root16, dim3(1), dim3(64), 0, st, (const uint4*)s0, (uint32_t)party, s_a, v_a, t_a);
+  HIP_TRY(hipGetLastError());
+  const uint32_t nlev = (uint32_t)(8 * n_bytes);  // > levels: no level here is the last one
+  for (uint32_t lev = 0; lev < levels; ++lev) {
+    const uint64_t parents = 1ull << lev;
+    hipLaunchKernelGGL(k_fd_level16, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b,
+                       (uint4*)nullptr, ctrs + lev);
+    HIP_TRY(hipGetLastError());
+    std::swap(s_a, s_b);
+    std::swap(v_a, v_b);
+    std::swap(t_a, t_b);
+  }
+  *out = PrefixTable{s_a, v_a, t_a, levels};
   return DCF_OK;
 }
 
@@ -326,6 +393,7 @@ void dcf_prg_free(dcf_prg* p) {
     if (p->d_kdig) (void)hipFree(p->d_kdig);
     if (p->d_ws) (void)hipFree(p->d_ws);
     if (p->d_ctr) (void)hipFree(p->d_ctr);
+    if (p->d_pfx) (void)hipFree(p->d_pfx);
     if (p->d_slabs) (void)hipFree(p->d_slabs);
   }
   delete p;
@@ -338,6 +406,23 @@ int dcf_prg_set_eval_mode(dcf_prg* p, int mode) {
   if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_STREAM) return fail(DCF_ERR_ARG, "bad eval mode");
   p->eval_mode = mode;
   return DCF_OK;
+}
+
+int dcf_prg_set_prefix_levels(dcf_prg* p, int levels) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  if (levels < -1) return fail(DCF_ERR_ARG, "prefix levels must be -1 (auto), 0 (off) or > 0");
+  p->prefix_levels = levels;
+  return DCF_OK;
+}
+
+int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, size_t points_per_key) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
+  const uint64_t total = (uint64_t)num_keys * points_per_key;
+  // the paths eval_launch takes without a table: small batches in auto mode, non-stream engines
+  if (p->eval_mode == DCF_EVAL_AUTO && total < (uint64_t)p->cus * kBlock * 2) return 0;
+  if (p->eval_mode != DCF_EVAL_AUTO && p->eval_mode != DCF_EVAL_STREAM) return 0;
+  return (int)prefix_depth(p, n_bytes, num_keys, total);
 }
 
 int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves, int slab_variant) {
@@ -538,17 +623,25 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
       scs = (const uint4*)p->d_kdig;
       sct = p->d_kdig + (size_t)num_keys * n * 32;
     }
+    PrefixTable pf{nullptr, nullptr, nullptr, 0u};
+    if (!multi) {
+      const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
+      if (d) {
+        int rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+        if (rc) return rc;
+      }
+    }
 #define DCF_STREAM(XR, MK)                                                                                    \
   hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], scs, \
                      cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,  \
-                     (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys)
+                     (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf)
 #ifdef DCF_STREAM_TT2
     if (xreg && !multi) {
       uint64_t b2 = (units + 9) / 10;
       if (b2 > 2 * (uint64_t)p->cus) b2 = 2 * (uint64_t)p->cus;
       hipLaunchKernelGGL((k_eval16_stream<2, true, false, 640, true>), dim3((unsigned)b2), dim3(640), 0, st, p->d_tab,
                          p->rk[0], scs, cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes,
-                         (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys);
+                         (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf);
     } else
 #endif
     if (xreg && multi) DCF_STREAM(true, true);

@@ -48,23 +48,25 @@ struct StreamLane {
   bool alive[NS];
 };
 
+// Shared prefix (single key): the walk's state after its first `levels` levels depends
+// only on those bits of x, so the host expands that top tree once (the full-domain
+// level kernels, k_fd_level16) into a table indexed by the prefix, and a point
+// starts at level `levels` from its table row.  levels = 0: no table.
+struct PrefixTable {
+  const uint4* s;
+  const uint4* v;
+  const uint8_t* t;
+  uint32_t levels;  // < 32 and < 8N
+};
+
 template <int NS, bool XREG, bool MULTI>
 __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int i, uint64_t p,
                                              const uint4* __restrict__ s0s, const uint4 s0v, uint32_t party,
-                                             const uint8_t* __restrict__ xs, uint32_t nbytes, uint64_t ppk) {
+                                             const uint8_t* __restrict__ xs, uint32_t nbytes, uint64_t ppk,
+                                             const PrefixTable& pf) {
   const uint64_t k = MULTI ? p / ppk : 0;
-  const uint4 sv = MULTI ? s0s[k] : s0v;  // k.s0s[0] (lib.rs:168)
-  L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) L.v[i][j] = 0u;
-  L.t[i] = party;  // lib.rs:169
-  L.ph[i] = 0u;
-  L.lev[i] = 0u;
-  L.ci[i] = k * (8u * nbytes);  // key-major digest row (MULTI); level 0 of the single key otherwise
-  L.key[i] = k;
-  L.pt[i] = p;
-  L.alive[i] = true;
   const uint8_t* row = xs + p * nbytes;
+  uint32_t w0;  // first 32 x bits, Msb0 (lib.rs:181)
   if (XREG) {
     if (nbytes == 16) {
       const uint4 x = *reinterpret_cast<const uint4*>(row);
@@ -74,10 +76,42 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
       for (int w = 0; w < 4; ++w)
         L.xw[i][w] = (4u * w < nbytes) ? reinterpret_cast<const uint32_t*>(row)[w] : 0u;
     }
-    L.fresh[i] = true;
+    w0 = bswap32(L.xw[i][0]);
   } else {
     L.xp[i] = row;
-    L.cur[i] = load_bits32(row, 0, nbytes);
+    w0 = load_bits32(row, 0, nbytes);
+  }
+  uint32_t lev0 = 0u;
+  if (!MULTI && pf.levels) {  // start below the shared prefix: its row of the top-tree table
+    lev0 = pf.levels;
+    const uint32_t idx = w0 >> (32u - lev0);
+    const uint4 sv = pf.s[idx], vv = pf.v[idx];
+    L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
+    L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
+    L.t[i] = pf.t[idx];
+  } else {
+    const uint4 sv = MULTI ? s0s[k] : s0v;  // k.s0s[0] (lib.rs:168)
+    L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L.v[i][j] = 0u;
+    L.t[i] = party;  // lib.rs:169
+  }
+  L.ph[i] = 0u;
+  L.lev[i] = lev0;
+  L.ci[i] = k * (8u * nbytes) + lev0;  // key-major digest row (MULTI); the level of the single key otherwise
+  L.key[i] = k;
+  L.pt[i] = p;
+  L.alive[i] = true;
+  if (XREG) {
+    if (lev0) {  // word 0 is consumed here, shifted past the prefix bits
+      L.cur[i] = w0 << lev0;
+      L.xw[i][0] = L.xw[i][1]; L.xw[i][1] = L.xw[i][2]; L.xw[i][2] = L.xw[i][3];
+      L.fresh[i] = false;
+    } else {
+      L.fresh[i] = true;
+    }
+  } else {
+    L.cur[i] = w0 << lev0;
   }
 }
 
@@ -88,7 +122,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
                                               uint64_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
                                               uint64_t nunits, uint64_t total, const uint4* __restrict__ s0s,
                                               const uint4 s0v, uint32_t party, const uint8_t* __restrict__ xs,
-                                              uint32_t nbytes, uint64_t ppk) {
+                                              uint32_t nbytes, uint64_t ppk, const PrefixTable& pf) {
   uint64_t need = __ballot(mine);
   while (need) {
     if (unext >= uend && !exhausted) {
@@ -109,7 +143,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
     }
     const uint32_t rank = lane_rank(need);
     const bool take = mine && (uint64_t)rank < uend - unext;
-    if (take) stream_start(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk);
+    if (take) stream_start(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk, pf);
     const uint64_t taken = __ballot(take);
     unext += (uint64_t)__popcll(taken);
     need &= ~taken;
@@ -155,7 +189,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
-    uint4* __restrict__ ys) {
+    uint4* __restrict__ ys, const PrefixTable pf) {
   __shared__ uint32_t lds[TT2 ? kLdsWords2 : kLdsWords];
   if (TT2)
     lds_fill_tables2(lds, tab);
@@ -177,7 +211,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   }
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    stream_refill(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs, nbytes, ppk);
+    stream_refill(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs, nbytes, ppk, pf);
 
   for (;;) {
     bool any = false;
@@ -271,7 +305,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
       }
       if (__ballot(done))
         stream_refill(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs, nbytes,
-                      ppk);
+                      ppk, pf);
     }
   }
 }

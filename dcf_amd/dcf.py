@@ -157,6 +157,18 @@ class Aes256HirosePrg:
         4 stream (LDS T-table, per-lane block scheduling)."""
         check(_lib.load().dcf_prg_set_eval_mode(self._h, int(mode)))
 
+    def set_prefix_levels(self, levels: int) -> None:
+        """Shared-prefix depth for single-key LAMBDA = 16 eval (Hirose, stream engine):
+        -1 automatic (default), 0 off, > 0 that depth.  Output bytes are identical."""
+        check(_lib.load().dcf_prg_set_prefix_levels(self._h, int(levels)))
+
+    def eval_prefix_levels(self, n_bytes: int, num_keys: int, points_per_key: int) -> int:
+        """The prefix depth an eval of this shape uses (0 = none)."""
+        r = _lib.load().dcf_eval_prefix_levels(self._h, int(n_bytes), int(num_keys), int(points_per_key))
+        if r < 0:
+            check(r)
+        return r
+
     def set_hybrid_split(self, ttable_waves: int, slab_variant: int = 1) -> None:
         """Hybrid engine: T-table waves per workgroup (rest bitsliced); slab_variant 1 = 16-wave
         workgroups with bitsliced state in scratch slabs, 0 = 12 waves with state in registers."""

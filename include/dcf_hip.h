@@ -110,6 +110,20 @@ size_t dcf_prg_lambda(const dcf_prg* prg);
  * test knob only: every engine returns identical bytes. */
 int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 
+/* Shared prefix for single-key eval at LAMBDA = 16 (Hirose PRG, stream engine).
+ * Every point's walk (lib.rs:174-189) passes through the node of the key's GGM
+ * tree named by its first D bits, and that node's (s, v, t) depends on nothing
+ * else, so eval expands the top D levels once (2^(D+1) AES blocks, 33 B per node,
+ * as the full-domain eval does) and starts each point at level D from its node:
+ * D fewer levels per point, identical output bytes.
+ *   levels = -1: automatic (the default): D = log2(points) - 1, at most 24, none
+ *                below 8 or for small batches;
+ *   levels =  0: off;  levels > 0: that depth (capped at 24 and at 8N - 1).
+ * The table lives on the prg (its size follows the largest D used). */
+int dcf_prg_set_prefix_levels(dcf_prg* prg, int levels);
+/* The prefix depth D a dcf_eval* call of this shape would use (0 = none). */
+int dcf_eval_prefix_levels(const dcf_prg* prg, size_t n_bytes, size_t num_keys, size_t points_per_key);
+
 /* Hybrid engine tuning (results are identical for every setting):
  *   slab_variant 1: 16-wave workgroups, bitsliced s/v state in a scratch slab;
  *   slab_variant 0: 12-wave workgroups, bitsliced state in registers;

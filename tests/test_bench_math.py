@@ -38,3 +38,14 @@ def test_wide_roofline_bound(bench):
     assert r["peak"] == pytest.approx(m / t_min / 1e6)
     assert r["frac"] == pytest.approx(t_min / 0.05)
     assert r["unit"] == "M evals/s" and r["bound"] == "lds+hbm"
+
+
+def test_zero_bits_below_prefix(bench):
+    # the stream engine's A blocks: 0 bits of x below a shared prefix of `skip` levels
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(3)
+    x = rng.integers(0, 256, (777, 5), dtype=np.uint8)
+    for skip in (0, 1, 7, 8, 9, 15, 24, 33, 39):
+        want = int((np.unpackbits(x, axis=1)[:, skip:] == 0).sum())
+        assert bench.zero_bits(torch.from_numpy(x), skip) == want, skip

@@ -142,6 +142,48 @@ def test_eval_random_vs_oracle(dcf, nb, mode):
             assert np.array_equal(got, want), (nb, m, b)
 
 
+@pytest.mark.parametrize("nb,levels", [(1, 1), (1, 7), (2, 9), (2, 15), (3, 23), (4, 8), (4, 24), (5, 1),
+                                        (16, 13), (16, 24), (17, 20), (32, 24)])
+def test_eval_prefix_table_vs_oracle(dcf, nb, levels):
+    """Shared-prefix eval (stream engine, forced depth): points start at level D from
+    the key's expanded top tree; the output must not change.  Covers D = 1, D = 8N - 1
+    (the walk's last level only), D across x's word boundary (N = 3: 24 bits) and
+    the 24-level cap (N = 16, 32)."""
+    rng = np.random.default_rng(700 + 31 * nb + levels)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    prg.set_eval_mode(4)
+    prg.set_prefix_levels(levels)
+    want_d = min(levels, 24, 8 * nb - 1)
+    m = 3001
+    assert prg.eval_prefix_levels(nb, 1, m) == want_d
+    d = dcf.DcfImpl(nb, 16, prg)
+    for bound in (0, 1):
+        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
+        ok = O.gen(P, alpha, beta, s0, s1, bound)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
+        xs = _rand(rng, (m, nb))
+        a = np.frombuffer(alpha, np.uint8)
+        xs[0] = a
+        xs[1] = 0
+        xs[2] = 255
+        xs[3:40] = a  # points sharing alpha's prefix, differing in the last byte
+        xs[3:40, -1] = rng.integers(0, 256, 37, dtype=np.uint8)
+        for b, s in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+            want = O.eval_(P, b, ok, s, xs, nthreads=8)
+            assert np.array_equal(got, want), (nb, levels, bound, b)
+    prg.set_prefix_levels(0)
+    assert prg.eval_prefix_levels(nb, 1, m) == 0
+    prg.set_prefix_levels(-1)
+    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 24  # auto: log2(points) - 1, capped
+    assert prg.eval_prefix_levels(16, 1, 1 << 20) == 19
+    assert prg.eval_prefix_levels(2, 1, 1 << 20) == 15   # < 8N
+    assert prg.eval_prefix_levels(16, 2, 1 << 20) == 0   # one key only
+    with pytest.raises(dcf.DcfError):
+        prg.set_prefix_levels(-2)
+
+
 def test_eval_length_mismatch_is_error(dcf):
     prg = dcf.Aes256HirosePrg(REF_KEYS, 16)
     d = dcf.DcfImpl(16, 16, prg)
