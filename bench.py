@@ -70,7 +70,7 @@ def engine_peak(engine: str) -> float:
     return hybrid_peak()
 
 
-def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int):
+def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels: int = 0):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, written by scripts/prof_summary.py from
     scripts/gpu_profile.sh: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md §HBM),
@@ -81,8 +81,8 @@ def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int):
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if (t.get("kernel"), t.get("points_per_launch"), t.get("n_bytes"), t.get("lambda")) != (kernel, points, n_bytes,
-                                                                                            lam):
+    if (t.get("kernel"), t.get("points_per_launch"), t.get("n_bytes"), t.get("lambda"),
+            t.get("prefix_levels", 0)) != (kernel, points, n_bytes, lam, prefix_levels):
         return None
     return t.get("traffic_bytes")
 
@@ -267,7 +267,7 @@ def run_eval(args, world, rank):
         w0, k0 = timed(args.steps)
         prg.set_prefix_levels(args.prefix)
         no_prefix = {"value": m * world * args.steps * parties / w0, "kernel_ms": k0 * 1e3,
-                     "executed_blocks_per_eval": 8 * nb + zero_bits(xs) / m,
+                     "executed_blocks_per_eval": 16 * nb if args.prg == "mmo" else 8 * nb + zero_bits(xs) / m,
                      "speedup": w0 / wall}
     total_evals = m * world * args.steps * parties
     value = total_evals / wall
@@ -283,8 +283,13 @@ def run_eval(args, world, rank):
     # stream engine, which encrypts B on every level and A on left (x bit 0) levels only.
     # With a shared-prefix table of depth D a point walks levels D..8N-1 only, and the
     # table costs 2 blocks per node of the top tree (2^(D+1) - 2), spread over the batch.
-    exec_bpe = ((8 * nb - pfx) + zero_bits(xs, pfx) / m + (2 ** (pfx + 1) - 2) / m) if engine == "stream" \
-        else bpe  # mmo: 2 AES-128 per level
+    # MMO: 2 AES-128 blocks per level below the prefix (the table: 2 per node as well).
+    if engine == "stream":
+        exec_bpe = (8 * nb - pfx) + zero_bits(xs, pfx) / m + (2 ** (pfx + 1) - 2) / m
+    elif engine == "mmo":
+        exec_bpe = 2 * (8 * nb - pfx) + (2 ** (pfx + 1) - 2) / m
+    else:
+        exec_bpe = bpe
     if lam > 16:
         # LAMBDA >= 32: the stream head encrypts B, A (left) or B, D, C (right) per level, and the
         # tail writes LAMBDA - 32 output bytes per eval: time bound = AES (LDS) + output (HBM write).
@@ -292,6 +297,9 @@ def run_eval(args, world, rank):
         if engine == "stream-head":
             exec_bpe = 3 * 8 * nb - zero_bits(xs) / m
     per_gpu_blocks = m * exec_bpe / kern_s
+    # HBM bytes per launch of the dominant kernel: x in, y out, and with a shared prefix
+    # one 32-byte table row gathered per point (kernels16.h PrefixTable)
+    alg_bytes = m * (nb + lam) + (m * 32 if pfx else 0)
     kernel = KERNEL.get(engine, "k_eval16") if lam == 16 else (
         "k_eval_wide_head_stream+k_eval_wide_tail" if engine == "stream-head" else "k_eval_wide_head+k_eval_wide_tail")
     peak = engine_peak(engine)
@@ -310,15 +318,16 @@ def run_eval(args, world, rank):
             "bound": "lds" if engine in ("ttable", "ttable-small", "stream", "mmo") else ("valu" if engine == "bitsliced" else "lds+valu"),
             "kernel": kernel, "engine": engine,
             "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-128 blocks/s" if engine == "mmo" else "G AES-256 blocks/s",
-            "frac": per_gpu_blocks / peak, "traffic": pmc_traffic(kernel, m, nb, lam),
-            "algorithmic_bytes": m * (nb + lam), "kernel_ms": kern_s * 1e3,
-            "hbm_GBps": m * (nb + lam) / kern_s / 1e9,
+            "frac": per_gpu_blocks / peak, "traffic": pmc_traffic(kernel, m, nb, lam, pfx),
+            "algorithmic_bytes": alg_bytes, "kernel_ms": kern_s * 1e3,
+            "hbm_GBps": alg_bytes / kern_s / 1e9,
             "ttable_only_peak": PEAK_TT_BLOCKS / 1e9,
             "executed_blocks_per_eval": exec_bpe, "reference_blocks_per_eval": bpe,
             "prefix_levels": pfx, "no_prefix": no_prefix,
-            "note": "achieved = AES-256 blocks the kernel encrypts per second (stream engine: B every "
-                    "level + A on left levels, below a shared-prefix table of prefix_levels levels built "
-                    "inside the timed call and counted; other engines: the reference count, 2 per level); "
+            "note": "achieved = AES blocks the kernel encrypts per second (stream engine: B every "
+                    "level + A on left levels; mmo: 2 AES-128 per level; both below a shared-prefix table "
+                    "of prefix_levels levels built inside the timed call and counted; other engines: the "
+                    "reference count, 2 per level); "
                     "aes_blocks_per_s above uses the reference count.  Peak per GPU at 2.4 GHz: T-table "
                     "engines LDS-bound (32 ds_read_b32 lookups/clk/CU, 224 per block), bitsliced VALU-bound "
                     "(128 lane-ops/clk/CU, ~800 per block); hybrid = LDS-saturating T-table + bitsliced on "

@@ -142,7 +142,7 @@ int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
 // (1.44 without); C3 (2^28, N = 16): D = 16 / 24 -> 450 / 477 M (397 M without).
 constexpr uint32_t kPrefixMax = 24;
 uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
-  if (p->kind != 0 || p->lambda != 16 || num_keys != 1 || p->prefix_levels == 0) return 0;
+  if (p->lambda != 16 || num_keys != 1 || p->prefix_levels == 0) return 0;
   uint32_t d;
   if (p->prefix_levels > 0) {
     d = (uint32_t)p->prefix_levels;
@@ -185,15 +185,24 @@ int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const 
   const uint32_t nlev = (uint32_t)(8 * n_bytes);  // > levels: no level here is the last one
   for (uint32_t lev = 0; lev < levels; ++lev) {
     const uint64_t parents = 1ull << lev;
-    hipLaunchKernelGGL(k_fd_level16, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
-                       p->rk[0], cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b,
-                       (uint4*)nullptr, ctrs + lev);
+    if (p->kind == 1)
+      hipLaunchKernelGGL(k_fd_level16_mmo, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                         p->d_rk128, cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b,
+                         (uint4*)nullptr, ctrs + lev);
+    else
+      hipLaunchKernelGGL(k_fd_level16, dim3((unsigned)grid_for(parents, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                         p->rk[0], cws, cwv, cwt, np1, lev, nlev, parents, s_a, v_a, t_a, s_b, v_b, t_b,
+                         (uint4*)nullptr, ctrs + lev);
     HIP_TRY(hipGetLastError());
     std::swap(s_a, s_b);
     std::swap(v_a, v_b);
     std::swap(t_a, t_b);
   }
-  *out = PrefixTable{s_a, v_a, t_a, levels};
+  // 32-byte rows (kernels16.h PrefixTable) into the other buffer: 2^D * 32 <= half.
+  hipLaunchKernelGGL(k_prefix_pack, dim3((unsigned)std::min<uint64_t>((maxnodes + 255) / 256, 4096)), dim3(256), 0,
+                     st, s_a, v_a, t_a, maxnodes, s_b);
+  HIP_TRY(hipGetLastError());
+  *out = PrefixTable{s_b, levels};
   return DCF_OK;
 }
 
@@ -419,8 +428,11 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   if (!p) return fail(DCF_ERR_ARG, "null prg");
   if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
   const uint64_t total = (uint64_t)num_keys * points_per_key;
-  // the paths eval_launch takes without a table: small batches in auto mode, non-stream engines
-  if (p->eval_mode == DCF_EVAL_AUTO && total < (uint64_t)p->cus * kBlock * 2) return 0;
+  // the paths eval_launch takes without a table: small batches (MMO: at auto depth; Hirose: in
+  // auto mode), Hirose engines other than the stream engine (MMO ignores the engine setting)
+  const bool small = total < (uint64_t)p->cus * kBlock * 2;
+  if (p->kind == 1) return small && p->prefix_levels < 0 ? 0 : (int)prefix_depth(p, n_bytes, num_keys, total);
+  if (p->eval_mode == DCF_EVAL_AUTO && small) return 0;
   if (p->eval_mode != DCF_EVAL_AUTO && p->eval_mode != DCF_EVAL_STREAM) return 0;
   return (int)prefix_depth(p, n_bytes, num_keys, total);
 }
@@ -512,7 +524,16 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #define DCF_MMO(MODE)                                                                                          \
   hipLaunchKernelGGL(k_eval16_mmo<MODE>, grid, block, 0, st, p->d_tab, p->d_rk128, cws, cwv, cwt, np1,            \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk, \
-                     (uint4*)ys)
+                     (uint4*)ys, pf)
+    PrefixTable pf{nullptr, 0u};
+    // auto depth: none for small batches (latency-bound: the table's D launches cost what it saves)
+    if (num_keys == 1 && (p->prefix_levels > 0 || total >= (uint64_t)p->cus * kBlock * 2)) {
+      const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
+      if (d) {
+        int rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+        if (rc) return rc;
+      }
+    }
     if (num_keys == 1) DCF_MMO(0);
     else if (ppk % 64 == 0) DCF_MMO(1);
     else DCF_MMO(2);
@@ -623,7 +644,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
       scs = (const uint4*)p->d_kdig;
       sct = p->d_kdig + (size_t)num_keys * n * 32;
     }
-    PrefixTable pf{nullptr, nullptr, nullptr, 0u};
+    PrefixTable pf{nullptr, 0u};
     if (!multi) {
       const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
       if (d) {

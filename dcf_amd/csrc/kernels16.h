@@ -417,6 +417,37 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_tail16(
   }
 }
 
+// Shared prefix (single key): the walk's state after its first `levels` levels depends
+// only on those bits of x, so the host expands that top tree once (the full-domain
+// level kernels, k_fd_level16 / k_fd_level16_mmo) into a table indexed by the prefix, and a point
+// starts at level `levels` from its table row.  levels = 0: no table.
+// Row i is 32 contiguous bytes, sv[2i] = s and sv[2i+1] = v, with t in s's bit 0 of
+// byte 15: below the root s is always masked there (s' = side & M ^ t*cw.s, and cw.s
+// is a XOR of two masked seeds, lib.rs:119-121 / prg.rs:63-68), so a point's start
+// is one 32-byte gather (one cache line) instead of three arrays' lines.
+struct PrefixTable {
+  const uint4* sv;
+  uint32_t levels;  // < 32 and < 8N
+};
+
+__device__ __forceinline__ void prefix_row(const PrefixTable& pf, uint32_t idx, uint4& s, uint4& v, uint32_t& t) {
+  s = pf.sv[2u * idx];
+  v = pf.sv[2u * idx + 1u];
+  t = (s.w >> 24) & 1u;
+  s.w &= kMaskLast;
+}
+
+// Pack the prefix level's (s, v, t) arrays into PrefixTable rows.
+__global__ void k_prefix_pack(const uint4* __restrict__ s, const uint4* __restrict__ v,
+                              const uint8_t* __restrict__ t, const uint64_t n, uint4* __restrict__ sv) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint4 a = s[i];
+    a.w = (a.w & kMaskLast) | ((uint32_t)(t[i] & 1u) << 24);
+    sv[2 * i] = a;
+    sv[2 * i + 1] = v[i];
+  }
+}
+
 // Root node for full-domain eval: s = s0 (k.s0s[0]), v = 0, t = party.
 __global__ void k_fd_root16(const uint4* __restrict__ s0, const uint32_t party, uint4* __restrict__ s,
                             uint4* __restrict__ v, uint8_t* __restrict__ t) {

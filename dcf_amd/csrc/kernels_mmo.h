@@ -12,6 +12,7 @@
 #pragma once
 
 #include "aes_lds.h"
+#include "kernels16.h"
 
 namespace {
 
@@ -29,17 +30,25 @@ __device__ __forceinline__ uint4 mmo_eval_one(const uint32_t* lds, uint32_t lc, 
                                               const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
                                               const uint8_t* __restrict__ cw_t, const uint4 np, const uint4 sv,
                                               uint32_t party, const uint8_t* __restrict__ x, uint32_t nbytes,
-                                              uint64_t num_keys, uint64_t key) {
+                                              uint64_t num_keys, uint64_t key, const PrefixTable& pf) {
   const uint32_t nlev = 8u * nbytes;
   const uint32_t nchunk = (nbytes + 3u) >> 2;
   uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w};
   uint32_t v[4] = {0u, 0u, 0u, 0u};
   uint32_t t = party;
   uint32_t lev = 0;
+  uint32_t w0 = load_bits32(x, 0, nbytes);
+  if (pf.levels) {  // one key: start below the shared prefix (wave-uniform depth)
+    lev = pf.levels;
+    uint4 ps, pv;
+    prefix_row(pf, w0 >> (32u - lev), ps, pv, t);
+    s[0] = ps.x; s[1] = ps.y; s[2] = ps.z; s[3] = ps.w;
+    v[0] = pv.x; v[1] = pv.y; v[2] = pv.z; v[3] = pv.w;
+  }
   for (uint32_t c = 0; c < nchunk; ++c) {
-    uint32_t cur = load_bits32(x, c, nbytes);
+    uint32_t cur = c ? load_bits32(x, c, nbytes) : w0 << lev;  // levels < 32: the prefix sits in word 0
     const uint32_t lend = min(32u, nlev - 32u * c);
-    for (uint32_t b = 0; b < lend; ++b, ++lev) {
+    for (uint32_t b = c ? 0u : lev; b < lend; ++b, ++lev) {
       const uint32_t xb = cur >> 31;  // Msb0 bit of x (lib.rs:181)
       cur <<= 1;
       const uint4* const rk[2] = {rks + kMmoRk * (2u * xb), rks + kMmoRk * (2u * xb + 1u)};
@@ -73,7 +82,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_mmo(
     const uint32_t* __restrict__ tab, const uint4* __restrict__ rk128, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
-    const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys) {
+    const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys, const PrefixTable pf) {
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint4 rks[4 * kMmoRk];
   lds_fill_rk128(rks, rk128);
@@ -89,7 +98,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_mmo(
     if (MODE == 1) key = __builtin_amdgcn_readfirstlane((uint32_t)(gg / points_per_key));
     if (MODE == 2) key = gg / points_per_key;
     const uint4 y = mmo_eval_one(lds, lc, rks, cw_s, cw_v, cw_t, cw_np1[key], s0s[key], party, xs + gg * nbytes,
-                                 nbytes, num_keys, key);
+                                 nbytes, num_keys, key, pf);
     if (live) ys[g] = y;
   }
 }

@@ -28,6 +28,7 @@
 #pragma once
 
 #include "aes_lds.h"
+#include "kernels16.h"
 
 namespace {
 
@@ -46,17 +47,6 @@ struct StreamLane {
   const uint8_t* xp[NS];          // !XREG: the point's row in xs
   uint64_t ci[NS], pt[NS], key[NS];
   bool alive[NS];
-};
-
-// Shared prefix (single key): the walk's state after its first `levels` levels depends
-// only on those bits of x, so the host expands that top tree once (the full-domain
-// level kernels, k_fd_level16) into a table indexed by the prefix, and a point
-// starts at level `levels` from its table row.  levels = 0: no table.
-struct PrefixTable {
-  const uint4* s;
-  const uint4* v;
-  const uint8_t* t;
-  uint32_t levels;  // < 32 and < 8N
 };
 
 template <int NS, bool XREG, bool MULTI>
@@ -84,11 +74,10 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
   uint32_t lev0 = 0u;
   if (!MULTI && pf.levels) {  // start below the shared prefix: its row of the top-tree table
     lev0 = pf.levels;
-    const uint32_t idx = w0 >> (32u - lev0);
-    const uint4 sv = pf.s[idx], vv = pf.v[idx];
+    uint4 sv, vv;
+    prefix_row(pf, w0 >> (32u - lev0), sv, vv, L.t[i]);
     L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
     L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
-    L.t[i] = pf.t[idx];
   } else {
     const uint4 sv = MULTI ? s0s[k] : s0v;  // k.s0s[0] (lib.rs:168)
     L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
@@ -209,6 +198,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     L.ci[i] = 0;
     L.ph[i] = 0u;
   }
+  const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
 #pragma unroll
   for (int i = 0; i < NS; ++i)
     stream_refill(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs, nbytes, ppk, pf);
@@ -298,7 +288,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
       if (done) {
-        const uint4 np = cw_np1[L.key[i]];
+        const uint4 np = MULTI ? cw_np1[L.key[i]] : np1v;
         const uint32_t tm = 0u - L.t[i];
         ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
                                  L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));

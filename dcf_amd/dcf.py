@@ -158,7 +158,7 @@ class Aes256HirosePrg:
         check(_lib.load().dcf_prg_set_eval_mode(self._h, int(mode)))
 
     def set_prefix_levels(self, levels: int) -> None:
-        """Shared-prefix depth for single-key LAMBDA = 16 eval (Hirose, stream engine):
+        """Shared-prefix depth for single-key LAMBDA = 16 eval (Hirose: stream engine; MMO):
         -1 automatic (default), 0 off, > 0 that depth.  Output bytes are identical."""
         check(_lib.load().dcf_prg_set_prefix_levels(self._h, int(levels)))
 

@@ -110,7 +110,8 @@ size_t dcf_prg_lambda(const dcf_prg* prg);
  * test knob only: every engine returns identical bytes. */
 int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 
-/* Shared prefix for single-key eval at LAMBDA = 16 (Hirose PRG, stream engine).
+/* Shared prefix for single-key eval at LAMBDA = 16 (Hirose PRG: stream engine;
+ * Aes128MatyasMeyerOseasPrg: every engine setting).
  * Every point's walk (lib.rs:174-189) passes through the node of the key's GGM
  * tree named by its first D bits, and that node's (s, v, t) depends on nothing
  * else, so eval expands the top D levels once (2^(D+1) AES blocks, 33 B per node,

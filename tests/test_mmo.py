@@ -205,3 +205,34 @@ def test_gpu_mmo_errors(dcf):
     with pytest.raises(dcf.DcfError) as e:
         dcf.Aes128MatyasMeyerOseasPrg([bytes(16)] * 8, 32)
     assert e.value.code == -7
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb,levels", [(1, 1), (1, 7), (2, 15), (3, 23), (4, 24), (16, 13), (16, 24), (17, 20)])
+def test_gpu_mmo_eval_prefix_table_vs_oracle(dcf, nb, levels):
+    """Shared-prefix eval with the MMO PRG (forced depth D): points start at level D
+    from the key's top tree, expanded by the MMO full-domain level kernel; output
+    unchanged.  D = 8N - 1, D across x's word boundary and the 24-level cap."""
+    rng = np.random.default_rng(900 + 31 * nb + levels)
+    keys = [rng.bytes(16) for _ in range(4)]
+    prg, P = dcf.Aes128MatyasMeyerOseasPrg(keys, 16), O.OracleMmoPrg(keys, 16)
+    prg.set_prefix_levels(levels)
+    m = 3001
+    assert prg.eval_prefix_levels(nb, 1, m) == min(levels, 24, 8 * nb - 1)
+    d = dcf.DcfImpl(nb, 16, prg)
+    for bound in (0, 1):
+        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
+        ok = O.gen(P, alpha, beta, s0, s1, bound)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
+        xs = rng.integers(0, 256, size=(m, nb), dtype=np.uint8)
+        a = np.frombuffer(alpha, np.uint8)
+        xs[0], xs[1], xs[2] = a, 0, 255
+        xs[3:40] = a
+        xs[3:40, -1] = rng.integers(0, 256, 37, dtype=np.uint8)
+        for b, s in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+            assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (nb, levels, bound, b)
+    prg.set_prefix_levels(-1)
+    assert prg.eval_prefix_levels(16, 1, m) == 0           # auto: no table for small batches
+    assert prg.eval_prefix_levels(16, 1, 1 << 22) == 21    # auto: log2(points) - 1
+    assert prg.eval_prefix_levels(16, 2, 1 << 22) == 0     # one key only
