@@ -51,9 +51,9 @@ def hybrid_peak() -> float:
     return b_tt + max(0.0, valu_left) / BS_VALU_PER_BLOCK
 
 
-ENGINE = {0: "stream", 1: "ttable", 2: "bitsliced", 3: "hybrid", 4: "stream"}
+ENGINE = {0: "stream", 1: "ttable", 2: "bitsliced", 3: "hybrid", 4: "stream", 5: "stream-hybrid"}
 KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "ttable-small": "k_eval16", "bitsliced": "k_eval16_bs",
-          "stream": "k_eval16_stream", "mmo": "k_eval16_mmo"}
+          "stream": "k_eval16_stream", "mmo": "k_eval16_mmo", "stream-hybrid": "k_eval16_shybrid"}
 
 
 # MMO (AES-128, kernels_mmo.h): 10 rounds x 16 lookups + 11 round-key ds_read_b128 (16 lanes/clk) per block
@@ -217,6 +217,8 @@ def run_eval(args, world, rank):
     prg.set_eval_mode(args.eval_mode)
     if args.hybrid_split is not None:
         prg.set_hybrid_split(args.hybrid_split, args.hybrid_mem)
+    if args.shy_mask is not None:
+        prg.set_stream_hybrid(int(args.shy_mask, 0), args.shy_prio)
     prg.set_prefix_levels(args.prefix)
     pfx = prg.eval_prefix_levels(nb, 1, m)  # shared-prefix depth this eval uses (0 = none)
     d = dcf_amd.DcfImpl(nb, lam, prg)
@@ -273,7 +275,7 @@ def run_eval(args, world, rank):
     value = total_evals / wall
     bpe = blocks_per_eval(nb, lam)
     engine = ENGINE[args.eval_mode] if lam == 16 else "ttable"
-    if engine in ("hybrid", "bitsliced") and nb > 16:
+    if engine in ("hybrid", "bitsliced", "stream-hybrid") and nb > 16:
         engine = "ttable"
     if args.prg == "mmo":
         engine = "mmo"
@@ -486,6 +488,8 @@ def main():
                     help="shared-prefix table depth for single-key eval: -1 auto (library default), 0 off")
     ap.add_argument("--no-compare", action="store_true", help="skip the no-prefix comparison timing")
     ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves per workgroup")
+    ap.add_argument("--shy-mask", default=None, help="stream-hybrid (eval mode 5): stream-wave mask, e.g. 0x7777")
+    ap.add_argument("--shy-prio", type=int, default=0, help="stream-hybrid: 1 = stream waves at raised priority")
     ap.add_argument("--hybrid-mem", type=int, default=1, help="hybrid: 1 = 16 waves + scratch slabs, 0 = 12 waves")
     args = ap.parse_args()
     args.lam = 16

@@ -38,6 +38,7 @@
 #include "kernels_stream.h"
 #include "kernels_mmo.h"
 #include "kernels_wide_stream.h"
+#include "kernels_shybrid.h"
 
 namespace {
 
@@ -113,6 +114,8 @@ struct dcf_prg {
   size_t pfx_bytes = 0;
   int hybrid_tt_waves = 13;   // T-table waves per hybrid workgroup (r01 sweep: 13 of 16 best)
   int hybrid_mem = 1;         // 1: 16-wave workgroups with s/v slabs; 0: 12 waves, s/v in registers
+  uint32_t shy_mask = 0x7777; // stream-hybrid: stream waves (bit w = wave w); 0x7777 = one SIMD bitsliced
+  int shy_prio = 0;           // stream-hybrid: raise the stream waves' issue priority
 };
 
 namespace {
@@ -140,18 +143,19 @@ int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
 // point), at most 24 (a 553 MB table), none below 8, always < 8N.  Measured (r01i,
 // C2: 2^24 points, N = 4): D = 12 / 16 / 20 / 24 -> 2.00 / 2.29 / 2.62 / 2.83 G evals/s
 // (1.44 without); C3 (2^28, N = 16): D = 16 / 24 -> 450 / 477 M (397 M without).
-constexpr uint32_t kPrefixMax = 24;
+constexpr uint32_t kPrefixMax = 24;       // auto
+constexpr uint32_t kPrefixMaxForced = 28;  // dcf_prg_set_prefix_levels (2^28 x 33 B x 2 = 17.7 GB)
 uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
   if (p->lambda != 16 || num_keys != 1 || p->prefix_levels == 0) return 0;
   uint32_t d;
   if (p->prefix_levels > 0) {
-    d = (uint32_t)p->prefix_levels;
+    d = std::min((uint32_t)p->prefix_levels, kPrefixMaxForced);
   } else {
     const uint32_t lg = 63u - (uint32_t)__builtin_clzll(total | 1u);
     d = lg > 1u ? lg - 1u : 0u;
     if (d < 8u) return 0;
+    d = std::min(d, kPrefixMax);
   }
-  d = std::min(d, kPrefixMax);
   return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
 }
 
@@ -412,7 +416,7 @@ size_t dcf_prg_lambda(const dcf_prg* p) { return p ? p->lambda : 0; }
 
 int dcf_prg_set_eval_mode(dcf_prg* p, int mode) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");
-  if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_STREAM) return fail(DCF_ERR_ARG, "bad eval mode");
+  if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_STREAM_HYBRID) return fail(DCF_ERR_ARG, "bad eval mode");
   p->eval_mode = mode;
   return DCF_OK;
 }
@@ -433,7 +437,8 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   const bool small = total < (uint64_t)p->cus * kBlock * 2;
   if (p->kind == 1) return small && p->prefix_levels < 0 ? 0 : (int)prefix_depth(p, n_bytes, num_keys, total);
   if (p->eval_mode == DCF_EVAL_AUTO && small) return 0;
-  if (p->eval_mode != DCF_EVAL_AUTO && p->eval_mode != DCF_EVAL_STREAM) return 0;
+  if (p->eval_mode != DCF_EVAL_AUTO && p->eval_mode != DCF_EVAL_STREAM && p->eval_mode != DCF_EVAL_STREAM_HYBRID)
+    return 0;
   return (int)prefix_depth(p, n_bytes, num_keys, total);
 }
 
@@ -443,6 +448,31 @@ int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves, int slab_variant) {
   if (slab_variant != 0 && slab_variant != 1) return fail(DCF_ERR_ARG, "slab_variant must be 0 or 1");
   p->hybrid_tt_waves = ttable_waves;
   p->hybrid_mem = slab_variant;
+  return DCF_OK;
+}
+
+int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priority) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  if (ttable_wave_mask > 0xFFFFu || __builtin_popcount(ttable_wave_mask) < 16 - kShybridXlSlots)
+    return fail(DCF_ERR_ARG, "ttable_wave_mask: 16 bits, at least 4 set");
+  if (priority != 0 && priority != 1) return fail(DCF_ERR_ARG, "priority must be 0 or 1");
+  p->shy_mask = ttable_wave_mask;
+  p->shy_prio = priority;
+  return DCF_OK;
+}
+
+// Per-wave scratch slabs (bitsliced v) for every 16-wave workgroup of the hybrid kernels.
+static int ensure_slabs(dcf_prg* p, hipStream_t st) {
+  const size_t need = (size_t)p->cus * 16 * kSlabUint4 * sizeof(uint4);
+  if (p->slab_bytes >= need) return DCF_OK;
+  if (p->d_slabs) {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipFree(p->d_slabs));
+    p->d_slabs = nullptr;
+    p->slab_bytes = 0;
+  }
+  HIP_TRY(hipMalloc(&p->d_slabs, need));
+  p->slab_bytes = need;
   return DCF_OK;
 }
 
@@ -589,17 +619,8 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
     uint4* slabs = nullptr;
     if (mem) {
-      const size_t need = (size_t)p->cus * 16 * kSlabUint4 * sizeof(uint4);
-      if (p->slab_bytes < need) {
-        if (p->d_slabs) {
-          HIP_TRY(hipStreamSynchronize(st));
-          HIP_TRY(hipFree(p->d_slabs));
-          p->d_slabs = nullptr;
-          p->slab_bytes = 0;
-        }
-        HIP_TRY(hipMalloc(&p->d_slabs, need));
-        p->slab_bytes = need;
-      }
+      int rc = ensure_slabs(p, st);
+      if (rc) return rc;
       slabs = reinterpret_cast<uint4*>(p->d_slabs);
     }
     const dim3 g((unsigned)blocks), b((unsigned)(waves * 64));
@@ -613,6 +634,27 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     else if (mem) DCF_HYB(false, true);
     else DCF_HYB(false, false);
 #undef DCF_HYB
+  } else if (mode == DCF_EVAL_STREAM_HYBRID) {
+    if (!(num_keys == 1 && n_bytes % 4 == 0 && n_bytes <= 16))
+      return fail(DCF_ERR_UNSUPPORTED, "stream-hybrid eval: single key, N % 4 == 0, N <= 16");
+    const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
+    if (units > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "stream-hybrid eval: more than 2^32 work units");
+    int rc = ensure_slabs(p, st);
+    if (rc) return rc;
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
+    PrefixTable pf{nullptr, 0u};
+    const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
+    if (d) {
+      rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+      if (rc) return rc;
+    }
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+    uint64_t blocks = (units + 15) / 16;
+    if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
+    hipLaunchKernelGGL(k_eval16_shybrid, dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
+                       (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, p->d_ctr,
+                       (uint4*)ys, pf, p->shy_mask, (uint32_t)p->shy_prio, reinterpret_cast<uint4*>(p->d_slabs),
+                       p->d_km);
   } else if (mode == DCF_EVAL_STREAM) {
 #ifndef DCF_STREAM_NS
 #define DCF_STREAM_NS 2  // streams per lane

@@ -106,7 +106,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
 
 // Give every lane whose stream i is free (`mine`) a new point, or retire the
 // stream when the counter is exhausted.  Called in wave-uniform control flow.
-template <int NS, bool XREG, bool MULTI>
+template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit>
 __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint64_t& unext,
                                               uint64_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
                                               uint64_t nunits, uint64_t total, const uint4* __restrict__ s0s,
@@ -119,8 +119,8 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
       if (u >= nunits) {
         exhausted = true;
       } else {
-        unext = (uint64_t)u * kStreamUnit;
-        uend = min(unext + kStreamUnit, total);
+        unext = (uint64_t)u * UNIT;
+        uend = min(unext + (uint64_t)UNIT, total);
       }
     }
     if (exhausted && unext >= uend) {
@@ -171,22 +171,17 @@ __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ c
   }
 }
 
-// TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.
-template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false>
-__global__ __launch_bounds__(WG, 1) void k_eval16_stream(
-    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+// The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
+template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT>
+__device__ __forceinline__ void stream_run(
+    const uint32_t* lds, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
-    uint4* __restrict__ ys, const PrefixTable pf) {
-  __shared__ uint32_t lds[TT2 ? kLdsWords2 : kLdsWords];
-  if (TT2)
-    lds_fill_tables2(lds, tab);
-  else
-    lds_fill_tables(lds, tab);
+    uint4* __restrict__ ys, const PrefixTable& pf) {
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
-  const uint64_t nunits = (total + kStreamUnit - 1) / kStreamUnit;
+  const uint64_t nunits = (total + UNIT - 1) / UNIT;
   uint64_t unext = 0, uend = 0;
   bool exhausted = false;
   const uint4 s0v = s0s[0];
@@ -201,7 +196,8 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    stream_refill(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs, nbytes, ppk, pf);
+    stream_refill<NS, XREG, MULTI, UNIT>(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs,
+                                         nbytes, ppk, pf);
 
   for (;;) {
     bool any = false;
@@ -294,10 +290,27 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
                                  L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
       }
       if (__ballot(done))
-        stream_refill(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs, nbytes,
-                      ppk, pf);
+        stream_refill<NS, XREG, MULTI, UNIT>(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s, s0v,
+                                             party, xs, nbytes, ppk, pf);
     }
   }
+}
+
+// TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.
+template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false>
+__global__ __launch_bounds__(WG, 1) void k_eval16_stream(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
+    const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
+    uint4* __restrict__ ys, const PrefixTable pf) {
+  __shared__ uint32_t lds[TT2 ? kLdsWords2 : kLdsWords];
+  if (TT2)
+    lds_fill_tables2(lds, tab);
+  else
+    lds_fill_tables(lds, tab);
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit>(lds, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys,
+                                                ppk, total, ctr, ys, pf);
 }
 
 }  // namespace

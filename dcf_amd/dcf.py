@@ -154,7 +154,7 @@ class Aes256HirosePrg:
 
     def set_eval_mode(self, mode: int) -> None:
         """AES engine for LAMBDA = 16 eval: 0 auto, 1 LDS T-table, 2 VALU bitsliced, 3 hybrid,
-        4 stream (LDS T-table, per-lane block scheduling)."""
+        4 stream (LDS T-table, per-lane block scheduling), 5 stream + bitsliced waves."""
         check(_lib.load().dcf_prg_set_eval_mode(self._h, int(mode)))
 
     def set_prefix_levels(self, levels: int) -> None:
@@ -173,6 +173,12 @@ class Aes256HirosePrg:
         """Hybrid engine: T-table waves per workgroup (rest bitsliced); slab_variant 1 = 16-wave
         workgroups with bitsliced state in scratch slabs, 0 = 12 waves with state in registers."""
         check(_lib.load().dcf_prg_set_hybrid_split(self._h, int(ttable_waves), int(slab_variant)))
+
+    def set_stream_hybrid(self, ttable_wave_mask: int, priority: int = 0) -> None:
+        """Stream-hybrid engine (mode 5): bit w of the mask = wave w of the 16-wave workgroup
+        runs the stream T-table engine, clear = bitsliced (waves w and w + 4 share a SIMD);
+        priority 1 raises the stream waves' issue priority.  Output bytes are identical."""
+        check(_lib.load().dcf_prg_set_stream_hybrid(self._h, int(ttable_wave_mask), int(priority)))
 
     def gen(self, seed: bytes):
         """`Prg::gen` (lib.rs:52-54) for one seed — the GPU PRG kernel, not a CPU path."""

@@ -74,6 +74,7 @@ extern "C" {
 #define DCF_EVAL_BITSLICED 2 /* VALU bitsliced AES, 32 points per lane quad (single key, N <= 16) */
 #define DCF_EVAL_HYBRID 3    /* both engines side by side on every CU (single key, N <= 16) */
 #define DCF_EVAL_STREAM 4    /* LDS T-table AES, per-lane block scheduling: a right step encrypts B only */
+#define DCF_EVAL_STREAM_HYBRID 5 /* STREAM waves + bitsliced waves on every CU (single key, N % 4 == 0, N <= 16) */
 
 /* Opaque: an Aes256HirosePrg (prg.rs:22-24) whose AES-256 schedules live on one
  * device, i.e. `DcfImpl::new(Aes256HirosePrg::new(keys))` (lib.rs:74, prg.rs:27). */
@@ -131,6 +132,13 @@ int dcf_eval_prefix_levels(const dcf_prg* prg, size_t n_bytes, size_t num_keys, 
  *   ttable_waves:  waves per workgroup running the T-table engine (the rest
  *                  run the bitsliced engine; clamped to [1, 16] / [0, 12]). */
 int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves, int slab_variant);
+
+/* DCF_EVAL_STREAM_HYBRID tuning (results are identical for every setting):
+ *   ttable_wave_mask: bit w set = wave w of the 16-wave workgroup runs the stream
+ *                     T-table engine, clear = the bitsliced engine; waves w and
+ *                     w + 4 share a SIMD (at least 4 bits set);
+ *   priority:         1 = stream waves issue at raised priority (s_setprio). */
+int dcf_prg_set_stream_hybrid(dcf_prg* prg, unsigned ttable_wave_mask, int priority);
 
 /* CWB layout helpers (see above). */
 size_t dcf_cwb_bytes(size_t n_bytes, size_t lambda, size_t num_keys);

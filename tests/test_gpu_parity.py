@@ -143,18 +143,18 @@ def test_eval_random_vs_oracle(dcf, nb, mode):
 
 
 @pytest.mark.parametrize("nb,levels", [(1, 1), (1, 7), (2, 9), (2, 15), (3, 23), (4, 8), (4, 24), (5, 1),
-                                        (16, 13), (16, 24), (17, 20), (32, 24)])
+                                        (16, 13), (16, 24), (17, 20), (32, 24), (4, 26), (32, 30)])
 def test_eval_prefix_table_vs_oracle(dcf, nb, levels):
     """Shared-prefix eval (stream engine, forced depth): points start at level D from
     the key's expanded top tree; the output must not change.  Covers D = 1, D = 8N - 1
     (the walk's last level only), D across x's word boundary (N = 3: 24 bits) and
-    the 24-level cap (N = 16, 32)."""
+    the 28-level cap on a forced depth (N = 32, D = 30)."""
     rng = np.random.default_rng(700 + 31 * nb + levels)
     keys = [rng.bytes(32) for _ in range(2)]
     prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
     prg.set_eval_mode(4)
     prg.set_prefix_levels(levels)
-    want_d = min(levels, 24, 8 * nb - 1)
+    want_d = min(levels, 28, 8 * nb - 1)
     m = 3001
     assert prg.eval_prefix_levels(nb, 1, m) == want_d
     d = dcf.DcfImpl(nb, 16, prg)
@@ -337,6 +337,58 @@ def test_hybrid_splits_identical(dcf, split, variant):
     got = d.eval_device(False, cwb, s0, xs)
     torch.cuda.synchronize()
     assert torch.equal(ref, got)
+
+
+@pytest.mark.parametrize("nb,prefix,mask,prio", [(16, -1, 0x7777, 0), (16, -1, 0x3333, 1), (16, 0, 0xEEEE, 0),
+                                                   (16, 13, 0xFFF0, 1), (4, -1, 0x7777, 0), (4, 23, 0x5555, 0),
+                                                   (8, 1, 0x7777, 1), (12, 0, 0x0F0F, 0)])
+def test_stream_hybrid_vs_oracle(dcf, nb, prefix, mask, prio):
+    """Stream-hybrid engine (mode 5: stream T-table waves + bitsliced waves, both below
+    the shared prefix): bit-exact with the oracle on a sample and with the stream
+    engine on a batch large enough that both roles take units (300k points), for
+    several wave masks, depths (auto, forced, off) and N (4, 8, 12, 16)."""
+    import torch
+    rng = np.random.default_rng(0x5E + nb * 7 + mask)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    d = dcf.DcfImpl(nb, 16, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
+    bound = int(rng.integers(0, 2))
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
+    ok = O.gen(P, alpha, beta, s0, s1, bound)
+    m = 300_001
+    xs_h = _rand(rng, (m, nb))
+    a = np.frombuffer(alpha, np.uint8)
+    xs_h[0] = a
+    xs_h[1:200] = a
+    xs_h[1:200, -1] = rng.integers(0, 256, 199, dtype=np.uint8)
+    cwb = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, nb, 16), np.uint8).copy()).cuda()
+    xs = torch.from_numpy(xs_h).cuda()
+    prg.set_prefix_levels(prefix)
+    for b, s in ((0, s0), (1, s1)):
+        sd = torch.from_numpy(np.frombuffer(s, np.uint8).copy()).cuda()
+        prg.set_eval_mode(4)
+        ref = d.eval_device(bool(b), cwb, sd, xs)
+        prg.set_eval_mode(5)
+        prg.set_stream_hybrid(mask, prio)
+        got = d.eval_device(bool(b), cwb, sd, xs)
+        torch.cuda.synchronize()
+        assert torch.equal(ref, got), (nb, prefix, hex(mask), b)
+        idx = np.r_[0:3000, m - 3000:m]
+        want = O.eval_(P, b, ok, s, xs_h[idx], nthreads=8)
+        assert np.array_equal(got.cpu().numpy()[idx], want), (nb, prefix, hex(mask), b)
+
+
+def test_stream_hybrid_rejects(dcf):
+    prg = dcf.Aes256HirosePrg([bytes(32)] * 2, 16)
+    for mask in (0x0007, 0x10000):
+        with pytest.raises(dcf.DcfError):
+            prg.set_stream_hybrid(mask, 0)
+    prg.set_eval_mode(5)
+    d = dcf.DcfImpl(3, 16, prg)  # N % 4 != 0: not served by this engine
+    k = d.gen(dcf.CmpFn(bytes(3), bytes(16)), [bytes(16), bytes(16)], dcf.BoundState.LtBeta)
+    with pytest.raises(dcf.DcfError):
+        d.eval(False, k, np.zeros((10, 3), np.uint8))
 
 
 def test_error_codes_on_device(dcf):
