@@ -262,14 +262,17 @@ def run_eval(args, world, rank):
         return float(t.item()), ev0.elapsed_time(ev1) / 1e3 / steps / parties
 
     wall, kern_s = timed(args.steps)
+    dev_blocks = prg.last_eval_blocks()  # stream engine: AES blocks of the last launch, counted on the device
     no_prefix = None
     if pfx and not args.no_compare:
         # the same batch without the shared-prefix table (each point walks all 8N levels)
         prg.set_prefix_levels(0)
         w0, k0 = timed(args.steps)
+        np_blocks = prg.last_eval_blocks()
         prg.set_prefix_levels(args.prefix)
         no_prefix = {"value": m * world * args.steps * parties / w0, "kernel_ms": k0 * 1e3,
-                     "executed_blocks_per_eval": 16 * nb if args.prg == "mmo" else 8 * nb + zero_bits(xs) / m,
+                     "executed_blocks_per_eval": 16 * nb if args.prg == "mmo" else (
+                         np_blocks / m if np_blocks else 8 * nb + zero_bits(xs) / m),
                      "speedup": w0 / wall}
     total_evals = m * world * args.steps * parties
     value = total_evals / wall
@@ -287,7 +290,10 @@ def run_eval(args, world, rank):
     # table costs 2 blocks per node of the top tree (2^(D+1) - 2), spread over the batch.
     # MMO: 2 AES-128 blocks per level below the prefix (the table: 2 per node as well).
     if engine == "stream":
-        exec_bpe = (8 * nb - pfx) + zero_bits(xs, pfx) / m + (2 ** (pfx + 1) - 2) / m
+        # B every level + A on left levels, minus the B blocks reused after a right step at
+        # t = 0 (kernels_stream.h): counted by the kernel itself, plus the prefix table
+        walk = dev_blocks / m if dev_blocks else (8 * nb - pfx) + zero_bits(xs, pfx) / m
+        exec_bpe = walk + (2 ** (pfx + 1) - 2) / m
     elif engine == "mmo":
         exec_bpe = 2 * (8 * nb - pfx) + (2 ** (pfx + 1) - 2) / m
     else:
@@ -327,7 +333,7 @@ def run_eval(args, world, rank):
             "executed_blocks_per_eval": exec_bpe, "reference_blocks_per_eval": bpe,
             "prefix_levels": pfx, "no_prefix": no_prefix,
             "note": "achieved = AES blocks the kernel encrypts per second (stream engine: B every "
-                    "level + A on left levels; mmo: 2 AES-128 per level; both below a shared-prefix table "
+                    "level + A on left levels, minus B blocks reused after a right step at t = 0, counted on the device; mmo: 2 AES-128 per level; both below a shared-prefix table "
                     "of prefix_levels levels built inside the timed call and counted; other engines: the "
                     "reference count, 2 per level); "
                     "aes_blocks_per_s above uses the reference count.  Peak per GPU at 2.4 GHz: T-table "

@@ -88,6 +88,8 @@ struct DevBuf {
 
 }  // namespace
 
+constexpr size_t kCtrBytes = 16;  // d_ctr: work counter (u32), then the stream engine's block count (u64)
+
 struct dcf_prg {
   int kind = 0;               // 0: Aes256HirosePrg (prg.rs), 1: Aes128MatyasMeyerOseasPrg (kernels_mmo.h)
   int device = 0;
@@ -244,8 +246,8 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
     const uint64_t cnt = (m - off < chunk) ? m - off : chunk;
     const dim3 grid((unsigned)grid_for(cnt, p->cus));
     if (p->eval_mode != DCF_EVAL_TTABLE) {  // stream head: 2.5 AES blocks per level instead of 4
-      if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
-      HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+      if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
+      HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
       if (!p->d_rk2) {  // round keys of ciphers 0 and 17 (2 x 15 x 16 B), read into LDS by the kernel
         HIP_TRY(hipMalloc(&p->d_rk2, 2 * sizeof(RoundKeys)));
         HIP_TRY(hipMemcpy(p->d_rk2, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice));
@@ -451,6 +453,15 @@ int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves, int slab_variant) {
   return DCF_OK;
 }
 
+int dcf_prg_last_eval_blocks(dcf_prg* p, uint64_t* blocks) {
+  if (!p || !blocks) return fail(DCF_ERR_ARG, "null argument");
+  *blocks = 0;
+  if (!p->d_ctr) return DCF_OK;
+  DeviceGuard dg(p->device);
+  HIP_TRY(hipMemcpy(blocks, p->d_ctr + 2, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return DCF_OK;
+}
+
 int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priority) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");
   if (ttable_wave_mask > 0xFFFFu || __builtin_popcount(ttable_wave_mask) < 16 - kShybridXlSlots)
@@ -514,8 +525,8 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
   // Large batches: 64-key units from the work counter (waves drift apart, as in k_eval16).
   uint32_t* ctr = nullptr;
   if (num_keys >= (uint64_t)p->cus * kBlock * 2 && (num_keys + 63) / 64 <= 0xFFFFFFFFull) {
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), (hipStream_t)stream));
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, (hipStream_t)stream));
     ctr = p->d_ctr;
   }
   hipLaunchKernelGGL(k_gen16, dim3((unsigned)grid_for(num_keys, p->cus)), dim3(kBlock), 0, (hipStream_t)stream,
@@ -612,8 +623,8 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     int ntt = tt_single ? 16 : p->hybrid_tt_waves;
     if (mem && ntt < 1) ntt = 1;  // 15 LDS x-slots for bitsliced waves
     if (ntt > waves) ntt = waves;
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
     const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
     uint64_t blocks = (units + waves - 1) / waves;
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
@@ -641,14 +652,14 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     if (units > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "stream-hybrid eval: more than 2^32 work units");
     int rc = ensure_slabs(p, st);
     if (rc) return rc;
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
     PrefixTable pf{nullptr, 0u};
     const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
     if (d) {
       rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
       if (rc) return rc;
     }
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
     uint64_t blocks = (units + 15) / 16;
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
     hipLaunchKernelGGL(k_eval16_shybrid, dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
@@ -659,8 +670,8 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #ifndef DCF_STREAM_NS
 #define DCF_STREAM_NS 2  // streams per lane
 #endif
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
     const uint64_t units = (total + kStreamUnit - 1) / kStreamUnit;
     if (units > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "stream eval: more than 2^32 work units");
     uint64_t blocks = (units + 15) / 16;
@@ -725,8 +736,8 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
       hipLaunchKernelGGL(k_eval16_bs<false>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
                          (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
   } else {  // lockstep T-table, 64-point units from the work counter
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, sizeof(uint32_t)));
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, sizeof(uint32_t), st));
+    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
+    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
     if ((total + 63) / 64 > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "more than 2^32 64-point units");
 #define DCF_TT(MODE)                                                                                         \
   hipLaunchKernelGGL(k_eval16<MODE>, grid, block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,               \

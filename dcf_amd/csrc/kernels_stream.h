@@ -140,6 +140,20 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
   }
 }
 
+// The stream's next 32 x bits at level nl (a multiple of 32): from the queue (XREG) or x.
+template <int NS, bool XREG, bool MULTI>
+__device__ __forceinline__ void stream_next_word(StreamLane<NS, XREG, MULTI>& L, int i, uint32_t nl, uint32_t nlev,
+                                                 uint32_t nbytes) {
+  if (XREG) {
+    L.cur[i] = bswap32(L.xw[i][0]);
+    L.xw[i][0] = L.xw[i][1];
+    L.xw[i][1] = L.xw[i][2];
+    L.xw[i][2] = L.xw[i][3];
+  } else if (nl < nlev) {
+    L.cur[i] = load_bits32(L.xp[i], nl >> 5, nbytes);
+  }
+}
+
 // Key-major CW digest for the multi-key stream engine: one workgroup per 16 keys
 // stages their 8N levels through LDS so both the level-major reads (16 keys x 16 B
 // per row) and the key-major writes (4 KiB per key) are contiguous.
@@ -199,14 +213,21 @@ __device__ __forceinline__ void stream_run(
     stream_refill<NS, XREG, MULTI, UNIT>(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs,
                                          nbytes, ppk, pf);
 
+  uint64_t nblk = 0;  // AES blocks this wave encrypts for live streams (wave-uniform)
   for (;;) {
     bool any = false;
 #pragma unroll
-    for (int i = 0; i < NS; ++i) any = any || L.alive[i];
+    for (int i = 0; i < NS; ++i) {
+      any = any || L.alive[i];
+      nblk += (uint64_t)__popcll(__ballot(L.alive[i]));
+    }
     if (!__ballot(any)) break;
-    // Correction words of each stream's current level (vector loads, issued before the AES).
-    uint4 cs[NS], cv[NS];
-    uint32_t ct[NS];
+    // Correction words of each stream's current level (vector loads, issued before the AES),
+    // and of the next level for a stream whose step may end with B still valid (a right
+    // step at t = 0 keeps s: see "B reuse" below).
+    uint4 cs[NS], cv[NS], cs2[NS], cv2[NS];
+    uint32_t ct[NS], ct2[NS];
+    bool maybe[NS];  // the next level's CWs were loaded
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       if (MULTI) {  // cw_s = digest (2 uint4 per level), cw_t = digest t bytes
@@ -217,6 +238,25 @@ __device__ __forceinline__ void stream_run(
         cv[i] = cw_v[L.ci[i]];
       }
       ct[i] = cw_t[L.ci[i]];
+      // XREG: a fresh stream's x word is still in the queue; its first step is a B step
+      // at the root, whose seed may be unmasked, so no reuse follows it anyway.
+#ifndef DCF_NO_B_REUSE
+      maybe[i] = L.alive[i] && L.ph[i] == 0u && L.t[i] == 0u && (!XREG || !L.fresh[i]) &&
+                 (L.cur[i] >> 31) != 0u && L.lev[i] + 1u < nlev;
+#else
+      maybe[i] = false;
+#endif
+      // Loaded unconditionally (L1-resident): loads under a divergent branch made the
+      // compiler wait for them before the AES.
+      const uint64_t c2 = L.ci[i] + (L.lev[i] + 1u < nlev ? 1u : 0u);
+      if (MULTI) {
+        cs2[i] = cw_s[2 * c2];
+        cv2[i] = cw_s[2 * c2 + 1];
+      } else {
+        cs2[i] = cw_s[c2];
+        cv2[i] = cw_v[c2];
+      }
+      ct2[i] = cw_t[c2];
     }
     // Slot i encrypts ~s (B) in phase 0 and s (A) in phase 1.
     uint32_t st[NS][4];
@@ -237,6 +277,10 @@ __device__ __forceinline__ void stream_run(
       asm volatile("" : "+v"(cs[i].x), "+v"(cs[i].y), "+v"(cs[i].z), "+v"(cs[i].w), "+v"(cv[i].x), "+v"(cv[i].y),
                    "+v"(cv[i].z), "+v"(cv[i].w), "+v"(ct[i]));
 #pragma unroll
+    for (int i = 0; i < NS; ++i)
+      asm volatile("" : "+v"(cs2[i].x), "+v"(cs2[i].y), "+v"(cs2[i].z), "+v"(cs2[i].w), "+v"(cv2[i].x),
+                   "+v"(cv2[i].y), "+v"(cv2[i].z), "+v"(cv2[i].w), "+v"(ct2[i]));
+#pragma unroll
     for (int i = 0; i < NS; ++i) {
       if (XREG) {  // next 32 x bits from the word queue (raw loads, byte-swapped here)
         const bool nw = L.fresh[i];
@@ -244,6 +288,7 @@ __device__ __forceinline__ void stream_run(
         L.xw[i][0] = nw ? L.xw[i][1] : L.xw[i][0];
         L.xw[i][1] = nw ? L.xw[i][2] : L.xw[i][1];
         L.xw[i][2] = nw ? L.xw[i][3] : L.xw[i][2];
+        L.fresh[i] = false;
       }
       const uint32_t p = L.ph[i], xb = L.cur[i] >> 31;  // Msb0 bit of x (lib.rs:181)
       const uint32_t adv = L.alive[i] ? (p | xb) : 0u;   // this step finishes the level
@@ -252,7 +297,14 @@ __device__ __forceinline__ void stream_run(
       const uint32_t tm = 0u - L.t[i], am = 0u - adv, pm = 0u - p;
       const uint32_t csw[4] = {cs[i].x, cs[i].y, cs[i].z, cs[i].w};
       const uint32_t cvw[4] = {cv[i].x, cv[i].y, cv[i].z, cv[i].w};
-      const uint32_t d0 = st[i][0] ^ L.s[i][0] ^ inv;  // (A^s) or (B^~s), word 0
+      uint32_t d[4];  // (A^s) or (B^~s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = st[i][j] ^ L.s[i][j] ^ inv;
+      const uint32_t d0 = d[0];
+      // B reuse: a right step at t = 0 leaves s = s & M, which is s itself when s is
+      // already masked (every seed below the root: side & M ^ t*cw.s, cw.s masked), so
+      // the next level's PRG(s) is this one's and its B is d ^ ~s, already in hand.
+      const bool reuse = maybe[i] && (L.s[i][3] & ~kMaskLast) == 0u;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
@@ -269,15 +321,32 @@ __device__ __forceinline__ void stream_run(
       const uint32_t tb = (d0 ^ (L.t[i] & (ct[i] >> xb))) & 1u;
       L.t[i] = (am & tb) | (~am & L.t[i]);
       L.ph[i] = adv ^ 1u;
-      const uint32_t nl = L.lev[i] + adv;
-      const bool bnd = adv && (nl & 31u) == 0u;  // this stream's next 32 x bits start here
+      uint32_t nl = L.lev[i] + adv;
       L.cur[i] <<= adv;
-      if (XREG)
-        L.fresh[i] = bnd;
-      else if (bnd && nl < nlev)
-        L.cur[i] = load_bits32(L.xp[i], nl >> 5, nbytes);
-      L.lev[i] = nl;
+      if (adv && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
       L.ci[i] += adv;
+      if (reuse) {  // level nl with B known: its B half now, without an AES slot
+        const uint32_t xb2 = L.cur[i] >> 31, t1 = L.t[i], tm1 = 0u - t1;
+        const uint32_t cs2w[4] = {cs2[i].x, cs2[i].y, cs2[i].z, cs2[i].w};
+        const uint32_t cv2w[4] = {cv2[i].x, cv2[i].y, cv2[i].z, cv2[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+          // v ^= v_hat(side) ^ t*cw.v: right ~s & M, left (B^~s) & M   (lib.rs:182/186)
+          L.v[i][j] ^= ((xb2 ? ~L.s[i][j] : d[j]) & msk) ^ (tm1 & cv2w[j]);
+          if (xb2) L.s[i][j] ^= tm1 & cs2w[j];  // right: s' = s & M ^ t*cw.s   (lib.rs:178)
+        }
+        if (xb2) {  // a right step ends the level: t' = lsb(B^~s) ^ t & cw.tr   (lib.rs:180)
+          L.t[i] = (d0 ^ (t1 & (ct2[i] >> 1))) & 1u;
+          ++nl;
+          L.cur[i] <<= 1;
+          if ((nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+          L.ci[i] += 1u;
+        } else {
+          L.ph[i] = 1u;  // left: A next
+        }
+      }
+      L.lev[i] = nl;
     }
     // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.
 #pragma unroll
@@ -294,6 +363,8 @@ __device__ __forceinline__ void stream_run(
                                              party, xs, nbytes, ppk, pf);
     }
   }
+  // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
+  if ((threadIdx.x & 63u) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, (unsigned long long)nblk);
 }
 
 // TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.

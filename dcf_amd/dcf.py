@@ -180,6 +180,13 @@ class Aes256HirosePrg:
         priority 1 raises the stream waves' issue priority.  Output bytes are identical."""
         check(_lib.load().dcf_prg_set_stream_hybrid(self._h, int(ttable_wave_mask), int(priority)))
 
+    def last_eval_blocks(self) -> int:
+        """AES blocks the last stream-engine eval encrypted for live points, counted on the
+        device (no prefix table build).  Call after synchronizing the eval's stream."""
+        n = ctypes.c_uint64(0)
+        check(_lib.load().dcf_prg_last_eval_blocks(self._h, ctypes.byref(n)))
+        return int(n.value)
+
     def gen(self, seed: bytes):
         """`Prg::gen` (lib.rs:52-54) for one seed — the GPU PRG kernel, not a CPU path."""
         return self.gen_many([seed])[0]

@@ -140,6 +140,12 @@ int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves, int slab_variant);
  *   priority:         1 = stream waves issue at raised priority (s_setprio). */
 int dcf_prg_set_stream_hybrid(dcf_prg* prg, unsigned ttable_wave_mask, int priority);
 
+/* AES blocks the last LAMBDA = 16 stream-engine eval on this prg encrypted for live
+ * points (DCF_EVAL_STREAM / _STREAM_HYBRID's stream waves; not counting a shared-prefix
+ * table build), counted on the device.  Measurement hook for the bench; call after
+ * the eval's stream has been synchronized.  0 before any such eval. */
+int dcf_prg_last_eval_blocks(dcf_prg* prg, uint64_t* blocks);
+
 /* CWB layout helpers (see above). */
 size_t dcf_cwb_bytes(size_t n_bytes, size_t lambda, size_t num_keys);
 size_t dcf_cwb_np1_offset(size_t n_bytes, size_t lambda, size_t num_keys);

@@ -339,6 +339,45 @@ def test_hybrid_splits_identical(dcf, split, variant):
     assert torch.equal(ref, got)
 
 
+@pytest.mark.parametrize("nb", [1, 4, 5, 8, 16, 17, 32])
+@pytest.mark.parametrize("prefix", [0, -1])
+def test_stream_b_reuse_vs_oracle(dcf, nb, prefix):
+    """Stream engine's B reuse (a right step at t = 0 keeps the seed, so the next level's
+    B is known): runs of right steps (x bytes 0xFF, 0xFE, 0x7F), both parties (t starts
+    at 0 and 1), a root seed with the masked bit set and clear, 32-level word boundaries
+    (N = 5, 17, 32); bit-exact with the oracle.  The kernel's own block count must sit
+    below the no-reuse count 8N + zeros(x) and above 8N - (levels it could skip)."""
+    rng = np.random.default_rng(0xB0 + nb)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    prg.set_eval_mode(4)
+    prg.set_prefix_levels(prefix)
+    d = dcf.DcfImpl(nb, 16, prg)
+    m = 600_000 if prefix else 20_000
+    for bound, masked in ((0, True), (1, False)):
+        alpha, beta = rng.bytes(nb), rng.bytes(16)
+        s0, s1 = bytearray(rng.bytes(16)), bytearray(rng.bytes(16))
+        for sd in (s0, s1):
+            sd[15] = (sd[15] & 0xFE) | (0 if masked else 1)
+        s0, s1 = bytes(s0), bytes(s1)
+        ok = O.gen(P, alpha, beta, s0, s1, bound)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
+        xs = _rand(rng, (m, nb))
+        xs[:1000] = 0xFF
+        xs[1000:2000] = rng.choice(np.array([0xFF, 0xFE, 0x7F, 0xEF], np.uint8), size=(1000, nb))
+        xs[2000] = np.frombuffer(alpha, np.uint8)
+        for b, sd in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([sd], k.cws, k.cw_np1), xs)
+            blocks = prg.last_eval_blocks()
+            idx = np.r_[0:4000, m - 2000:m]
+            want = O.eval_(P, b, ok, sd, xs[idx], nthreads=8)
+            assert np.array_equal(got[idx], want), (nb, prefix, bound, b)
+            if prefix == 0:
+                zeros = int(np.unpackbits(xs).size - np.unpackbits(xs).sum())
+                assert blocks < 8 * nb * m + zeros, (blocks, 8 * nb * m + zeros)
+                assert blocks > 0.5 * (8 * nb * m + zeros)
+
+
 @pytest.mark.parametrize("nb,prefix,mask,prio", [(16, -1, 0x7777, 0), (16, -1, 0x3333, 1), (16, 0, 0xEEEE, 0),
                                                    (16, 13, 0xFFF0, 1), (4, -1, 0x7777, 0), (4, 23, 0x5555, 0),
                                                    (8, 1, 0x7777, 1), (12, 0, 0x0F0F, 0)])
