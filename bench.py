@@ -303,7 +303,8 @@ def run_eval(args, world, rank):
         # tail writes LAMBDA - 32 output bytes per eval: time bound = AES (LDS) + output (HBM write).
         engine = "stream-head" if args.eval_mode != 1 else "ttable"
         if engine == "stream-head":
-            exec_bpe = 3 * 8 * nb - zero_bits(xs) / m
+            # below a shared prefix of pfx levels (k_wpfx_level: 4 blocks per parent node)
+            exec_bpe = 3 * (8 * nb - pfx) - zero_bits(xs, pfx) / m + 4 * (2 ** pfx - 1) / m
     per_gpu_blocks = m * exec_bpe / kern_s
     # HBM bytes per launch of the dominant kernel: x in, y out, and with a shared prefix
     # one 32-byte table row gathered per point (kernels16.h PrefixTable)
@@ -342,6 +343,8 @@ def run_eval(args, world, rank):
                     "the VALU left over (DESIGN.md section 4)",
         },
     }
+    if lam > 16:
+        out["roofline"]["prefix_levels"] = pfx  # wide stream head below a shared-prefix table
     if rank == 0 and world == 1 and not args.no_cpu:
         ns = min(m, 1 << 26, max(4096, (1 << 30) // lam))  # at most ~1 GiB of outputs copied back
         xs_h = xs[:ns].cpu().numpy()

@@ -161,6 +161,60 @@ uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint6
   return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
 }
 
+// Shared-prefix depth for the LAMBDA >= 32 stream head over m points of one key
+// (kernels_wide_stream.h WidePrefix): 80 B per node, 4 AES blocks per parent.
+// Auto: log2(m) - 1, at most 22 (two 336 MB node buffers at 2^22), none below 8.
+constexpr uint32_t kWidePrefixMax = 22;
+uint32_t wide_prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t m) {
+  if (p->lambda <= 16 || p->prefix_levels == 0 || p->eval_mode == DCF_EVAL_TTABLE || m == 0) return 0;
+  uint32_t d;
+  if (p->prefix_levels > 0) {
+    d = std::min((uint32_t)p->prefix_levels, 30u);
+  } else {
+    const uint32_t lg = 63u - (uint32_t)__builtin_clzll(m | 1u);
+    d = lg > 1u ? lg - 1u : 0u;
+    if (d < 8u) return 0;
+    d = std::min(d, kWidePrefixMax);
+  }
+  return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
+}
+
+// Expand the top `levels` levels of one key's tree for the wide stream head (the CW
+// digest p->d_dig must hold this key) into WidePrefix rows in p->d_pfx.
+int build_wide_prefix(dcf_prg* p, uint32_t nlev, int party, const uint8_t* s0, uint32_t levels, WidePrefix* out,
+                      hipStream_t st) {
+  const size_t half = (((size_t)80 << levels) + 255) & ~(size_t)255;
+  const size_t need = 2 * half;
+  if (p->pfx_bytes < need) {
+    if (p->d_pfx) {
+      HIP_TRY(hipStreamSynchronize(st));
+      HIP_TRY(hipFree(p->d_pfx));
+      p->d_pfx = nullptr;
+      p->pfx_bytes = 0;
+    }
+    HIP_TRY(hipMalloc(&p->d_pfx, need));
+    p->pfx_bytes = need;
+  }
+  uint4* a = (uint4*)p->d_pfx;
+  uint4* b = (uint4*)(p->d_pfx + half);
+  hipLaunchKernelGGL(k_wpfx_root, dim3(1), dim3(64), 0, st, s0, (uint32_t)party, a);
+  HIP_TRY(hipGetLastError());
+  for (uint32_t lev = 0; lev < levels; ++lev) {
+    const uint64_t parents = 1ull << lev;
+    const dim3 grid((unsigned)grid_for(parents, p->cus));
+    if (p->lambda == 32)
+      hipLaunchKernelGGL(k_wpfx_level<true>, grid, dim3(kBlock), 0, st, p->d_tab, p->d_rk2, (const uint4*)p->d_dig,
+                         p->d_dig + (size_t)nlev * 64, lev, parents, a, b);
+    else
+      hipLaunchKernelGGL(k_wpfx_level<false>, grid, dim3(kBlock), 0, st, p->d_tab, p->d_rk2, (const uint4*)p->d_dig,
+                         p->d_dig + (size_t)nlev * 64, lev, parents, a, b);
+    HIP_TRY(hipGetLastError());
+    std::swap(a, b);
+  }
+  *out = WidePrefix{a, levels};
+  return DCF_OK;
+}
+
 // Expand the top `levels` levels of the key's tree (s = s0, v = 0, t = party at the
 // root; k_fd_level16 per level, as the full-domain eval does) into p->d_pfx.
 int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const uint4* cwv, const uint8_t* cwt,
@@ -242,6 +296,7 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
   if (rc) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(p->d_ws);
   const uint32_t nch = (nlev + 1 + 3) / 4;
+  WidePrefix wpf{nullptr, 0u};
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = (m - off < chunk) ? m - off : chunk;
     const dim3 grid((unsigned)grid_for(cnt, p->cus));
@@ -265,6 +320,11 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
         hipLaunchKernelGGL(k_cw_digest, dim3((4 * nlev + 255) / 256), dim3(256), 0, st, cws, cwv, cwt, nlev, lam, K,
                            key, (uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64);
         HIP_TRY(hipGetLastError());
+        const uint32_t d = wide_prefix_depth(p, n_bytes, m);
+        if (d) {
+          rc = build_wide_prefix(p, nlev, party, s0, d, &wpf, st);
+          if (rc) return rc;
+        }
       }
       const uint64_t units = (cnt + kStreamUnit - 1) / kStreamUnit;
       uint64_t blocks = (units + 15) / 16;
@@ -275,7 +335,7 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
 #define DCF_WHS(MH, XR)                                                                                        \
   hipLaunchKernelGGL((k_eval_wide_head_stream<DCF_WHS_NS, MH, XR>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab,     \
                      p->d_rk2, (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
-                     lam, K, key, cnt, p->d_ctr, ys + off * lam, tvec)
+                     lam, K, key, cnt, p->d_ctr, ys + off * lam, tvec, wpf)
       const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16;
       if (lam == 32 && xreg) DCF_WHS(true, true);
       else if (lam == 32) DCF_WHS(true, false);
@@ -438,6 +498,7 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   // auto mode), Hirose engines other than the stream engine (MMO ignores the engine setting)
   const bool small = total < (uint64_t)p->cus * kBlock * 2;
   if (p->kind == 1) return small && p->prefix_levels < 0 ? 0 : (int)prefix_depth(p, n_bytes, num_keys, total);
+  if (p->lambda > 16) return n_bytes > 31 ? 0 : (int)wide_prefix_depth(p, n_bytes, points_per_key);
   if (p->eval_mode == DCF_EVAL_AUTO && small) return 0;
   if (p->eval_mode != DCF_EVAL_AUTO && p->eval_mode != DCF_EVAL_STREAM && p->eval_mode != DCF_EVAL_STREAM_HYBRID)
     return 0;

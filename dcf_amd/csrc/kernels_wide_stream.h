@@ -19,6 +19,14 @@
 
 namespace {
 
+// Shared prefix for the stream head (as kernels16.h PrefixTable at LAMBDA = 16): the
+// key's top `levels` tree levels expanded once, one 80-byte node per prefix:
+// rows[5 i .. 5 i + 5) = s[0:32) | v[0:32) | {t, t-vector word 0, partial t-vector word, 0}.
+struct WidePrefix {
+  const uint4* rows;
+  uint32_t levels;  // < 31 and < 8N; 0 = none
+};
+
 template <int NS>
 struct WideLane {
   uint32_t s[NS][8], v[NS][8];           // bytes [0,32) of the seed and of the v accumulator
@@ -30,7 +38,8 @@ struct WideLane {
 
 template <int NS, bool XREG>
 __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, const uint8_t* __restrict__ s0p,
-                                           uint32_t party, const uint8_t* __restrict__ xs, uint32_t nbytes) {
+                                           uint32_t party, const uint8_t* __restrict__ xs, uint32_t nbytes,
+                                           const WidePrefix& pf, uint32_t* __restrict__ tvec) {
   const uint4* s4 = reinterpret_cast<const uint4*>(s0p);  // k.s0s[0] (lib.rs:168), L2-resident
   const uint4 a = s4[0], b = s4[1];
   L.s[i][0] = a.x; L.s[i][1] = a.y; L.s[i][2] = a.z; L.s[i][3] = a.w;
@@ -62,13 +71,28 @@ __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, c
   } else {
     L.cur[i] = load_bits32(row, 0, nbytes);
   }
+  if (pf.levels) {  // start at level D from the node named by x's first D bits (Msb0)
+    const uint32_t D = pf.levels;
+    const uint4* nd = pf.rows + 5u * (L.cur[i] >> (32u - D));
+    const uint4 a0 = nd[0], a1 = nd[1], b0 = nd[2], b1 = nd[3], e = nd[4];
+    L.s[i][0] = a0.x; L.s[i][1] = a0.y; L.s[i][2] = a0.z; L.s[i][3] = a0.w;
+    L.s[i][4] = a1.x; L.s[i][5] = a1.y; L.s[i][6] = a1.z; L.s[i][7] = a1.w;
+    L.v[i][0] = b0.x; L.v[i][1] = b0.y; L.v[i][2] = b0.z; L.v[i][3] = b0.w;
+    L.v[i][4] = b1.x; L.v[i][5] = b1.y; L.v[i][6] = b1.z; L.v[i][7] = b1.w;
+    L.t[i] = e.x;
+    L.tacc[i] = e.z;  // rows 16 (D >> 4) .. D of the t-vector
+    if (D >= 15u) tvec[(uint64_t)p * kTWords] = e.y;  // rows 0..15, complete (row 15 = t_15 of depth 15)
+    L.lev[i] = D;
+    L.cur[i] <<= D;
+  }
 }
 
 template <int NS, bool XREG>
 __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, uint64_t& unext, uint64_t& uend,
                                             bool& exhausted, uint32_t* __restrict__ ctr, uint64_t nunits,
                                             uint64_t count, const uint8_t* __restrict__ s0p, uint32_t party,
-                                            const uint8_t* __restrict__ xs, uint32_t nbytes) {
+                                            const uint8_t* __restrict__ xs, uint32_t nbytes, const WidePrefix& pf,
+                                            uint32_t* __restrict__ tvec) {
   uint64_t need = __ballot(mine);
   while (need) {
     if (unext >= uend && !exhausted) {
@@ -89,7 +113,7 @@ __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, u
     }
     const uint32_t rank = lane_rank(need);
     const bool take = mine && (uint64_t)rank < uend - unext;
-    if (take) wide_start<NS, XREG>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes);
+    if (take) wide_start<NS, XREG>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes, pf, tvec);
     const uint64_t taken = __ballot(take);
     unext += (uint64_t)__popcll(taken);
     need &= ~taken;
@@ -119,7 +143,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
     const uint8_t* __restrict__ dig_t, const uint8_t* __restrict__ cw_np1,
     const uint8_t* __restrict__ s0p, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint32_t lam, const uint64_t num_keys, const uint64_t key, const uint64_t count, uint32_t* __restrict__ ctr,
-    uint8_t* __restrict__ ys, uint32_t* __restrict__ tvec) {
+    uint8_t* __restrict__ ys, uint32_t* __restrict__ tvec, const WidePrefix pf) {
   __shared__ uint32_t lds[kLdsWords];
   // Schedules of cipher 0 (slots 0..14) and cipher 17 (slots 23..37): 23 slots apart,
   // so lanes reading the two never share a ds_read_b128 bank group.
@@ -141,7 +165,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
   }
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    wide_refill<NS, XREG>(L, i, true, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes);
+    wide_refill<NS, XREG>(L, i, true, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes, pf,
+                          tvec);
 
   for (;;) {
     bool any = false;
@@ -264,7 +289,102 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
       if (__ballot(done))
-        wide_refill<NS, XREG>(L, i, done, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes);
+        wide_refill<NS, XREG>(L, i, done, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes, pf,
+                              tvec);
+    }
+  }
+}
+
+// Root of the wide prefix tree: s = k.s0s[0][0:32), v = 0, t = party (lib.rs:167-169);
+// t-vector row 0 = t_0 = party.
+__global__ void k_wpfx_root(const uint8_t* __restrict__ s0p, const uint32_t party, uint4* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s0p);
+    out[0] = s4[0];
+    out[1] = s4[1];
+    out[2] = out[3] = make_uint4(0u, 0u, 0u, 0u);
+    out[4] = make_uint4(party, 0u, party, 0u);
+  }
+}
+
+// One level of the wide prefix tree: each parent node at depth `lev` -> its two
+// children (out[2 i] left, out[2 i + 1] right), bytes [0,32) of the walk exactly as
+// k_eval_wide_head_stream updates them: A = E0(s_lo), B = E0(~s_lo) (left),
+// C = E17(s_hi), D = E17(~s_hi) (right), one lane per parent, all four blocks.
+template <bool MASK_HEAD>
+__global__ __launch_bounds__(kBlock, 1) void k_wpfx_level(
+    const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
+    const uint8_t* __restrict__ dig_t, const uint32_t lev, const uint64_t parents, const uint4* __restrict__ in,
+    uint4* __restrict__ out) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint4 rks[23 + 15];
+  if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint32_t mlast = MASK_HEAD ? kMaskLast : 0xFFFFFFFFu;
+  const uint4* d4 = dig + 4u * lev;
+  const uint4 cs0 = d4[0], cs1 = d4[1], cv0 = d4[2], cv1 = d4[3];
+  const uint32_t ct = dig_t[lev];
+  const uint32_t csw[8] = {cs0.x, cs0.y, cs0.z, cs0.w, cs1.x, cs1.y, cs1.z, cs1.w};
+  const uint32_t cvw[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
+  const uint32_t r = lev + 1u, pos = 8u * ((r >> 2) & 3u) + (r & 3u);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g - threadIdx.x % 64u < parents; g += stride) {
+    const uint64_t nd = g < parents ? g : parents - 1;  // whole waves stay in the loop (uniform AES)
+    const uint4* pn = in + 5u * nd;
+    const uint4 a0 = pn[0], a1 = pn[1], b0 = pn[2], b1 = pn[3], e = pn[4];
+    const uint32_t sw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const uint32_t vw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    uint32_t ab[2][4], cd[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ab[0][j] = sw[j];           // A
+      ab[1][j] = ~sw[j];          // B
+      cd[0][j] = sw[4 + j];       // C
+      cd[1][j] = ~sw[4 + j];      // D
+    }
+    const uint4* rk0[2] = {rks, rks};
+    const uint4* rk17[2] = {rks + 23, rks + 23};
+    aes_tt_lk<14, 2, true>(ab, rk0, lds, lc);
+    aes_tt_lk<14, 2, true>(cd, rk17, lds, lc);
+    const uint32_t t = e.x, tm = 0u - t;
+    uint32_t sl[8], vl[8], sr[8], vr[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t dA = ab[0][j] ^ sw[j], dB = ab[1][j] ^ ~sw[j];
+      const uint32_t dC = cd[0][j] ^ sw[4 + j], dD = cd[1][j] ^ ~sw[4 + j];
+      const uint32_t msk = (j == 3) ? mlast : 0xFFFFFFFFu;
+      // left: s = (A^s_lo, s_hi & M), v ^= (B^~s_lo, ~s_hi & M)   (prg.rs:57-68 with the diagonal zip)
+      sl[j] = dA ^ (tm & csw[j]);
+      sl[4 + j] = (sw[4 + j] & msk) ^ (tm & csw[4 + j]);
+      vl[j] = vw[j] ^ dB ^ (tm & cvw[j]);
+      vl[4 + j] = vw[4 + j] ^ (~sw[4 + j] & msk) ^ (tm & cvw[4 + j]);
+      // right: s = (s_lo, (C^s_hi) & M), v ^= (~s_lo, (D^~s_hi) & M)
+      sr[j] = sw[j] ^ (tm & csw[j]);
+      sr[4 + j] = (dC & msk) ^ (tm & csw[4 + j]);
+      vr[j] = vw[j] ^ ~sw[j] ^ (tm & cvw[j]);
+      vr[4 + j] = vw[4 + j] ^ (dD & msk) ^ (tm & cvw[4 + j]);
+    }
+    // t_L = lsb(A^s)[0], t_R = lsb(B^~s)[0], each ^ t & its cw.t   (lib.rs:179-180)
+    const uint32_t tl = ((ab[0][0] ^ sw[0]) ^ (t & ct)) & 1u;
+    const uint32_t trr = ((ab[1][0] ^ ~sw[0]) ^ (t & (ct >> 1))) & 1u;
+    uint32_t accl = e.z | (tl << pos), accr = e.z | (trr << pos), w0l = e.y, w0r = e.y;
+    if ((r & 15u) == 15u) {  // word r >> 4 of the t-vector is complete (r < 31: word 0)
+      w0l = accl; w0r = accr;
+      accl = accr = 0u;
+    }
+    if (g < parents) {
+      uint4* o = out + 10u * g;
+      o[0] = make_uint4(sl[0], sl[1], sl[2], sl[3]);
+      o[1] = make_uint4(sl[4], sl[5], sl[6], sl[7]);
+      o[2] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+      o[3] = make_uint4(vl[4], vl[5], vl[6], vl[7]);
+      o[4] = make_uint4(tl, w0l, accl, 0u);
+      o[5] = make_uint4(sr[0], sr[1], sr[2], sr[3]);
+      o[6] = make_uint4(sr[4], sr[5], sr[6], sr[7]);
+      o[7] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
+      o[8] = make_uint4(vr[4], vr[5], vr[6], vr[7]);
+      o[9] = make_uint4(trr, w0r, accr, 0u);
     }
   }
 }

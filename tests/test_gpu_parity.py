@@ -295,6 +295,39 @@ def test_wide_eval_random_vs_oracle(dcf, lam, nb, m, mode):
             assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, b, bound)
 
 
+@pytest.mark.parametrize("lam,nb,depth,m", [(32, 2, 1, 300), (32, 4, 16, 3000), (64, 16, 8, 2000), (48, 3, 23, 700),
+                                            (272, 5, 17, 2500), (16384, 16, 15, 120), (16384, 16, 21, 64), (64, 4, 15, 900),
+                                            (128, 2, 30, 500), (64, 16, -1, 1100)])
+def test_wide_prefix_vs_oracle(dcf, lam, nb, depth, m):
+    """LAMBDA >= 32 stream head below a shared-prefix table (k_wpfx_level: bytes [0,32)
+    of the walk for the top D levels, with t-vector rows 0..D): bit-exact with the oracle
+    for D = 1, 8 (partial t-vector word), 15 (word 0 completed by the table's last
+    level), 16 and 17 (word 0 complete, word 1 partial at start), 21,
+    23, D capped at 8N - 1 (N = 2, D = 30), auto (-1: 2^10 points -> 9), lambda = 32
+    (the cleared bit inside the head's bytes), both parties and bounds."""
+    rng = np.random.default_rng(lam + 31 * nb + depth)
+    keys = [rng.bytes(32) for _ in range(18)]
+    prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    prg.set_prefix_levels(depth)
+    want_d = min(8 * nb - 1, 30, depth) if depth > 0 else min(8 * nb - 1, 22, int(np.log2(m)) - 1)
+    assert prg.eval_prefix_levels(nb, 1, m) == want_d
+    d = dcf.DcfImpl(nb, lam, prg)
+    for bound in (0, 1):
+        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+        ok = O.gen(P, alpha, beta, s0, s1, bound)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
+        xs = _rand(rng, (m, nb))
+        a = np.frombuffer(alpha, np.uint8)
+        xs[0] = a
+        xs[1:20] = a
+        xs[1:20, -1] = rng.integers(0, 256, 19, dtype=np.uint8)
+        for b, s in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+            assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, depth, b, bound)
+    prg.set_eval_mode(1)  # the lockstep head takes no table
+    assert prg.eval_prefix_levels(nb, 1, m) == 0
+
+
 def test_wide_gen_batch_and_multikey(dcf):
     import torch
     lam, nb, K, Pp = 64, 2, 5, 7
