@@ -112,15 +112,17 @@ size_t dcf_prg_lambda(const dcf_prg* prg);
 int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 
 /* Shared prefix for single-key eval at LAMBDA = 16 (Hirose PRG: stream engine;
- * Aes128MatyasMeyerOseasPrg: every engine setting).
+ * Aes128MatyasMeyerOseasPrg: every engine setting) and, per key, for the LAMBDA >= 32
+ * stream head (bytes [0,32) of the walk and the t-vector rows, 80 B per node).
  * Every point's walk (lib.rs:174-189) passes through the node of the key's GGM
  * tree named by its first D bits, and that node's (s, v, t) depends on nothing
  * else, so eval expands the top D levels once (2^(D+1) AES blocks, 33 B per node,
  * as the full-domain eval does) and starts each point at level D from its node:
  * D fewer levels per point, identical output bytes.
- *   levels = -1: automatic (the default): D = log2(points) - 1, at most 24, none
- *                below 8 or for small batches;
- *   levels =  0: off;  levels > 0: that depth (capped at 24 and at 8N - 1).
+ *   levels = -1: automatic (the default): D = log2(points) - 1, at most 24 (LAMBDA
+ *                >= 32: 22), none below 8 or (LAMBDA = 16) for small batches;
+ *   levels =  0: off;  levels > 0: that depth (capped at 28 (LAMBDA >= 32: 30) and
+ *                at 8N - 1).
  * The table lives on the prg (its size follows the largest D used). */
 int dcf_prg_set_prefix_levels(dcf_prg* prg, int levels);
 /* The prefix depth D a dcf_eval* call of this shape would use (0 = none). */
