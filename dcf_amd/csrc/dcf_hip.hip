@@ -655,14 +655,25 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   // spread over every CU with workgroups just big enough (C1, 100k points: 3.2 -> see
   // DESIGN.md).
   if (mode == DCF_EVAL_AUTO && total < (uint64_t)p->cus * kBlock * 2) {
-    uint64_t threads = (total + p->cus - 1) / p->cus;
+#ifndef DCF_SMALL_PAIR
+#define DCF_SMALL_PAIR 1
+#endif
+    const uint64_t lanes_per_point = DCF_SMALL_PAIR ? 2 : 1;
+    uint64_t threads = (total * lanes_per_point + p->cus - 1) / p->cus;
     threads = ((threads + 63) / 64) * 64;
     if (threads > (uint64_t)kBlock) threads = kBlock;
-    const dim3 g2((unsigned)((total + threads - 1) / threads)), b2((unsigned)threads);
+    const dim3 g2((unsigned)((total * lanes_per_point + threads - 1) / threads)), b2((unsigned)threads);
+#if DCF_SMALL_PAIR
+#define DCF_SMALL(MODE)                                                                                           \
+  hipLaunchKernelGGL(k_eval16_pair<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,                  \
+                     (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk,  \
+                     (uint4*)ys)
+#else
 #define DCF_SMALL(MODE)                                                                                           \
   hipLaunchKernelGGL(k_eval16<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s,    \
                      (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk, (uint4*)ys,          \
                      (uint32_t*)nullptr)
+#endif
     if (num_keys == 1) DCF_SMALL(0);
     else if (ppk % 64 == 0) DCF_SMALL(1);
     else DCF_SMALL(2);

@@ -120,6 +120,92 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16(
   }
 }
 
+// Small batches, two lanes per point: lane 2k encrypts A = AES(s), lane 2k + 1
+// B = AES(~s), they swap the result (DPP quad_perm 1,0,3,2) and both run the level
+// update (lib.rs:174-189).  Twice the waves of k_eval16 for the same points, each
+// with half the AES work per level: a small batch has too few waves per SIMD to
+// overlap the LDS lookups with the rest (C1: 7 waves per CU with one lane per point).
+constexpr int kQpSwap1 = 1 | (0 << 2) | (3 << 4) | (2 << 6);
+
+__device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, const RoundKeys& rk,
+                                              const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
+                                              const uint8_t* __restrict__ cw_t, const uint4 np, const uint4 sv,
+                                              uint32_t party, const uint8_t* __restrict__ x, uint32_t nbytes,
+                                              uint64_t num_keys, uint64_t key, uint32_t odd) {
+  const uint32_t nlev = 8u * nbytes;
+  const uint32_t nchunk = (nbytes + 3u) >> 2;
+  const uint32_t inv = 0u - odd;  // odd lane: ~s (B)
+  uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w};
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  uint32_t t = party;
+  uint32_t lev = 0;
+  for (uint32_t c = 0; c < nchunk; ++c) {
+    uint32_t cur = load_bits32(x, c, nbytes);
+    const uint32_t lend = min(32u, nlev - 32u * c);
+    for (uint32_t b = 0; b < lend; ++b, ++lev) {
+      uint32_t st[1][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[0][j] = s[j] ^ inv;
+      aes256_tt<1>(st, rk, lds, lc);
+      uint32_t A[4], B[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)st[0][j], kQpSwap1, 0xF, 0xF, true);
+        A[j] = odd ? other : st[0][j];
+        B[j] = odd ? st[0][j] : other;
+      }
+      const uint64_t ci = (uint64_t)lev * num_keys + key;
+      const uint4 cs = cw_s[ci];
+      const uint4 cv = cw_v[ci];
+      const uint32_t ct = cw_t[ci];
+      const uint32_t xb = cur >> 31;  // Msb0 bit of x (lib.rs:181)
+      cur <<= 1;
+      const uint32_t keepA = xb - 1u;  // all ones when going left
+      const uint32_t tm = 0u - t;
+      const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w};
+      const uint32_t cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+      const uint32_t tl = (A[0] ^ s[0]) & 1u;
+      const uint32_t tr = (B[0] ^ ~s[0]) & 1u;
+      const uint32_t tn = (xb ? tr : tl) ^ (t & (ct >> xb) & 1u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+        v[j] ^= (((~s[j]) ^ (B[j] & keepA)) & msk) ^ (tm & cvw[j]);  // lib.rs:182/186
+        s[j] = ((s[j] ^ (A[j] & keepA)) & msk) ^ (tm & csw[j]);      // lib.rs:177-178, 183/187
+      }
+      t = tn;
+    }
+  }
+  const uint32_t tm = 0u - t;  // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192)
+  return make_uint4(v[0] ^ s[0] ^ (tm & np.x), v[1] ^ s[1] ^ (tm & np.y), v[2] ^ s[2] ^ (tm & np.z),
+                    v[3] ^ s[3] ^ (tm & np.w));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock, 1) void k_eval16_pair(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
+    const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint64_t total = num_keys * points_per_key;
+  const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 1);
+  for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 1; g - ((threadIdx.x & 63u) >> 1) < total;
+       g += stride) {
+    const bool live = g < total;
+    const uint64_t gg = live ? g : total - 1;
+    uint64_t key = 0;
+    if (MODE == 1) key = __builtin_amdgcn_readfirstlane((uint32_t)(gg / points_per_key));
+    if (MODE == 2) key = gg / points_per_key;
+    const uint32_t odd = threadIdx.x & 1u;
+    const uint4 y = tt_eval_pair(lds, lc, rk, cw_s, cw_v, cw_t, cw_np1[key], s0s[key], party, xs + gg * nbytes,
+                                 nbytes, num_keys, key, odd);
+    if (live && !odd) ys[g] = y;
+  }
+}
+
 // ------------------------------------------------------------------------
 // k_gen16: DcfImpl::gen (lib.rs:86-161) at LAMBDA = 16, one lane per key.
 // Four AES blocks per level (PRG on both parties' seeds, lib.rs:103-104).

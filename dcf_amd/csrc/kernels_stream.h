@@ -32,7 +32,10 @@
 
 namespace {
 
-constexpr uint32_t kStreamUnit = 256;  // points per refill of a wave
+#ifndef DCF_STREAM_UNIT
+#define DCF_STREAM_UNIT 256
+#endif
+constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wave
 
 // Lane's rank among the set bits of `mask` (bits below this lane).
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
@@ -266,10 +269,16 @@ __device__ __forceinline__ void stream_run(
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[i][j] = L.s[i][j] ^ inv;
     }
+#ifdef DCF_PRIO_UPDATE
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (TT2)
       aes256_tt2<NS>(st, rk, lds, lc);
     else
       aes256_tt<NS>(st, rk, lds, lc);
+#ifdef DCF_PRIO_UPDATE
+    __builtin_amdgcn_s_setprio(DCF_PRIO_UPDATE);
+#endif
     // Pin the CW loads above the update: without this the compiler sinks the
     // cw_t load into the (divergent) level-done path and waits on it there.
 #pragma unroll

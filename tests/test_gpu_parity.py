@@ -231,9 +231,11 @@ def test_eval_device_large_sample_and_reconstruction(dcf, nb, m, mode):
     assert not rec[~lt].any()
 
 
-@pytest.mark.parametrize("mode", [1, 4])
+@pytest.mark.parametrize("mode", [0, 1, 4])
 @pytest.mark.parametrize("K,P", [(1, 100), (37, 64), (10, 13), (300, 128)])
 def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P, mode):
+    """mode 0 (auto) on these small batches runs the two-lanes-per-point lockstep kernel
+    (k_eval16_pair) in all three key modes: one key, keys wave-uniform (P % 64 == 0), any P."""
     import torch
     nb = 16
     rng = np.random.default_rng(K * 1000 + P)
