@@ -52,7 +52,7 @@ def hybrid_peak() -> float:
 
 
 ENGINE = {0: "stream", 1: "ttable", 2: "bitsliced", 3: "hybrid", 4: "stream", 5: "stream-hybrid"}
-KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "ttable-small": "k_eval16", "bitsliced": "k_eval16_bs",
+KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "ttable-small": "k_eval16_pair", "bitsliced": "k_eval16_bs",
           "stream": "k_eval16_stream", "mmo": "k_eval16_mmo", "stream-hybrid": "k_eval16_shybrid"}
 
 
