@@ -334,6 +334,28 @@ __device__ __forceinline__ void stream_run(
       L.cur[i] <<= adv;
       if (adv && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
       L.ci[i] += adv;
+#ifndef DCF_REUSE_BRANCH
+      {  // reuse: level nl with B known: its B half now, without an AES slot (branch-free)
+        const uint32_t xb2 = L.cur[i] >> 31, t1 = L.t[i], tm1 = 0u - t1;
+        const uint32_t rm = 0u - (uint32_t)reuse, rr = rm & (0u - xb2);  // reuse / reuse and right
+        const uint32_t cs2w[4] = {cs2[i].x, cs2[i].y, cs2[i].z, cs2[i].w};
+        const uint32_t cv2w[4] = {cv2[i].x, cv2[i].y, cv2[i].z, cv2[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+          // v ^= v_hat(side) ^ t*cw.v: right ~s & M, left (B^~s) & M   (lib.rs:182/186)
+          L.v[i][j] ^= rm & ((((xb2 ? ~L.s[i][j] : d[j]) & msk) ^ (tm1 & cv2w[j])));
+          L.s[i][j] ^= rr & tm1 & cs2w[j];  // right: s' = s & M ^ t*cw.s   (lib.rs:178)
+        }
+        // right: the level ends, t' = lsb(B^~s) ^ t & cw.tr (lib.rs:180); left: A next
+        L.t[i] = rr ? ((d0 ^ (t1 & (ct2[i] >> 1))) & 1u) : L.t[i];
+        L.ph[i] = (reuse && !xb2) ? 1u : L.ph[i];
+        nl += rr & 1u;
+        L.cur[i] <<= (rr & 1u);
+        L.ci[i] += rr & 1u;
+        if (rr && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+      }
+#else
       if (reuse) {  // level nl with B known: its B half now, without an AES slot
         const uint32_t xb2 = L.cur[i] >> 31, t1 = L.t[i], tm1 = 0u - t1;
         const uint32_t cs2w[4] = {cs2[i].x, cs2[i].y, cs2[i].z, cs2[i].w};
@@ -355,6 +377,7 @@ __device__ __forceinline__ void stream_run(
           L.ph[i] = 1u;  // left: A next
         }
       }
+#endif
       L.lev[i] = nl;
     }
     // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.
