@@ -36,6 +36,12 @@ namespace {
 #define DCF_STREAM_UNIT 256
 #endif
 constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wave
+#ifndef DCF_LDS_KEYS
+#define DCF_LDS_KEYS 0  // 1: stream engine round keys from LDS (no SGPR spills, but 28 more LDS
+#endif                  //    reads per iteration: C3 463-480 vs 499 M evals/s, A/B r01l)
+#ifndef DCF_LDS_KEYS_LATE
+#define DCF_LDS_KEYS_LATE true  // ... read late (per round), so they are not all hoisted into VGPRs
+#endif
 
 // Lane's rank among the set bits of `mask` (bits below this lane).
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
@@ -189,9 +195,9 @@ __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ c
 }
 
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
-template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT>
+template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false>
 __device__ __forceinline__ void stream_run(
-    const uint32_t* lds, const RoundKeys& rk, const uint4* __restrict__ cw_s,
+    const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
@@ -272,10 +278,16 @@ __device__ __forceinline__ void stream_run(
 #ifdef DCF_PRIO_UPDATE
     __builtin_amdgcn_s_setprio(0);
 #endif
-    if (TT2)
+    if (TT2) {
       aes256_tt2<NS>(st, rk, lds, lc);
-    else
+    } else if (LK) {  // round keys from LDS: one ds_read_b128 per round (see k_eval16_stream)
+      const uint4* rkp[NS];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) rkp[i] = rkl;
+      aes_tt_lk<14, NS, DCF_LDS_KEYS_LATE>(st, rkp, lds, lc);
+    } else {
       aes256_tt<NS>(st, rk, lds, lc);
+    }
 #ifdef DCF_PRIO_UPDATE
     __builtin_amdgcn_s_setprio(DCF_PRIO_UPDATE);
 #endif
@@ -408,11 +420,18 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
     uint4* __restrict__ ys, const PrefixTable pf) {
   __shared__ uint32_t lds[TT2 ? kLdsWords2 : kLdsWords];
+  // DCF_LDS_KEYS: the AES-256 schedule in LDS (240 B), one broadcast ds_read_b128 per
+  // round, instead of 60 kernel-argument SGPRs that the compiler partly spills to VGPR
+  // lanes (v_readlane per key word and round).  Measured slower (LDS is the tighter unit).
+  __shared__ uint4 rks[15];
+  if (threadIdx.x < 15)
+    rks[threadIdx.x] = make_uint4(rk.w[4 * threadIdx.x], rk.w[4 * threadIdx.x + 1], rk.w[4 * threadIdx.x + 2],
+                                  rk.w[4 * threadIdx.x + 3]);
   if (TT2)
     lds_fill_tables2(lds, tab);
   else
-    lds_fill_tables(lds, tab);
-  stream_run<NS, XREG, MULTI, TT2, kStreamUnit>(lds, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys,
+    lds_fill_tables(lds, tab);  // its barrier also publishes rks
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0>(lds, rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys,
                                                 ppk, total, ctr, ys, pf);
 }
 
