@@ -94,6 +94,22 @@ __device__ __forceinline__ uint64_t next_unit_base(uint32_t* __restrict__ ctr, u
 }
 constexpr uint32_t kFdUnit = 16;
 
+// Runtime unit size for a grid over n items: kFdUnit wave iterations per unit when
+// there is work for every wave that many times over, fewer (down to 1) otherwise,
+// so a small level is spread over all the grid's waves instead of one wave walking
+// a whole 1024-item unit (the shared-prefix tables' upper levels: 60-110 us each).
+__device__ __forceinline__ uint32_t fd_unit(uint64_t n) {
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t per = n / (64u * waves);
+  return per >= kFdUnit ? kFdUnit : (per ? (uint32_t)per : 1u);
+}
+__device__ __forceinline__ uint64_t next_unit_base_n(uint32_t* __restrict__ ctr, uint64_t base, uint32_t U) {
+  if (base != ~0ull && ((base >> 6) + 1) % U != 0) return base + 64;
+  uint32_t u = 0;
+  if ((threadIdx.x & 63u) == 0) u = atomicAdd(ctr, 1u);
+  return (uint64_t)__builtin_amdgcn_readfirstlane(u) * 64u * U;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock, 1) void k_eval16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
@@ -369,8 +385,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
   const uint32_t npw[4] = {np.x, np.y, np.z, np.w};
   const bool last = lev + 1 == nlev;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = next_unit_base<kFdUnit>(ctr, ~0ull); base < nparents;
-       base = next_unit_base<kFdUnit>(ctr, base)) {
+  const uint32_t unit = fd_unit(nparents);
+  for (uint64_t base = next_unit_base_n(ctr, ~0ull, unit); base < nparents;
+       base = next_unit_base_n(ctr, base, unit)) {
     const uint64_t j = base + (threadIdx.x & 63u);
     const bool live = j < nparents;
     const uint64_t jj = live ? j : nparents - 1;
@@ -428,8 +445,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_tail16(
   const uint32_t lc = lane_const();
   const uint4 np = cw_np1[0];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = next_unit_base<kFdUnit>(ctr, ~0ull); base < nnodes;
-       base = next_unit_base<kFdUnit>(ctr, base)) {
+  const uint32_t unit = fd_unit(nnodes);
+  for (uint64_t base = next_unit_base_n(ctr, ~0ull, unit); base < nnodes;
+       base = next_unit_base_n(ctr, base, unit)) {
     const uint64_t j = base + (threadIdx.x & 63u);
     const bool live = j < nnodes;
     const uint64_t jj = live ? j : nnodes - 1;

@@ -249,8 +249,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16_mmo(
   const uint32_t npw[4] = {np.x, np.y, np.z, np.w};
   const bool last = lev + 1 == nlev;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = next_unit_base<kFdUnit>(ctr, ~0ull); base < nparents;
-       base = next_unit_base<kFdUnit>(ctr, base)) {
+  const uint32_t unit = fd_unit(nparents);
+  for (uint64_t base = next_unit_base_n(ctr, ~0ull, unit); base < nparents;
+       base = next_unit_base_n(ctr, base, unit)) {
     const uint64_t j = base + (threadIdx.x & 63u);
     const bool live = j < nparents;
     const uint64_t jj = live ? j : nparents - 1;
