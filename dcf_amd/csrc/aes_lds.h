@@ -239,6 +239,70 @@ __device__ __forceinline__ void aes_tt_lk(uint32_t (&st)[NB][4], const uint4* co
     for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
 }
 
+// AES-256 with round keys read per round from a device copy of the schedule (one
+// uniform global_load_dwordx4 per round, shared by the NB blocks).  The load
+// address is base + zb + 16 r, where zb is a zero that an empty asm "redefines"
+// after the previous round's state, so the compiler can neither hoist the
+// 15 loads into 60 live registers nor needs any VALU to form the address.
+template <int NB>
+__device__ __forceinline__ void aes256_tt_gk(uint32_t (&st)[NB][4], const uint4* __restrict__ rkg,
+                                             const uint32_t* lds, uint32_t lc) {
+  const char* base = reinterpret_cast<const char*>(rkg);
+  uint32_t zb = 0u;
+  {
+    const uint4 k = *reinterpret_cast<const uint4*>(base);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      st[b][0] ^= k.x; st[b][1] ^= k.y; st[b][2] ^= k.z; st[b][3] ^= k.w;
+    }
+  }
+#ifndef DCF_GK_AHEAD
+#define DCF_GK_AHEAD 3  // rounds between a key's load and its use (r01o A/B on C3: 1 -1.2 %, 2 +2.2 %,
+                        // 3 +3.6 %, 4 +3.1 %, 6 -12 % vs SGPR keys)
+#endif
+  uint4 kq[DCF_GK_AHEAD];
+#pragma unroll
+  for (int q = 0; q < DCF_GK_AHEAD - 1; ++q) kq[q] = *reinterpret_cast<const uint4*>(base + 16 * (q + 1));
+#pragma unroll
+  for (int r = 1; r < 15; ++r) {
+    asm volatile("" : "+v"(zb) : "v"(st[0][0]), "v"(st[NB - 1][0]));
+    const int rn = r + DCF_GK_AHEAD - 1;  // the round whose key is loaded now
+    if (rn < 15) kq[(rn - 1) % DCF_GK_AHEAD] = *reinterpret_cast<const uint4*>(base + zb + 16 * rn);
+    const uint4 k = kq[(r - 1) % DCF_GK_AHEAD];
+    const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+    uint32_t o[NB][4];
+    if (r < 14) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
+        }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+          const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
+          const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
+          o[b][j] = xor3(lo, hi, kw[j]);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+}
+
 template <int NB>
 __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* const (&rk)[NB], const uint32_t* lds,
                                           uint32_t lc) {

@@ -99,6 +99,7 @@ struct dcf_prg {
   std::vector<RoundKeys> rk;  // Aes256::new per key (prg.rs:28-31)
   uint4* d_rk128 = nullptr;   // MMO: AES-128 schedules of ciphers 0..3 (4 x 11 round keys)
   uint4* d_rk2 = nullptr;     // LAMBDA >= 32 stream head: AES-256 schedules of ciphers 0 and 17
+  uint4* d_rk0 = nullptr;     // LAMBDA = 16 stream eval: AES-256 schedule of cipher 0 (15 x 16 B)
   uint8_t* d_dig = nullptr;   // LAMBDA >= 32 stream head: compact CW digest of the current key
   uint8_t* d_kdig = nullptr;  // LAMBDA = 16 multi-key stream eval: key-major CW digest
   size_t kdig_bytes = 0;
@@ -464,6 +465,7 @@ void dcf_prg_free(dcf_prg* p) {
     if (p->d_km) (void)hipFree(p->d_km);
     if (p->d_rk128) (void)hipFree(p->d_rk128);
     if (p->d_rk2) (void)hipFree(p->d_rk2);
+    if (p->d_rk0) (void)hipFree(p->d_rk0);
     if (p->d_dig) (void)hipFree(p->d_dig);
     if (p->d_kdig) (void)hipFree(p->d_kdig);
     if (p->d_ws) (void)hipFree(p->d_ws);
@@ -743,6 +745,10 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #define DCF_STREAM_NS 2  // streams per lane
 #endif
     if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
+    if (!p->d_rk0) {
+      HIP_TRY(hipMalloc(&p->d_rk0, sizeof(RoundKeys)));
+      HIP_TRY(hipMemcpy(p->d_rk0, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice));
+    }
     HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
     const uint64_t units = (total + kStreamUnit - 1) / kStreamUnit;
     if (units > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "stream eval: more than 2^32 work units");
@@ -780,14 +786,14 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #define DCF_STREAM(XR, MK)                                                                                    \
   hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], scs, \
                      cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,  \
-                     (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf)
+                     (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf, p->d_rk0)
 #ifdef DCF_STREAM_TT2
     if (xreg && !multi) {
       uint64_t b2 = (units + 9) / 10;
       if (b2 > 2 * (uint64_t)p->cus) b2 = 2 * (uint64_t)p->cus;
       hipLaunchKernelGGL((k_eval16_stream<2, true, false, 640, true>), dim3((unsigned)b2), dim3(640), 0, st, p->d_tab,
                          p->rk[0], scs, cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes,
-                         (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf);
+                         (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf, p->d_rk0);
     } else
 #endif
     if (xreg && multi) DCF_STREAM(true, true);

@@ -39,6 +39,9 @@ constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wav
 #ifndef DCF_LDS_KEYS
 #define DCF_LDS_KEYS 0  // 1: stream engine round keys from LDS (no SGPR spills, but 28 more LDS
 #endif                  //    reads per iteration: C3 463-480 vs 499 M evals/s, A/B r01l)
+#ifndef DCF_STREAM_GK
+#define DCF_STREAM_GK 1  // 1: single-key stream engine reads round keys from global memory (aes256_tt_gk)
+#endif
 #ifndef DCF_LDS_KEYS_LATE
 #define DCF_LDS_KEYS_LATE true  // ... read late (per round), so they are not all hoisted into VGPRs
 #endif
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ c
 }
 
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
-template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false>
+template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -280,6 +283,8 @@ __device__ __forceinline__ void stream_run(
 #endif
     if (TT2) {
       aes256_tt2<NS>(st, rk, lds, lc);
+    } else if (GK) {  // round keys from global memory, loaded DCF_GK_AHEAD rounds ahead
+      aes256_tt_gk<NS>(st, rkl, lds, lc);
     } else if (LK) {  // round keys from LDS: one ds_read_b128 per round (see k_eval16_stream)
       const uint4* rkp[NS];
 #pragma unroll
@@ -418,7 +423,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
-    uint4* __restrict__ ys, const PrefixTable pf) {
+    uint4* __restrict__ ys, const PrefixTable pf, const uint4* __restrict__ rkg) {
   __shared__ uint32_t lds[TT2 ? kLdsWords2 : kLdsWords];
   // DCF_LDS_KEYS: the AES-256 schedule in LDS (240 B), one broadcast ds_read_b128 per
   // round, instead of 60 kernel-argument SGPRs that the compiler partly spills to VGPR
@@ -431,7 +436,12 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     lds_fill_tables2(lds, tab);
   else
     lds_fill_tables(lds, tab);  // its barrier also publishes rks
-  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0>(lds, rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys,
+  // GK (single key): per-round reads from the device copy of the schedule instead
+  // (global_load_dwordx4 of a uniform address, L1-resident, 3 rounds ahead: no SGPR
+  // spill reloads, no LDS traffic; C3 +3.6 %, r01o A/B).  Multi-key runs keep the
+  // SGPR schedule (C5 -14 % with GK: its CW digest loads share the vector memory path).
+  constexpr bool GK = DCF_STREAM_GK && !MULTI && !TT2;
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK>(lds, GK ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys,
                                                 ppk, total, ctr, ys, pf);
 }
 
