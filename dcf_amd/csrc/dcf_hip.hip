@@ -216,6 +216,14 @@ int build_wide_prefix(dcf_prg* p, uint32_t nlev, int party, const uint8_t* s0, u
   return DCF_OK;
 }
 
+// Device copy of cipher 0's AES-256 schedule (read per round by aes256_tt_gk).
+int ensure_rk0(dcf_prg* p) {
+  if (p->d_rk0) return DCF_OK;
+  HIP_TRY(hipMalloc(&p->d_rk0, sizeof(RoundKeys)));
+  HIP_TRY(hipMemcpy(p->d_rk0, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice));
+  return DCF_OK;
+}
+
 // Expand the top `levels` levels of the key's tree (s = s0, v = 0, t = party at the
 // root; k_fd_level16 per level, as the full-domain eval does) into p->d_pfx.
 int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const uint4* cwv, const uint8_t* cwt,
@@ -745,10 +753,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #define DCF_STREAM_NS 2  // streams per lane
 #endif
     if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
-    if (!p->d_rk0) {
-      HIP_TRY(hipMalloc(&p->d_rk0, sizeof(RoundKeys)));
-      HIP_TRY(hipMemcpy(p->d_rk0, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice));
-    }
+    if (int rc = ensure_rk0(p)) return rc;
     HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
     const uint64_t units = (total + kStreamUnit - 1) / kStreamUnit;
     if (units > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "stream eval: more than 2^32 work units");
@@ -960,6 +965,7 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   const size_t ctr_off = (2 * maxnodes * nodeb + 64 + 255) & ~(size_t)255;
   int rc = ensure_ws(p, ctr_off + 64 * sizeof(uint32_t), st);
   if (rc) return rc;
+  if (fused && (rc = ensure_rk0(p))) return rc;
   uint8_t* w = p->d_ws;
   uint32_t* ctrs = (uint32_t*)(w + ctr_off);
   HIP_TRY(hipMemsetAsync(ctrs, 0, 64 * sizeof(uint32_t), st));
@@ -995,7 +1001,7 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   if (fused) {
     const uint64_t nodes = 1ull << lev_end;
     hipLaunchKernelGGL(k_fd_tail16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
-                       p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63);
+                       p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63, p->d_rk0);
     HIP_TRY(hipGetLastError());
   }
   return DCF_OK;

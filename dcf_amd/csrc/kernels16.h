@@ -434,12 +434,16 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
 // Last D levels of the full-domain expansion in registers: one lane per node at
 // level nlev - D expands its 2^D leaves (2^D - 1 PRG calls) and writes their y
 // contiguously (2^D x 16 B), so the two largest node levels never go to HBM.
+#ifndef DCF_FD_GK
+#define DCF_FD_GK 0  // 1: aes256_tt_gk round keys (r01o A/B on FD N=4: 138.5 vs 119.7 ms, -13 %)
+#endif
 template <int D>
 __global__ __launch_bounds__(kBlock, 1) void k_fd_tail16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint32_t lev0, const uint64_t nnodes, const uint4* __restrict__ s_in, const uint4* __restrict__ v_in,
-    const uint8_t* __restrict__ t_in, uint4* __restrict__ ys, uint32_t* __restrict__ ctr) {
+    const uint8_t* __restrict__ t_in, uint4* __restrict__ ys, uint32_t* __restrict__ ctr,
+    const uint4* __restrict__ rkg) {
   __shared__ uint32_t lds[kLdsWords];
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
@@ -474,7 +478,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_tail16(
           st[0][k] = ns[i][k];
           st[1][k] = ~ns[i][k];
         }
-        aes256_tt<2>(st, rk, lds, lc);  // A, B: both children (lib.rs:176-189 with x bit 0 / 1)
+        // A, B: both children (lib.rs:176-189 with x bit 0 / 1)
+        if (DCF_FD_GK)
+          aes256_tt_gk<2>(st, rkg, lds, lc);  // round keys per round from global memory (no SGPR spills)
+        else
+          aes256_tt<2>(st, rk, lds, lc);
         const uint32_t tm = 0u - nt[i];
         uint32_t sl[4], vl[4], sr[4], vr[4];
 #pragma unroll
