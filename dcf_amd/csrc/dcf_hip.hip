@@ -668,6 +668,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #ifndef DCF_SMALL_PAIR
 #define DCF_SMALL_PAIR 1
 #endif
+    if (int rc = ensure_rk0(p)) return rc;
     const uint64_t lanes_per_point = DCF_SMALL_PAIR ? 2 : 1;
     uint64_t threads = (total * lanes_per_point + p->cus - 1) / p->cus;
     threads = ((threads + 63) / 64) * 64;
@@ -677,7 +678,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #define DCF_SMALL(MODE)                                                                                           \
   hipLaunchKernelGGL(k_eval16_pair<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,                  \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk,  \
-                     (uint4*)ys)
+                     (uint4*)ys, p->d_rk0)
 #else
 #define DCF_SMALL(MODE)                                                                                           \
   hipLaunchKernelGGL(k_eval16<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s,    \

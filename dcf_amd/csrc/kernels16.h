@@ -142,12 +142,16 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16(
 // with half the AES work per level: a small batch has too few waves per SIMD to
 // overlap the LDS lookups with the rest (C1: 7 waves per CU with one lane per point).
 constexpr int kQpSwap1 = 1 | (0 << 2) | (3 << 4) | (2 << 6);
+#ifndef DCF_PAIR_GK
+#define DCF_PAIR_GK 1
+#endif
 
 __device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, const RoundKeys& rk,
                                               const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
                                               const uint8_t* __restrict__ cw_t, const uint4 np, const uint4 sv,
                                               uint32_t party, const uint8_t* __restrict__ x, uint32_t nbytes,
-                                              uint64_t num_keys, uint64_t key, uint32_t odd) {
+                                              uint64_t num_keys, uint64_t key, uint32_t odd,
+                                              const uint4* __restrict__ rkg) {
   const uint32_t nlev = 8u * nbytes;
   const uint32_t nchunk = (nbytes + 3u) >> 2;
   const uint32_t inv = 0u - odd;  // odd lane: ~s (B)
@@ -162,7 +166,10 @@ __device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, 
       uint32_t st[1][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[0][j] = s[j] ^ inv;
-      aes256_tt<1>(st, rk, lds, lc);
+      if (DCF_PAIR_GK)
+        aes256_tt_gk<1>(st, rkg, lds, lc);  // round keys per round from global memory
+      else
+        aes256_tt<1>(st, rk, lds, lc);
       uint32_t A[4], B[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -202,7 +209,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_pair(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
-    const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys) {
+    const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys,
+    const uint4* __restrict__ rkg) {
   __shared__ uint32_t lds[kLdsWords];
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
@@ -217,7 +225,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_pair(
     if (MODE == 2) key = gg / points_per_key;
     const uint32_t odd = threadIdx.x & 1u;
     const uint4 y = tt_eval_pair(lds, lc, rk, cw_s, cw_v, cw_t, cw_np1[key], s0s[key], party, xs + gg * nbytes,
-                                 nbytes, num_keys, key, odd);
+                                 nbytes, num_keys, key, odd, rkg);
     if (live && !odd) ys[g] = y;
   }
 }
