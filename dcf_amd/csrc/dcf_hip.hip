@@ -146,7 +146,7 @@ int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
 // point), at most 24 (a 553 MB table), none below 8, always < 8N.  Measured (r01i,
 // C2: 2^24 points, N = 4): D = 12 / 16 / 20 / 24 -> 2.00 / 2.29 / 2.62 / 2.83 G evals/s
 // (1.44 without); C3 (2^28, N = 16): D = 16 / 24 -> 450 / 477 M (397 M without).
-constexpr uint32_t kPrefixMax = 24;       // auto
+constexpr uint32_t kPrefixMax = 26;       // auto (C3 r01q sweep: 24 519, 25 521, 26 524, 27 524 M evals/s)
 constexpr uint32_t kPrefixMaxForced = 28;  // dcf_prg_set_prefix_levels (2^28 x 33 B x 2 = 17.7 GB)
 uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
   if (p->lambda != 16 || num_keys != 1 || p->prefix_levels == 0) return 0;

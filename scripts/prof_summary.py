@@ -93,9 +93,9 @@ if __name__ == "__main__":
         t["source"] = sys.argv[1]
         t["kernel"] = prefix
         # the launch shape of scripts/gpu_profile.sh's bench run (bench.py defaults, workload C3)
-        # auto shared-prefix depth 24: x (16 B) + y (16 B) + one 32-byte table row per point
+        # auto shared-prefix depth 26: x (16 B) + y (16 B) + one 32-byte table row per point
         t.update({"workload": "C3", "points_per_launch": 1 << 28, "n_bytes": 16, "lambda": 16,
-                  "prefix_levels": 24, "algorithmic_bytes": (1 << 28) * 64,
+                  "prefix_levels": 26, "algorithmic_bytes": (1 << 28) * 64,
                   "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- "
                              "python bench.py --steps 2 --warmup 1 --no-cpu"})
         with open(sys.argv[2], "w") as f:
