@@ -1,14 +1,17 @@
 """Benchmark: DCF batch eval on MI355X (BASELINE.json metric).
 
 Workload (default, BASELINE.json configs[2] = SURVEY.md §8 C3): N = 16 (128-bit
-x), LAMBDA = 16, Aes256HirosePrg, one key, 2^28 uniformly random points per GPU
-resident in HBM, party 0 (the reference bench's shape, benches/dcf_batch_eval.rs:
-25-30, scaled up).  A step = one `Dcf::eval` pass over the rank's points.  Ranks
-hold disjoint contiguous slices of the global point space (weak scaling); the
-key is generated once on rank 0 and broadcast over RCCL before timing; there is
-no collective inside the timed region.
+x), LAMBDA = 16, Aes256HirosePrg, one key, 2^28 uniformly random points resident
+in HBM, party 0 (the reference bench's shape, benches/dcf_batch_eval.rs:25-30,
+scaled up).  A step = one `Dcf::eval` pass over the rank's points.  C3 is "a
+single key at 2^28 points sharded across 1/2/4/8 MI355X": by default the 2^28
+points are split into contiguous per-rank slices (strong scaling, dcf_point_slice);
+`--scaling weak` gives every rank its own 2^28 points instead.  The key is
+generated once on rank 0 and broadcast over RCCL before timing; there is no
+collective inside the timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5|fd]
+                  [--scaling strong|weak] [--host-path]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement" for every field).
@@ -20,6 +23,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -29,7 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import dcf_amd  # noqa: E402
-from dcf_amd.dist import broadcast_key, weak_slice  # noqa: E402
+from dcf_amd.dist import broadcast_key, point_slice, weak_slice  # noqa: E402
 
 METRIC = "DCF evals/sec (node) at 128-bit input, λ=16B; AES blocks/s vs INT roofline"
 
@@ -72,19 +76,29 @@ def engine_peak(engine: str) -> float:
 
 def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels: int = 0):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, written by scripts/prof_summary.py from
-    scripts/gpu_profile.sh: 2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md §HBM),
-    only when that profile ran this exact launch shape; else None."""
+    (profiles/pmc_traffic.json: one entry per profiled launch shape, written by
+    scripts/prof_summary.py from scripts/gpu_profile.sh: 2 x FETCH_SIZE + WRITE_SIZE,
+    MI355X_MICROARCH.md §HBM), only when a profile ran this exact launch shape; else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if (t.get("kernel"), t.get("points_per_launch"), t.get("n_bytes"), t.get("lambda"),
-            t.get("prefix_levels", 0)) != (kernel, points, n_bytes, lam, prefix_levels):
-        return None
-    return t.get("traffic_bytes")
+    for e in (t if isinstance(t, list) else [t]):
+        if (e.get("kernel"), e.get("points_per_launch"), e.get("n_bytes"), e.get("lambda"),
+                e.get("prefix_levels", 0)) == (kernel, points, n_bytes, lam, prefix_levels):
+            return e.get("traffic_bytes")
+    return None
+
+
+def traffic_fields(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels: int, alg_bytes: float):
+    """(traffic, source): the PMC figure when profiles/ holds this launch shape, otherwise
+    the algorithmic bytes, labelled as such (never null)."""
+    t = pmc_traffic(kernel, points, n_bytes, lam, prefix_levels)
+    if t is not None:
+        return t, "pmc: 2 x FETCH_SIZE + WRITE_SIZE per launch (profiles/pmc_traffic.json)"
+    return alg_bytes, "algorithmic bytes (no PMC profile of this exact launch shape in profiles/pmc_traffic.json)"
 
 
 def blocks_per_eval(n_bytes: int, lam: int) -> int:
@@ -159,53 +173,124 @@ def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int):
     return cwb, seeds, alpha, beta
 
 
-def gen_points(m: int, n_bytes: int, rank: int, seed: int) -> torch.Tensor:
-    """Rank r's slice [r*m, (r+1)*m) of the global point space (weak scaling),
-    drawn on device from a generator keyed by (seed, slice start)."""
-    start, _ = weak_slice(m, rank)
+def gen_points(m: int, n_bytes: int, start: int, seed: int) -> torch.Tensor:
+    """Global points [start, start + m) (the rank's slice), drawn on device from a
+    generator keyed by (seed, slice start)."""
     g = torch.Generator(device="cuda")
     g.manual_seed(seed * 1000003 + start)
     return torch.randint(0, 256, (m, n_bytes), dtype=torch.uint8, device="cuda", generator=g)
 
 
-def cpu_baseline(keys, n_bytes, lam, cwb_h: bytes, s0: bytes, xs_sample: np.ndarray, ys_gpu: np.ndarray,
-                 target_s: float, prg_kind: str = "hirose"):
-    """Time the C++-free C restatement of the reference eval (oracle, AES-NI,
-    one pthread per core over contiguous point chunks like rayon) on this host.
-    Bounded: calibrate on a small slice, then run ~target_s of CPU work."""
+def oracle_key(cwb_h: bytes, n_bytes: int, lam: int, K: int = 1, key: int = 0):
+    """Key `key` of a K-key CWB (include/dcf_hip.h layout) for the oracle (checker only)."""
     from oracle import oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    P = (O.OracleMmoPrg if prg_kind == "mmo" else O.OraclePrg)(keys, lam)
-    k = O.OracleKey(n_bytes, lam)
     n = 8 * n_bytes
-    k.cw_s[:] = np.frombuffer(cwb_h[:n * lam], np.uint8).reshape(n, lam)
-    k.cw_v[:] = np.frombuffer(cwb_h[n * lam:2 * n * lam], np.uint8).reshape(n, lam)
-    k.cw_t[:] = np.frombuffer(cwb_h[2 * n * lam:2 * n * lam + n], np.uint8)
-    off = dcf_amd.cwb_np1_offset(n_bytes, lam, 1)
-    k.cw_np1[:] = np.frombuffer(cwb_h[off:off + lam], np.uint8)
+    c = np.frombuffer(cwb_h, np.uint8)
+    k = O.OracleKey(n_bytes, lam)
+    k.cw_s[:] = c[:n * K * lam].reshape(n, K, lam)[:, key]
+    k.cw_v[:] = c[n * K * lam:2 * n * K * lam].reshape(n, K, lam)[:, key]
+    k.cw_t[:] = c[2 * n * K * lam:2 * n * K * lam + n * K].reshape(n, K)[:, key]
+    off = dcf_amd.cwb_np1_offset(n_bytes, lam, K)
+    k.cw_np1[:] = c[off:off + K * lam].reshape(K, lam)[key]
+    return k
+
+
+def host_threads() -> int:
+    return max(1, min(16, len(os.sched_getaffinity(0))))  # the GPU box's CPU share is 16
+
+
+def cpu_baseline(keys, n_bytes, lam, cwb_h: bytes, seeds, xs_sample: np.ndarray, ys_gpu, target_s: float,
+                 prg_kind: str = "hirose", threads: int = 0, parties=(0,)):
+    """Time the C restatement of the reference eval (oracle/dcf_oracle.c: AES-NI, one
+    pthread per core over contiguous point chunks like rayon, lib.rs:194-199) on this
+    host, on a bounded sample: calibrate on a small slice, then run ~target_s of CPU
+    work (whole-sample repeats when the sample is smaller than that).  ys_gpu[b]: the
+    GPU's outputs of party b for the sample rows (the check, `matches_gpu`)."""
+    from oracle import oracle as O
+    threads = threads or host_threads()
+    P = (O.OracleMmoPrg if prg_kind == "mmo" else O.OraclePrg)(keys, lam)
+    k = oracle_key(cwb_h, n_bytes, lam)
     cal = xs_sample[: min(len(xs_sample), max(threads, 8192 * threads * 16 // lam))]
     t0 = time.perf_counter()
-    y = O.eval_(P, 0, k, s0, cal, nthreads=threads)
+    matches = True
+    for b in parties:
+        y = O.eval_(P, b, k, seeds[b], cal, nthreads=threads)
+        matches = matches and bool(np.array_equal(y, ys_gpu[b][: len(cal)]))
     dt = time.perf_counter() - t0
-    matches = bool(np.array_equal(y, ys_gpu[: len(cal)]))
-    rate = len(cal) / dt
-    m = int(min(len(xs_sample), max(len(cal), rate * target_s)))
+    rate = len(cal) * len(parties) / dt
+    m = int(min(len(xs_sample), max(len(cal), rate * target_s / len(parties))))
+    reps = max(1, min(200, int(round(rate * target_s / (m * len(parties))))))
     t0 = time.perf_counter()
-    y = O.eval_(P, 0, k, s0, xs_sample[:m], nthreads=threads)
+    for r in range(reps):
+        for b in parties:
+            y = O.eval_(P, b, k, seeds[b], xs_sample[:m], nthreads=threads)
+            if r == 0:
+                matches = matches and bool(np.array_equal(y, ys_gpu[b][:m]))
     dt = time.perf_counter() - t0
-    matches = matches and bool(np.array_equal(y, ys_gpu[:m]))
+    who = "both parties" if len(parties) == 2 else f"party {parties[0]}"
     return {
-        "value": m / dt, "unit": "evals/s", "cores": threads, "kind": "port",
-        "sample": f"{m} of the GPU's points (first rows of rank 0's slice), party 0, same key; "
-                  f"C restatement of lib.rs:163-204 + prg.rs:42-73 with AES-NI, {threads} threads; "
-                  f"{dt:.1f} s",
-        "aesni": P.uses_aesni, "matches_gpu": matches,
+        "value": m * len(parties) * reps / dt, "unit": "evals/s", "cores": threads, "kind": "port",
+        "sample": f"{m} of the GPU's points (first rows of rank 0's slice) x {reps} repeat(s), {who}, same key; "
+                  f"C restatement of lib.rs:163-204 + prg.rs:42-73 with AES-NI, {threads} thread(s); {dt:.1f} s",
+        "ms_per_batch": dt / reps * 1e3, "aesni": P.uses_aesni, "matches_gpu": matches,
     }
+
+
+def timed_loop(step, steps: int, warmup: int, world: int, stream=None):
+    """Run `warmup` untimed steps, then time `steps` steps bracketed by barrier + sync.
+    Returns (wall seconds, max over ranks; seconds per step on `stream` by HIP events)."""
+    stream = stream or torch.cuda.current_stream()
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    w = time.perf_counter() - t0
+    t = torch.tensor([w], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), ev0.elapsed_time(ev1) / 1e3 / steps
+
+
+def host_path(d, k_share_fn, xs_dev, lam, parties: int, steps: int):
+    """`dcf_eval` on host buffers (what a Rust DcfHip::eval pays: PCIe both ways through
+    the pipelined staging path), over the same points; evals/s including PCIe."""
+    xs_h = xs_dev.cpu().numpy()
+    m = xs_h.shape[0]
+    ys = [np.empty((m, lam), np.uint8) for _ in range(parties)]
+    shares = [k_share_fn(b) for b in range(parties)]
+    for b in range(parties):  # warm-up: allocates the pooled staging buffers
+        d.eval(bool(b), shares[b], xs_h, ys[b])
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for b in range(parties):
+            d.eval(bool(b), shares[b], xs_h, ys[b])
+    dt = time.perf_counter() - t0
+    return {"value": m * parties * steps / dt, "unit": "evals/s", "ms_per_step": dt / steps * 1e3,
+            "pcie_bytes_per_step": parties * m * (xs_h.shape[1] + lam),
+            "note": "dcf_eval (host buffers, synchronous): x H2D + y D2H through pinned staging, 3 streams, "
+                    "128 MiB chunks overlapping copies with kernels; includes the host memcpy to/from staging"}, ys
 
 
 def run_eval(args, world, rank):
     nb, lam = args.n_bytes, args.lam
-    m = args.points
+    if args.scaling == "strong":
+        start, m = point_slice(args.points, world, rank)
+        global_points = args.points
+    else:
+        start, m = weak_slice(args.points, rank)
+        global_points = args.points * world
     rng = np.random.default_rng(0xDCF0001)
     # benches/dcf_batch_eval.rs:7 uses 2 AES keys at LAMBDA = 16; benches/dcf_large_lambda.rs:10 uses 2048.
     if args.prg == "mmo":  # Aes128MatyasMeyerOseasPrg (north_star's PRG; not in the reference): 4 AES-128 keys
@@ -225,7 +310,7 @@ def run_eval(args, world, rank):
     cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002)
     s0 = seeds[0].contiguous()
     s1 = seeds[1].contiguous()
-    xs = gen_points(m, nb, rank, 0xDCF0003)
+    xs = gen_points(m, nb, start, 0xDCF0003)
     ys = torch.empty((m, lam), dtype=torch.uint8, device="cuda")
     # C1 (benches/dcf_batch_eval.rs shape) evaluates both parties per step.
     parties = 2 if args.workload == "c1" else 1
@@ -236,45 +321,21 @@ def run_eval(args, world, rank):
         if parties == 2:
             d.eval_device(True, cwb, s1, xs, ys1)
 
-    def timed(steps):
-        """(wall seconds max over ranks, seconds per eval call on the launch stream)"""
-        stream = torch.cuda.current_stream()
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for _ in range(steps):
-            step()
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        w = time.perf_counter() - t0
-        t = torch.tensor([w], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()), ev0.elapsed_time(ev1) / 1e3 / steps / parties
-
-    wall, kern_s = timed(args.steps)
+    wall, kern_s = timed_loop(step, args.steps, args.warmup, world)
+    kern_s /= parties
     dev_blocks = prg.last_eval_blocks()  # stream engine: AES blocks of the last launch, counted on the device
     no_prefix = None
     if pfx and not args.no_compare:
         # the same batch without the shared-prefix table (each point walks all 8N levels)
         prg.set_prefix_levels(0)
-        w0, k0 = timed(args.steps)
+        w0, k0 = timed_loop(step, args.steps, args.warmup, world)
         np_blocks = prg.last_eval_blocks()
         prg.set_prefix_levels(args.prefix)
-        no_prefix = {"value": m * world * args.steps * parties / w0, "kernel_ms": k0 * 1e3,
+        no_prefix = {"value": global_points * args.steps * parties / w0, "kernel_ms": k0 / parties * 1e3,
                      "executed_blocks_per_eval": 16 * nb if args.prg == "mmo" else (
                          np_blocks / m if np_blocks else 8 * nb + zero_bits(xs) / m),
                      "speedup": w0 / wall}
-    total_evals = m * world * args.steps * parties
+    total_evals = global_points * args.steps * parties
     value = total_evals / wall
     bpe = blocks_per_eval(nb, lam)
     engine = ENGINE[args.eval_mode] if lam == 16 else "ttable"
@@ -312,22 +373,26 @@ def run_eval(args, world, rank):
     kernel = KERNEL.get(engine, "k_eval16") if lam == 16 else (
         "k_eval_wide_head_stream+k_eval_wide_tail" if engine == "stream-head" else "k_eval_wide_head+k_eval_wide_tail")
     peak = engine_peak(engine)
+    traffic, traffic_src = traffic_fields(kernel, m, nb, lam, pfx, alg_bytes)
+    slicing = (f"2^{int(np.log2(args.points))} points split over {world} GPU(s) (strong)" if args.scaling == "strong"
+               else f"{m} points per GPU (weak)")
     out = {
         "metric": METRIC, "value": value, "unit": "evals/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"{args.workload.upper()}: N={nb} ({8 * nb}-bit x), lambda={lam}, "
                                f"{'Aes128MatyasMeyerOseasPrg' if args.prg == 'mmo' else 'Aes256HirosePrg'} "
-                               f"({len(keys)} AES keys), 1 key, {m} points/GPU in HBM, "
+                               f"({len(keys)} AES keys), 1 key, {slicing}, in HBM, "
                                f"{'both parties' if parties == 2 else 'party 0'}, eval only",
-                   "n_bytes": nb, "lambda": lam, "points_per_gpu": m, "global_points": m * world,
-                   "parallelism": f"points sharded over {world} GPU(s), no collective in timed region"},
+                   "n_bytes": nb, "lambda": lam, "points_per_gpu": m, "global_points": global_points,
+                   "parallelism": f"points sharded over {world} GPU(s) in contiguous slices, "
+                                  "no collective in timed region"},
         "aes_blocks_per_s": value * bpe,
         "roofline": wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine) if lam > 16 else {
             "bound": "lds" if engine in ("ttable", "ttable-small", "stream", "mmo") else ("valu" if engine == "bitsliced" else "lds+valu"),
             "kernel": kernel, "engine": engine,
             "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-128 blocks/s" if engine == "mmo" else "G AES-256 blocks/s",
-            "frac": per_gpu_blocks / peak, "traffic": pmc_traffic(kernel, m, nb, lam, pfx),
+            "frac": per_gpu_blocks / peak, "traffic": traffic, "traffic_source": traffic_src,
             "algorithmic_bytes": alg_bytes, "kernel_ms": kern_s * 1e3,
             "hbm_GBps": alg_bytes / kern_s / 1e9,
             "ttable_only_peak": PEAK_TT_BLOCKS / 1e9,
@@ -345,60 +410,169 @@ def run_eval(args, world, rank):
     }
     if lam > 16:
         out["roofline"]["prefix_levels"] = pfx  # wide stream head below a shared-prefix table
-    if rank == 0 and world == 1 and not args.no_cpu:
+        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic_fields(
+            kernel, m, nb, lam, pfx, m * (nb + lam))
+    host_ys = None
+    if args.host_path or args.workload == "c1":
+        share = dcf_amd.cwb_to_share(cwb.cpu().numpy().tobytes(), nb, lam, [])
+        sd = seeds.cpu().numpy()
+        out["host_path"], host_ys = host_path(
+            d, lambda b: dcf_amd.Share([sd[b].tobytes()], share.cws, share.cw_np1), xs, lam, parties,
+            max(1, min(args.steps, 3)))
+        out["host_path"]["matches_device_path"] = bool(np.array_equal(host_ys[0], ys.cpu().numpy()))
+    if rank == 0 and not args.no_cpu:
         ns = min(m, 1 << 26, max(4096, (1 << 30) // lam))  # at most ~1 GiB of outputs copied back
         xs_h = xs[:ns].cpu().numpy()
-        ys_h = ys[:ns].cpu().numpy()
+        ys_h = [ys[:ns].cpu().numpy()] + ([ys1[:ns].cpu().numpy()] if parties == 2 else [])
         cwb_h = cwb.cpu().numpy().tobytes()
-        out["cpu_baseline"] = cpu_baseline(keys, nb, lam, cwb_h, seeds[0].cpu().numpy().tobytes(), xs_h, ys_h,
-                                           args.cpu_seconds, args.prg)
+        sd = [bytes(seeds[0].cpu().numpy().tobytes()), bytes(seeds[1].cpu().numpy().tobytes())]
+        pp = tuple(range(parties))
+        out["cpu_baseline"] = cpu_baseline(keys, nb, lam, cwb_h, sd, xs_h, ys_h, args.cpu_seconds, args.prg,
+                                           parties=pp)
+        if args.workload == "c1":  # all cores and 1 core
+            out["cpu_baseline_1core"] = cpu_baseline(keys, nb, lam, cwb_h, sd, xs_h, ys_h, args.cpu_seconds / 2,
+                                                     args.prg, threads=1, parties=pp)
     return out
 
 
 def run_c5(args, world, rank):
-    """C5: K independent keys x 64 points: batched gen + eval of both parties."""
+    """C5: K independent keys x 64 points: batched gen + eval of both parties per step.
+    Strong scaling by default: the 2^20 keys are split over the ranks (dcf_point_slice)."""
     nb, lam, P = args.n_bytes, 16, 64
-    K = args.keys
+    if args.scaling == "strong":
+        kstart, K = point_slice(args.keys, world, rank)
+        global_keys = args.keys
+    else:
+        kstart, K = weak_slice(args.keys, rank)
+        global_keys = args.keys * world
     rng = np.random.default_rng(0xDCF0005)
     keys = [rng.bytes(32) for _ in range(2)]
     prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
     d = dcf_amd.DcfImpl(nb, lam, prg)
     g = torch.Generator(device="cuda")
-    g.manual_seed(5 + rank)
+    g.manual_seed(5 * 1000003 + kstart)
     rnd = lambda *s: torch.randint(0, 256, s, dtype=torch.uint8, device="cuda", generator=g)  # noqa: E731
     alpha, beta, s0, s1 = rnd(K, nb), rnd(K, lam), rnd(K, lam), rnd(K, lam)
     xs = rnd(K * P, nb)
     cwb = torch.empty(dcf_amd.cwb_bytes(nb, lam, K), dtype=torch.uint8, device="cuda")
     y0 = torch.empty((K * P, lam), dtype=torch.uint8, device="cuda")
     y1 = torch.empty_like(y0)
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    phase = [0.0, 0.0, 0.0]
 
-    def step():
+    def step(record=False):
+        if record:
+            ev[0].record(stream)
         d.gen_batch_device(alpha, beta, s0, s1, dcf_amd.BoundState.LtBeta, cwb)
+        if record:
+            ev[1].record(stream)
         d.eval_multikey_device(False, cwb, s0, xs, P, y0)
+        if record:
+            ev[2].record(stream)
         d.eval_multikey_device(True, cwb, s1, xs, P, y1)
+        if record:
+            ev[3].record(stream)
 
-    for _ in range(args.warmup):
-        step()
+    # block counts on the device: party 0's eval alone, then party 1's (the last launch)
+    d.gen_batch_device(alpha, beta, s0, s1, dcf_amd.BoundState.LtBeta, cwb)
+    d.eval_multikey_device(False, cwb, s0, xs, P, y0)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
+    b0 = prg.last_eval_blocks()
+    wall, step_s = timed_loop(step, args.steps, args.warmup, world)
+    b1 = prg.last_eval_blocks()
+    # per-phase HIP-event times over the same number of steps (separate loop: events between phases)
     for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
-    evals = 2 * K * P * world * args.steps
-    return {"metric": "C5 batched gen + eval (both parties)", "value": evals / wall, "unit": "evals/s",
-            "keys_per_s": K * world * args.steps / wall, "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"C5: {K} keys x {P} points per GPU, N={nb}, lambda={lam}"}}
+        step(record=True)
+        torch.cuda.synchronize()
+        for i in range(3):
+            phase[i] += ev[i].elapsed_time(ev[i + 1]) / 1e3 / args.steps
+    evals = 2 * global_keys * P * args.steps
+    gen_blocks = 4 * 8 * nb * K                  # k_gen16: A and B of both parties' PRG per level
+    eval_blocks = b0 + b1                        # multi-key stream engine, counted on the device
+    n = 8 * nb
+    cwb_b = dcf_amd.cwb_bytes(nb, lam, K)
+    dig_b = K * n * 33                           # key-major digest (k_cw_keymajor): 32 B CW + 1 B t per level
+    key_bytes = cwb_b + 2 * (cwb_b + 2 * dig_b)  # gen writes CWB; per eval: digest reads CWB, writes + reads digest
+    io_bytes = K * (nb + 3 * lam) + 2 * K * P * (nb + lam)
+    alg_bytes = key_bytes + io_bytes
+    peak = PEAK_TT_BLOCKS
+    achieved = (gen_blocks + eval_blocks) / step_s
+    eval_s = phase[1] + phase[2]
+    traffic, traffic_src = traffic_fields("k_gen16+k_cw_keymajor+k_eval16_stream<MULTI>", K * P, nb, lam, 0, alg_bytes)
+    out = {"metric": "C5 batched gen + eval (both parties)", "value": evals / wall, "unit": "evals/s",
+           "keys_per_s": global_keys * args.steps / wall, "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+           "scaling": args.scaling, "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+           "aes_blocks_per_s": evals / wall * blocks_per_eval(nb, lam) + global_keys * args.steps / wall * 4 * n,
+           "config": {"workload": f"C5: {global_keys} keys x {P} points ({K} keys on this GPU), N={nb}, "
+                                  f"lambda={lam}, batched gen + multi-key eval of both parties per step",
+                      "n_bytes": nb, "lambda": lam, "keys_per_gpu": K, "points_per_key": P},
+           "phases_ms": {"gen": phase[0] * 1e3, "eval_party0": phase[1] * 1e3, "eval_party1": phase[2] * 1e3,
+                         "note": "HIP events on the launch stream; each eval includes its key-major CW digest "
+                                 "(k_cw_keymajor) — profiles/ has the per-kernel split"},
+           "key_traffic_GBps": key_bytes / step_s / 1e9,
+           "roofline": {"bound": "lds", "kernel": "k_gen16 + k_cw_keymajor + k_eval16_stream<MULTI> (whole step)",
+                        "engine": "stream (multi-key)", "achieved": achieved / 1e9, "peak": peak / 1e9,
+                        "unit": "G AES-256 blocks/s", "frac": achieved / peak,
+                        "eval_only": {"achieved": eval_blocks / eval_s / 1e9, "frac": eval_blocks / eval_s / peak,
+                                      "executed_blocks_per_eval": eval_blocks / (2 * K * P)},
+                        "gen_only": {"achieved": gen_blocks / phase[0] / 1e9, "frac": gen_blocks / phase[0] / peak},
+                        "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": alg_bytes,
+                        "kernel_ms": step_s * 1e3, "hbm_GBps": alg_bytes / step_s / 1e9,
+                        "executed_blocks_per_step": gen_blocks + eval_blocks,
+                        "note": "gen: 4 AES-256 blocks per level per key (k_gen16); eval: blocks the multi-key "
+                                "stream engine encrypts, counted on the device (B every level, A on left levels, "
+                                "minus reused B); peak = T-table LDS bound 87.8 G blocks/s"}}
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = c5_cpu_baseline(keys, nb, lam, alpha, beta, s0, s1, xs, cwb, y0, y1, K, P,
+                                              args.cpu_seconds)
+    return out
+
+
+def c5_cpu_baseline(keys, nb, lam, alpha, beta, s0, s1, xs, cwb, y0, y1, K, P, target_s):
+    """Oracle gen + eval of both parties for a bounded sample of C5's keys, keys spread over
+    host threads (ctypes releases the GIL), checked against the GPU's CWB and outputs."""
+    from oracle import oracle as O
+    threads = host_threads()
+    Po = O.OraclePrg(keys, lam)
+    A, B, S0, S1 = (t.cpu().numpy() for t in (alpha, beta, s0, s1))
+    cw = cwb.cpu().numpy().tobytes()
+
+    def work(ids):
+        ok_all = True
+        for key in ids:
+            ok = O.gen(Po, A[key].tobytes(), B[key].tobytes(), S0[key].tobytes(), S1[key].tobytes(), 0)
+            xk = X[key * P:(key + 1) * P]
+            ya = O.eval_(Po, 0, ok, S0[key].tobytes(), xk)
+            yb = O.eval_(Po, 1, ok, S1[key].tobytes(), xk)
+            if check:
+                kk = oracle_key(cw, nb, lam, K, int(key))
+                ok_all = ok_all and np.array_equal(kk.cw_s, ok.cw_s) and np.array_equal(kk.cw_v, ok.cw_v) \
+                    and np.array_equal(ya, Y0[key * P:(key + 1) * P]) and np.array_equal(yb, Y1[key * P:(key + 1) * P])
+        return ok_all
+
+    def run(nkeys):
+        ids = np.arange(nkeys)
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            res = list(ex.map(work, np.array_split(ids, threads)))
+        return time.perf_counter() - t0, all(res)
+
+    ncal = min(K, 64 * threads)
+    X = xs[:ncal * P].cpu().numpy()
+    Y0, Y1 = y0[:ncal * P].cpu().numpy(), y1[:ncal * P].cpu().numpy()
+    check = True
+    dt, ok = run(ncal)
+    nk = int(min(K, max(ncal, ncal / dt * target_s)))
+    X = xs[:nk * P].cpu().numpy()
+    Y0, Y1 = y0[:nk * P].cpu().numpy(), y1[:nk * P].cpu().numpy()
+    check = False
+    dt, _ = run(nk)
+    return {"value": 2 * nk * P / dt, "unit": "evals/s", "keys_per_s": nk / dt, "cores": threads, "kind": "port",
+            "sample": f"gen + eval of both parties (64 points each) for the first {nk} keys, keys split over "
+                      f"{threads} threads; C restatement of lib.rs:86-204 + prg.rs:42-73 with AES-NI; {dt:.1f} s",
+            "matches_gpu": ok}
 
 
 def run_fd(args, world, rank):
@@ -500,7 +674,14 @@ def main():
     ap.add_argument("--shy-mask", default=None, help="stream-hybrid (eval mode 5): stream-wave mask, e.g. 0x7777")
     ap.add_argument("--shy-prio", type=int, default=0, help="stream-hybrid: 1 = stream waves at raised priority")
     ap.add_argument("--hybrid-mem", type=int, default=1, help="hybrid: 1 = 16 waves + scratch slabs, 0 = 12 waves")
+    ap.add_argument("--scaling", default=None, choices=["strong", "weak"],
+                    help="strong: the workload's points (C5: keys) are split over the ranks (default for c3, c5); "
+                         "weak: every rank gets the full count (default otherwise)")
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time dcf_eval on host buffers (PCIe included; always on for c1)")
     args = ap.parse_args()
+    if args.scaling is None:
+        args.scaling = "strong" if args.workload in ("c3", "c5") else "weak"
     args.lam = 16
     if args.workload == "c1":    # benches/dcf_batch_eval.rs:17 shape
         args.n_bytes = args.n_bytes or 16

@@ -13,14 +13,16 @@ from .dcf import (  # noqa: F401
     CmpFn,
     Cw,
     DcfImpl,
+    MultiGpuDcf,
     Share,
     cwb_bytes,
     cwb_np1_offset,
     cwb_to_share,
+    point_slice,
     share_to_cwb,
 )
 
 __all__ = [
-    "Aes128MatyasMeyerOseasPrg", "Aes256HirosePrg", "BoundState", "CmpFn", "Cw", "DcfImpl", "Share", "DcfError",
+    "Aes128MatyasMeyerOseasPrg", "Aes256HirosePrg", "BoundState", "CmpFn", "Cw", "DcfImpl", "MultiGpuDcf", "Share", "point_slice", "DcfError",
     "cwb_bytes", "cwb_np1_offset", "cwb_to_share", "share_to_cwb", "load", "LIB_PATH",
 ]

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <utility>
 #include <vector>
@@ -52,10 +53,15 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// On failure the runtime's per-thread last error is cleared as well, so a later call on
+// this thread does not report a stale error (e.g. an OOM) from its own launch check.
 #define HIP_TRY(expr)                                                                   \
   do {                                                                                  \
     hipError_t e_ = (expr);                                                             \
-    if (e_ != hipSuccess) return fail(DCF_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    if (e_ != hipSuccess) {                                                             \
+      (void)hipGetLastError();                                                          \
+      return fail(DCF_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_));        \
+    }                                                                                   \
   } while (0)
 
 struct DeviceGuard {
@@ -119,10 +125,23 @@ struct dcf_prg {
   int hybrid_mem = 1;         // 1: 16-wave workgroups with s/v slabs; 0: 12 waves, s/v in registers
   uint32_t shy_mask = 0x7777; // stream-hybrid: stream waves (bit w = wave w); 0x7777 = one SIMD bitsliced
   int shy_prio = 0;           // stream-hybrid: raise the stream waves' issue priority
+  std::vector<uint8_t> key_blob;  // the PRG keys as given (multi-GPU calls check every prg holds the same)
+  // Host-pointer entry points (dcf_gen / dcf_eval / dcf_prg_gen / dcf_eval_multi_gpu): three
+  // prg-owned non-blocking streams (copy-in, compute, copy-out), their events, and staging
+  // pooled across calls (pinned host + device), so a call never synchronizes the device.
+  hipStream_t hs[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t hev[6] = {};     // in[2], kernel[2], out[2] (double-buffered chunks)
+  uint8_t* h_stage = nullptr; // pinned
+  size_t h_stage_bytes = 0;
+  uint8_t* d_stage = nullptr;
+  size_t d_stage_bytes = 0;
+  uint8_t* d_mkey = nullptr;  // dcf_eval_multi_gpu_device: this device's copy of the key (CWB + s0)
+  size_t mkey_bytes = 0;
 };
 
 namespace {
 
+constexpr int kPrefixNoMem = -100;            // build_prefix: table allocation failed (internal)
 constexpr uint64_t kWideChunk = 1ull << 22;   // points per head/tail pass (t-vector scratch 256 MiB)
 constexpr uint64_t kGenChunk = 4096;          // keys per wide-gen launch (scratch 3*LAMBDA per key)
 constexpr uint32_t kTailPts = 4096;          // points per tail workgroup (one table build each)
@@ -143,9 +162,12 @@ int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
 // Shared-prefix depth for a single-key stream eval of `total` points (kernels_stream.h
 // PrefixTable): the top tree has 2^D nodes (33 B each, built with 2^(D+1) AES blocks)
 // and saves every point D levels.  Auto: D = log2(total) - 1 (table build < 1 block per
-// point), at most 24 (a 553 MB table), none below 8, always < 8N.  Measured (r01i,
-// C2: 2^24 points, N = 4): D = 12 / 16 / 20 / 24 -> 2.00 / 2.29 / 2.62 / 2.83 G evals/s
-// (1.44 without); C3 (2^28, N = 16): D = 16 / 24 -> 450 / 477 M (397 M without).
+// point), at most kPrefixMax = 26 (a 2.2 GB table of 32-B rows inside 4.4 GB of build
+// buffers, 2 x 2^26 x 33 B), none below 8, always < 8N.  If the buffers cannot be
+// allocated in auto mode, eval retries 2 levels shallower down to 8, then runs without a
+// table (identical bytes; see try_prefix).  Measured (r01i, C2: 2^24 points, N = 4):
+// D = 12 / 16 / 20 / 24 -> 2.00 / 2.29 / 2.62 / 2.83 G evals/s (1.44 without);
+// C3 (2^28, N = 16): D = 16 / 24 / 26 -> 450 / 477 / ~482 M (397 M without; r01q/r).
 constexpr uint32_t kPrefixMax = 26;       // auto (C3 r01q sweep: 24 519, 25 521, 26 524, 27 524 M evals/s)
 constexpr uint32_t kPrefixMaxForced = 28;  // dcf_prg_set_prefix_levels (2^28 x 33 B x 2 = 17.7 GB)
 uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
@@ -238,7 +260,12 @@ int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const 
       p->d_pfx = nullptr;
       p->pfx_bytes = 0;
     }
-    HIP_TRY(hipMalloc(&p->d_pfx, need));
+    const hipError_t e = hipMalloc(&p->d_pfx, need);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      p->d_pfx = nullptr;
+      return fail(kPrefixNoMem, std::string("prefix table: hipMalloc: ") + hipGetErrorString(e));
+    }
     p->pfx_bytes = need;
   }
   uint4* s_a = (uint4*)p->d_pfx;
@@ -272,6 +299,21 @@ int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const 
                      st, s_a, v_a, t_a, maxnodes, s_b);
   HIP_TRY(hipGetLastError());
   *out = PrefixTable{s_b, levels};
+  return DCF_OK;
+}
+
+// build_prefix at depth d; in auto mode (prefix_levels < 0) an allocation failure retries
+// two levels shallower, down to 8, and then evaluates without a table (same output bytes).
+int try_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const uint4* cwv, const uint8_t* cwt,
+               const uint4* np1, const uint8_t* s0, uint32_t d, PrefixTable* out, hipStream_t st) {
+  *out = PrefixTable{nullptr, 0u};
+  while (d) {
+    const int rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0, d, out, st);
+    if (rc != kPrefixNoMem) return rc;
+    if (p->prefix_levels >= 0) return fail(DCF_ERR_HIP, t_err);  // a forced depth must fit
+    d = d >= 10u ? d - 2u : 0u;
+  }
+  *out = PrefixTable{nullptr, 0u};
   return DCF_OK;
 }
 
@@ -406,6 +448,7 @@ int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int 
   p->cipher_n = cipher_n;
   p->rk.resize(cipher_n);
   for (size_t i = 0; i < cipher_n; i++) aes256_expand_words(keys + 32 * i, &p->rk[i]);
+  p->key_blob.assign(keys, keys + 32 * cipher_n);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     p->cus = prop.multiProcessorCount;
@@ -446,6 +489,7 @@ int dcf_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int dev
   p->lambda = lambda;
   p->cipher_n = cipher_n;
   p->eval_mode = DCF_EVAL_TTABLE;
+  p->key_blob.assign(keys, keys + 16 * cipher_n);
   std::vector<uint32_t> w(4 * 44);
   for (size_t i = 0; i < 4; i++) aes128_expand_words(keys + 16 * i, w.data() + 44 * i);
   hipDeviceProp_t prop;
@@ -469,6 +513,8 @@ void dcf_prg_free(dcf_prg* p) {
   if (!p) return;
   {
     DeviceGuard dg(p->device);
+    for (hipStream_t s : p->hs)  // host-path work still queued (an error return drains these too)
+      if (s) (void)hipStreamSynchronize(s);
     if (p->d_tab) (void)hipFree(p->d_tab);
     if (p->d_km) (void)hipFree(p->d_km);
     if (p->d_rk128) (void)hipFree(p->d_rk128);
@@ -480,6 +526,13 @@ void dcf_prg_free(dcf_prg* p) {
     if (p->d_ctr) (void)hipFree(p->d_ctr);
     if (p->d_pfx) (void)hipFree(p->d_pfx);
     if (p->d_slabs) (void)hipFree(p->d_slabs);
+    for (hipStream_t s : p->hs)
+      if (s) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : p->hev)
+      if (e) (void)hipEventDestroy(e);
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
+    if (p->d_stage) (void)hipFree(p->d_stage);
+    if (p->d_mkey) (void)hipFree(p->d_mkey);
   }
   delete p;
 }
@@ -642,7 +695,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     if (num_keys == 1 && (p->prefix_levels > 0 || total >= (uint64_t)p->cus * kBlock * 2)) {
       const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
       if (d) {
-        int rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+        int rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
         if (rc) return rc;
       }
     }
@@ -739,7 +792,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     PrefixTable pf{nullptr, 0u};
     const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
     if (d) {
-      rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+      rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
       if (rc) return rc;
     }
     HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
@@ -785,7 +838,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     if (!multi) {
       const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
       if (d) {
-        int rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+        int rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
         if (rc) return rc;
       }
     }
@@ -845,6 +898,163 @@ int dcf_eval_multikey_device(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t
                              const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys,
                              void* stream) {
   return eval_launch(p, n_bytes, num_keys, points_per_key, party, cwb, s0s, xs, ys, stream);
+}
+
+// ---- host-pointer path: prg-owned streams, pooled staging, chunked pipeline ----
+
+static size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+// Points per chunk of the host eval pipeline: ~128 MiB of x + y per buffer (C3 shape: 4 Mi
+// points, an 8 ms kernel against ~3 ms of PCIe each way, so the copies hide behind it).
+constexpr size_t kHostChunkBytes = 128ull << 20;
+
+static int ensure_host_path(dcf_prg* p) {
+  if (p->hs[0]) return DCF_OK;
+  hipStream_t hs[3] = {nullptr, nullptr, nullptr};
+  for (auto& s : hs) HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  for (auto& e : p->hev)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (int i = 0; i < 3; ++i) p->hs[i] = hs[i];
+  return DCF_OK;
+}
+
+static int ensure_stage(dcf_prg* p, size_t hbytes, size_t dbytes) {
+  if (p->h_stage_bytes < hbytes) {
+    if (p->h_stage) HIP_TRY(hipHostFree(p->h_stage));
+    p->h_stage = nullptr;
+    p->h_stage_bytes = 0;
+    HIP_TRY(hipHostMalloc((void**)&p->h_stage, hbytes, hipHostMallocDefault));
+    p->h_stage_bytes = hbytes;
+  }
+  if (p->d_stage_bytes < dbytes) {
+    if (p->d_stage) HIP_TRY(hipFree(p->d_stage));
+    p->d_stage = nullptr;
+    p->d_stage_bytes = 0;
+    HIP_TRY(hipMalloc(&p->d_stage, dbytes));
+    p->d_stage_bytes = dbytes;
+  }
+  return DCF_OK;
+}
+
+// Every host entry point ends here: wait for the prg's own streams only (never the whole
+// device), also after an error, so no queued copy still targets the staging buffers.
+static int host_finish(dcf_prg* p, int rc) {
+  for (hipStream_t s : p->hs) {
+    if (!s) continue;
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess && rc == DCF_OK) {
+      (void)hipGetLastError();
+      rc = fail(DCF_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+    }
+  }
+  return rc;
+}
+
+// Dcf::eval over host buffers (caller: DeviceGuard held, arguments checked, m > 0).  Chunks
+// of `chunk` points flow through two staging slots on three streams: copy-in (pinned ->
+// device), compute (eval_launch), copy-out (device -> pinned); the host copies chunk c's x
+// into pinned memory and chunk c-1's y out of it while the GPU works on chunk c, so PCIe
+// transfers overlap the kernels of neighbouring chunks.  The GPU never touches caller memory.
+static int host_eval(dcf_prg* p, size_t nb, int party, const uint8_t* cwb, size_t cwb_len, const uint8_t* s0,
+                     const uint8_t* xs, uint64_t m, uint8_t* ys) {
+  const size_t lam = p->lambda;
+  if (int rc = ensure_host_path(p)) return rc;
+  const uint64_t chunk = std::min<uint64_t>(m, std::max<uint64_t>(256, kHostChunkBytes / (nb + lam)));
+  const int nbuf = m > chunk ? 2 : 1;
+  const size_t kb = align256(cwb_len) + align256(lam);
+  const size_t xb = align256(chunk * nb), yb = align256(chunk * lam);
+  if (int rc = ensure_stage(p, nbuf * (xb + yb), kb + nbuf * (xb + yb))) return rc;
+  uint8_t* dk = p->d_stage;
+  uint8_t* ds0 = dk + align256(cwb_len);
+  uint8_t *dx[2], *dy[2], *hx[2], *hy[2];
+  for (int b = 0; b < nbuf; ++b) {
+    dx[b] = dk + kb + b * xb;
+    dy[b] = dk + kb + nbuf * xb + b * yb;
+    hx[b] = p->h_stage + b * xb;
+    hy[b] = p->h_stage + nbuf * xb + b * yb;
+  }
+  hipStream_t si = p->hs[0], sc = p->hs[1], so = p->hs[2];
+  hipEvent_t *ev_in = p->hev, *ev_k = p->hev + 2, *ev_out = p->hev + 4;
+  HIP_TRY(hipMemcpyAsync(dk, cwb, cwb_len, hipMemcpyHostToDevice, sc));
+  HIP_TRY(hipMemcpyAsync(ds0, s0, lam, hipMemcpyHostToDevice, sc));
+  const uint64_t nch = (m + chunk - 1) / chunk;
+  for (uint64_t c = 0; c <= nch; ++c) {
+    if (c < nch) {
+      const int b = (int)(c & (nbuf - 1));
+      const uint64_t off = c * chunk, cnt = std::min<uint64_t>(chunk, m - off);
+      if (c >= 2) HIP_TRY(hipEventSynchronize(ev_in[b]));  // chunk c-2's H2D has read hx[b]
+      memcpy(hx[b], xs + off * nb, cnt * nb);
+      if (c >= 2) HIP_TRY(hipStreamWaitEvent(si, ev_k[b], 0));  // chunk c-2's kernel is done with dx[b]
+      HIP_TRY(hipMemcpyAsync(dx[b], hx[b], cnt * nb, hipMemcpyHostToDevice, si));
+      HIP_TRY(hipEventRecord(ev_in[b], si));
+      HIP_TRY(hipStreamWaitEvent(sc, ev_in[b], 0));
+      if (c >= 2) HIP_TRY(hipStreamWaitEvent(sc, ev_out[b], 0));  // chunk c-2's D2H is done with dy[b]
+      if (int rc = eval_launch(p, nb, 1, cnt, party, dk, ds0, dx[b], dy[b], sc)) return rc;
+      HIP_TRY(hipEventRecord(ev_k[b], sc));
+      HIP_TRY(hipStreamWaitEvent(so, ev_k[b], 0));
+      HIP_TRY(hipMemcpyAsync(hy[b], dy[b], cnt * lam, hipMemcpyDeviceToHost, so));
+      HIP_TRY(hipEventRecord(ev_out[b], so));
+    }
+    if (c >= 1) {  // drain chunk c-1 while chunk c is in flight
+      const uint64_t pc = c - 1;
+      const int b = (int)(pc & (nbuf - 1));
+      const uint64_t off = pc * chunk, cnt = std::min<uint64_t>(chunk, m - off);
+      HIP_TRY(hipEventSynchronize(ev_out[b]));
+      memcpy(ys + off * lam, hy[b], cnt * lam);
+    }
+  }
+  return DCF_OK;
+}
+
+// Dcf::gen for one key over host buffers, on the prg's compute stream.
+static int host_gen(dcf_prg* p, size_t nb, const uint8_t* alpha, const uint8_t* beta, const uint8_t* s0_0,
+                    const uint8_t* s0_1, int bound, uint8_t* cwb_out) {
+  const size_t lam = p->lambda, cwb_len = dcf_cwb_bytes(nb, lam, 1);
+  if (int rc = ensure_host_path(p)) return rc;
+  const size_t oa = 0, ob = align256(nb), o0 = ob + align256(lam), o1 = o0 + align256(lam), ok = o1 + align256(lam);
+  const size_t total = ok + align256(cwb_len);
+  if (int rc = ensure_stage(p, total, total)) return rc;
+  uint8_t *h = p->h_stage, *d = p->d_stage;
+  memcpy(h + oa, alpha, nb);
+  memcpy(h + ob, beta, lam);
+  memcpy(h + o0, s0_0, lam);
+  memcpy(h + o1, s0_1, lam);
+  hipStream_t sc = p->hs[1];
+  HIP_TRY(hipMemcpyAsync(d, h, ok, hipMemcpyHostToDevice, sc));
+  HIP_TRY(hipMemsetAsync(d + ok, 0, cwb_len, sc));
+  int rc = dcf_gen_batch_device(p, nb, 1, d + oa, d + ob, d + o0, d + o1, bound, d + ok, sc);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(h + ok, d + ok, cwb_len, hipMemcpyDeviceToHost, sc));
+  HIP_TRY(hipStreamSynchronize(sc));
+  memcpy(cwb_out, h + ok, cwb_len);
+  return DCF_OK;
+}
+
+// Prg::gen for m seeds over host buffers (test hook), on the prg's compute stream.
+static int host_prg_gen(dcf_prg* p, const uint8_t* seeds, size_t m, uint8_t* out) {
+  const size_t lam = p->lambda, row = 4 * lam + 2;
+  if (int rc = ensure_host_path(p)) return rc;
+  const size_t so = align256(m * lam), total = so + align256(m * row);
+  if (int rc = ensure_stage(p, total, total)) return rc;
+  uint8_t *h = p->h_stage, *d = p->d_stage;
+  hipStream_t sc = p->hs[1];
+  memcpy(h, seeds, m * lam);
+  HIP_TRY(hipMemcpyAsync(d, h, m * lam, hipMemcpyHostToDevice, sc));
+  if (p->kind == 1)
+    hipLaunchKernelGGL(k_prg16_mmo, dim3((unsigned)grid_for(m, p->cus)), dim3(kBlock), 0, sc, p->d_tab, p->d_rk128,
+                       (const uint4*)d, (uint64_t)m, d + so);
+  else if (lam == 16)
+    hipLaunchKernelGGL(k_prg16, dim3((unsigned)grid_for(m, p->cus)), dim3(kBlock), 0, sc, p->d_tab, p->rk[0],
+                       (const uint4*)d, (uint64_t)m, d + so);
+  else
+    hipLaunchKernelGGL(k_prg_wide, dim3((unsigned)std::min<uint64_t>((m * (lam / 16) + 255) / 256, 65535)),
+                       dim3(256), 0, sc, p->d_tab, p->rk[0], p->rk[17], (const uint8_t*)d, (uint64_t)m, (uint32_t)lam,
+                       d + so);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(h + so, d + so, m * row, hipMemcpyDeviceToHost, sc));
+  HIP_TRY(hipStreamSynchronize(sc));
+  memcpy(out, h + so, m * row);
+  return DCF_OK;
 }
 
 // ---- serde / bincode wire format of Share (lib.rs:217-340) ----
@@ -966,7 +1176,7 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   const size_t ctr_off = (2 * maxnodes * nodeb + 64 + 255) & ~(size_t)255;
   int rc = ensure_ws(p, ctr_off + 64 * sizeof(uint32_t), st);
   if (rc) return rc;
-  if (fused && (rc = ensure_rk0(p))) return rc;
+  if (DCF_FD_GK && fused && (rc = ensure_rk0(p))) return rc;  // the tail reads it only with DCF_FD_GK
   uint8_t* w = p->d_ws;
   uint32_t* ctrs = (uint32_t*)(w + ctr_off);
   HIP_TRY(hipMemsetAsync(ctrs, 0, 64 * sizeof(uint32_t), st));
@@ -1002,7 +1212,7 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   if (fused) {
     const uint64_t nodes = 1ull << lev_end;
     hipLaunchKernelGGL(k_fd_tail16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
-                       p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63, p->d_rk0);
+                       p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63, DCF_FD_GK ? p->d_rk0 : nullptr);
     HIP_TRY(hipGetLastError());
   }
   return DCF_OK;
@@ -1012,31 +1222,18 @@ int dcf_gen(dcf_prg* p, size_t n_bytes, const uint8_t* alpha, const uint8_t* bet
             const uint8_t* s0_1, int bound, uint8_t* cwb_out) {
   if (!p || !alpha || !beta || !s0_0 || !s0_1 || !cwb_out) return fail(DCF_ERR_ARG, "null argument");
   if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
-  const size_t lam = p->lambda, cwb_len = dcf_cwb_bytes(n_bytes, lam, 1);
+  if (bound != DCF_BOUND_LT_BETA && bound != DCF_BOUND_GT_BETA) return fail(DCF_ERR_ARG, "bad bound");
   DeviceGuard dg(p->device);
-  DevBuf a, b, s0, s1, out;
-  HIP_TRY(a.alloc(n_bytes));
-  HIP_TRY(b.alloc(lam));
-  HIP_TRY(s0.alloc(lam));
-  HIP_TRY(s1.alloc(lam));
-  HIP_TRY(out.alloc(cwb_len));
-  HIP_TRY(hipMemcpy(a.p, alpha, n_bytes, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(b.p, beta, lam, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s0.p, s0_0, lam, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s1.p, s0_1, lam, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(out.p, 0, cwb_len));
-  int rc = dcf_gen_batch_device(p, n_bytes, 1, (const uint8_t*)a.p, (const uint8_t*)b.p, (const uint8_t*)s0.p,
-                                (const uint8_t*)s1.p, bound, (uint8_t*)out.p, nullptr);
-  if (rc) return rc;
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(cwb_out, out.p, cwb_len, hipMemcpyDeviceToHost));
-  return DCF_OK;
+  if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
+  int rc = host_gen(p, n_bytes, alpha, beta, s0_0, s0_1, bound, cwb_out);
+  return host_finish(p, rc);
 }
 
 int dcf_eval(dcf_prg* p, size_t n_bytes, int party, const uint8_t* cwb, size_t cwb_len, const uint8_t* s0,
              const uint8_t* xs, size_t m, uint8_t* ys, size_t ys_len) {
   if (!p || !cwb || !s0) return fail(DCF_ERR_ARG, "null argument");
   if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
+  if (party != 0 && party != 1) return fail(DCF_ERR_ARG, "party must be 0 or 1");
   const size_t lam = p->lambda;
   if (cwb_len != dcf_cwb_bytes(n_bytes, lam, 1))
     return fail(DCF_ERR_KEY, "key size does not match 8*N levels (lib.rs:165)");
@@ -1044,20 +1241,9 @@ int dcf_eval(dcf_prg* p, size_t n_bytes, int party, const uint8_t* cwb, size_t c
   if (m == 0) return DCF_OK;
   if (!xs || !ys) return fail(DCF_ERR_ARG, "null buffer");
   DeviceGuard dg(p->device);
-  DevBuf k, s, x, y;
-  HIP_TRY(k.alloc(cwb_len));
-  HIP_TRY(s.alloc(lam));
-  HIP_TRY(x.alloc(m * n_bytes));
-  HIP_TRY(y.alloc(m * lam));
-  HIP_TRY(hipMemcpy(k.p, cwb, cwb_len, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s.p, s0, lam, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(x.p, xs, m * n_bytes, hipMemcpyHostToDevice));
-  int rc = dcf_eval_device(p, n_bytes, party, (const uint8_t*)k.p, (const uint8_t*)s.p, (const uint8_t*)x.p, m,
-                           (uint8_t*)y.p, nullptr);
-  if (rc) return rc;
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(ys, y.p, m * lam, hipMemcpyDeviceToHost));
-  return DCF_OK;
+  if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
+  int rc = host_eval(p, n_bytes, party, cwb, cwb_len, s0, xs, m, ys);
+  return host_finish(p, rc);
 }
 
 int dcf_prg_gen(dcf_prg* p, const uint8_t* seeds, size_t m, uint8_t* out) {
@@ -1065,26 +1251,125 @@ int dcf_prg_gen(dcf_prg* p, const uint8_t* seeds, size_t m, uint8_t* out) {
   if (m == 0) return DCF_OK;
   if (!seeds || !out) return fail(DCF_ERR_ARG, "null buffer");
   DeviceGuard dg(p->device);
-  const size_t lam = p->lambda, row = 4 * lam + 2;
-  DevBuf s, o;
-  HIP_TRY(s.alloc(m * lam));
-  HIP_TRY(o.alloc(m * row));
-  HIP_TRY(hipMemcpy(s.p, seeds, m * lam, hipMemcpyHostToDevice));
-  if (p->kind == 1)
-    hipLaunchKernelGGL(k_prg16_mmo, dim3((unsigned)grid_for(m, p->cus)), dim3(kBlock), 0, nullptr, p->d_tab,
-                       p->d_rk128, (const uint4*)s.p, (uint64_t)m, (uint8_t*)o.p);
-  else if (lam == 16)
-    hipLaunchKernelGGL(k_prg16, dim3((unsigned)grid_for(m, p->cus)), dim3(kBlock), 0, nullptr, p->d_tab, p->rk[0],
-                       (const uint4*)s.p, (uint64_t)m, (uint8_t*)o.p);
-  else
-    hipLaunchKernelGGL(k_prg_wide, dim3((unsigned)((m * (lam / 16) + 255) / 256 < 65535 ? (m * (lam / 16) + 255) / 256
-                                                                                      : 65535)),
-                       dim3(256), 0, nullptr, p->d_tab, p->rk[0], p->rk[17], (const uint8_t*)s.p, (uint64_t)m,
-                       (uint32_t)lam, (uint8_t*)o.p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, o.p, m * row, hipMemcpyDeviceToHost));
+  if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
+  int rc = host_prg_gen(p, seeds, m, out);
+  return host_finish(p, rc);
+}
+
+// ---- multi-GPU (SURVEY §8(b) dcf_eval_multi_gpu; the reference spreads Dcf::eval over
+// every host core inside one call, lib.rs:194-199) ----
+
+static int check_group(dcf_prg* const* prgs, size_t G) {
+  if (!prgs || G == 0) return fail(DCF_ERR_ARG, "prgs must hold at least one dcf_prg");
+  for (size_t g = 0; g < G; ++g) {
+    if (!prgs[g]) return fail(DCF_ERR_ARG, "null dcf_prg in prgs");
+    for (size_t h = 0; h < g; ++h)
+      if (prgs[h] == prgs[g]) return fail(DCF_ERR_ARG, "a dcf_prg appears twice in prgs (one thread per prg)");
+    if (prgs[g]->kind != prgs[0]->kind || prgs[g]->lambda != prgs[0]->lambda ||
+        prgs[g]->key_blob != prgs[0]->key_blob)
+      return fail(DCF_ERR_ARG, "prgs disagree on the PRG (kind, lambda or keys)");
+  }
   return DCF_OK;
+}
+
+int dcf_eval_multi_gpu(dcf_prg* const* prgs, size_t G, size_t n_bytes, int party, const uint8_t* cwb,
+                       size_t cwb_len, const uint8_t* s0, const uint8_t* xs, size_t m, uint8_t* ys, size_t ys_len) {
+  if (int rc = check_group(prgs, G)) return rc;
+  if (!cwb || !s0) return fail(DCF_ERR_ARG, "null argument");
+  if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
+  if (party != 0 && party != 1) return fail(DCF_ERR_ARG, "party must be 0 or 1");
+  const size_t lam = prgs[0]->lambda;
+  if (cwb_len != dcf_cwb_bytes(n_bytes, lam, 1))
+    return fail(DCF_ERR_KEY, "key size does not match 8*N levels (lib.rs:165)");
+  if (ys_len != m * lam) return fail(DCF_ERR_LEN, "ys length != m * lambda");
+  if (m == 0) return DCF_OK;
+  if (!xs || !ys) return fail(DCF_ERR_ARG, "null buffer");
+  std::vector<int> rcs(G, DCF_OK);
+  std::vector<std::string> errs(G);
+  auto run = [&](size_t g) {
+    size_t start, cnt;
+    dcf_point_slice(m, G, g, &start, &cnt);
+    if (cnt == 0) return;
+    DeviceGuard dg(prgs[g]->device);
+    if (!dg.ok) {
+      rcs[g] = fail(DCF_ERR_HIP, "hipSetDevice failed");
+    } else {
+      rcs[g] = host_finish(prgs[g], host_eval(prgs[g], n_bytes, party, cwb, cwb_len, s0, xs + start * n_bytes, cnt,
+                                              ys + start * lam));
+    }
+    if (rcs[g]) errs[g] = t_err;
+  };
+  std::vector<std::thread> th;
+  for (size_t g = 1; g < G; ++g) th.emplace_back(run, g);
+  run(0);
+  for (auto& t : th) t.join();
+  for (size_t g = 0; g < G; ++g)
+    if (rcs[g]) return fail(rcs[g], "device slice " + std::to_string(g) + ": " + errs[g]);
+  return DCF_OK;
+}
+
+int dcf_eval_multi_gpu_device(dcf_prg* const* prgs, size_t G, size_t n_bytes, int party, const uint8_t* cwb,
+                              size_t cwb_len, const uint8_t* s0, const uint8_t* const* xs, const size_t* ms,
+                              uint8_t* const* ys, void* const* streams, uint8_t* gather_ys) {
+  if (int rc = check_group(prgs, G)) return rc;
+  if (!cwb || !s0 || !xs || !ms || !ys) return fail(DCF_ERR_ARG, "null argument");
+  if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
+  if (party != 0 && party != 1) return fail(DCF_ERR_ARG, "party must be 0 or 1");
+  const size_t lam = prgs[0]->lambda;
+  if (cwb_len != dcf_cwb_bytes(n_bytes, lam, 1))
+    return fail(DCF_ERR_KEY, "key size does not match 8*N levels (lib.rs:165)");
+  const int dev0 = prgs[0]->device;
+  size_t off = 0;
+  for (size_t g = 0; g < G; ++g) {
+    dcf_prg* p = prgs[g];
+    hipStream_t st = streams ? (hipStream_t)streams[g] : nullptr;
+    DeviceGuard dg(p->device);
+    if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
+    // the key to this device, once per call (4.2 KB at N = LAMBDA = 16): the "broadcast"
+    const size_t kb = align256(cwb_len) + align256(lam);
+    if (p->mkey_bytes < kb) {
+      if (p->d_mkey) {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipFree(p->d_mkey));
+        p->d_mkey = nullptr;
+        p->mkey_bytes = 0;
+      }
+      HIP_TRY(hipMalloc(&p->d_mkey, kb));
+      p->mkey_bytes = kb;
+    }
+    HIP_TRY(hipMemcpyAsync(p->d_mkey, cwb, cwb_len, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(p->d_mkey + align256(cwb_len), s0, lam, hipMemcpyHostToDevice, st));
+    if (ms[g]) {
+      if (!xs[g] || !ys[g]) return fail(DCF_ERR_ARG, "null slice buffer");
+      int rc = eval_launch(p, n_bytes, 1, ms[g], party, p->d_mkey, p->d_mkey + align256(cwb_len), xs[g], ys[g], st);
+      if (rc) return rc;
+      if (gather_ys) {  // slice g -> its rows of the gather buffer on prgs[0]'s device, over xGMI
+        if (p->device != dev0) {
+          const hipError_t e = hipDeviceEnablePeerAccess(dev0, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+            return fail(DCF_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+          (void)hipGetLastError();
+          HIP_TRY(hipMemcpyPeerAsync(gather_ys + off * lam, dev0, ys[g], p->device, ms[g] * lam, st));
+        } else {
+          HIP_TRY(hipMemcpyAsync(gather_ys + off * lam, ys[g], ms[g] * lam, hipMemcpyDeviceToDevice, st));
+        }
+      }
+    }
+    off += ms[g];
+  }
+  return DCF_OK;
+}
+
+void dcf_point_slice(size_t total, size_t G, size_t g, size_t* start, size_t* count) {
+  if (!start || !count) return;
+  if (G == 0 || g >= G) {
+    *start = total;
+    *count = 0;
+    return;
+  }
+  const size_t base = total / G, rem = total % G;
+  *start = g * base + (g < rem ? g : rem);
+  *count = base + (g < rem ? 1 : 0);
 }
 
 }  // extern "C"

@@ -116,6 +116,26 @@ def _tptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _dev(t, name: str, device: int, shape=None, numel=None):
+    """Validate a device buffer before its pointer crosses the C ABI, which takes no
+    lengths for device buffers: a wrong dtype, device, row width or size would make a
+    kernel read or write out of bounds.  Returns the pointer."""
+    import torch
+    if not isinstance(t, torch.Tensor):
+        raise DcfError(-1, f"{name} must be a torch tensor")
+    if t.dtype != torch.uint8:
+        raise DcfError(-1, f"{name} must be uint8, got {t.dtype}")
+    if t.device.type != "cuda" or t.device.index != device:
+        raise DcfError(-1, f"{name} must be on cuda:{device}, got {t.device}")
+    if not t.is_contiguous():
+        raise DcfError(-1, f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise DcfError(-5, f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+    if numel is not None and t.numel() != numel:
+        raise DcfError(-5, f"{name} has {t.numel()} bytes, expected {numel}")
+    return ctypes.c_void_p(t.data_ptr())
+
+
 def _stream(device_index: int):
     import torch
     return ctypes.c_void_p(torch.cuda.current_stream(device_index).cuda_stream)
@@ -289,47 +309,127 @@ class DcfImpl:
         """K independent `Dcf::gen` calls in one launch.  alpha: (K, N), beta/s0_0/s0_1: (K, LAMBDA).
         Returns the K-key CWB tensor (include/dcf_hip.h layout)."""
         import torch
-        K = alpha.shape[0]
+        lam, nb, dev = self.lam, self.n_bytes, self.prg.device
+        K = alpha.shape[0] if alpha.dim() == 2 else -1
+        pa = _dev(alpha, "alpha", dev, shape=(K, nb))
+        pb = _dev(beta, "beta", dev, shape=(K, lam))
+        p0 = _dev(s0_0, "s0_0", dev, shape=(K, lam))
+        p1 = _dev(s0_1, "s0_1", dev, shape=(K, lam))
         if cwb_out is None:
-            cwb_out = torch.empty(cwb_bytes(self.n_bytes, self.lam, K), dtype=torch.uint8, device=alpha.device)
-        check(_lib.load().dcf_gen_batch_device(self.prg.handle, self.n_bytes, K, _tptr(alpha), _tptr(beta),
-                                               _tptr(s0_0), _tptr(s0_1), int(bound), _tptr(cwb_out),
-                                               _stream(self.prg.device)))
+            cwb_out = torch.empty(cwb_bytes(nb, lam, K), dtype=torch.uint8, device=alpha.device)
+        po = _dev(cwb_out, "cwb_out", dev, numel=cwb_bytes(nb, lam, K))
+        check(_lib.load().dcf_gen_batch_device(self.prg.handle, nb, K, pa, pb, p0, p1, int(bound), po,
+                                               _stream(dev)))
         return cwb_out
 
     def eval_device(self, b: bool, cwb, s0, xs, ys=None):
         """One key over m points: xs (m, N) -> ys (m, LAMBDA), device tensors."""
         import torch
-        m = xs.shape[0]
+        lam, nb, dev = self.lam, self.n_bytes, self.prg.device
+        m = xs.shape[0] if xs.dim() == 2 else -1
+        px = _dev(xs, "xs", dev, shape=(m, nb))
+        pk = _dev(cwb, "cwb", dev, numel=cwb_bytes(nb, lam, 1))
+        ps = _dev(s0, "s0", dev, numel=lam)
         if ys is None:
-            ys = torch.empty((m, self.lam), dtype=torch.uint8, device=xs.device)
-        if ys.numel() != m * self.lam:
-            raise DcfError(-5, "xs / ys length mismatch")
-        check(_lib.load().dcf_eval_device(self.prg.handle, self.n_bytes, int(bool(b)), _tptr(cwb), _tptr(s0),
-                                          _tptr(xs), m, _tptr(ys), _stream(self.prg.device)))
+            ys = torch.empty((m, lam), dtype=torch.uint8, device=xs.device)
+        py = _dev(ys, "ys", dev, numel=m * lam)
+        check(_lib.load().dcf_eval_device(self.prg.handle, nb, int(bool(b)), pk, ps, px, m, py, _stream(dev)))
         return ys
 
     def eval_multikey_device(self, b: bool, cwb, s0s, xs, points_per_key: int, ys=None):
         """K keys x P points: xs (K*P, N), s0s (K, LAMBDA) -> ys (K*P, LAMBDA)."""
         import torch
-        K = s0s.shape[0]
-        if xs.shape[0] != K * points_per_key:
-            raise DcfError(-5, "xs rows != num_keys * points_per_key")
+        lam, nb, dev = self.lam, self.n_bytes, self.prg.device
+        K = s0s.shape[0] if s0s.dim() == 2 else -1
+        ps = _dev(s0s, "s0s", dev, shape=(K, lam))
+        px = _dev(xs, "xs", dev, shape=(K * points_per_key, nb))
+        pk = _dev(cwb, "cwb", dev, numel=cwb_bytes(nb, lam, K))
         if ys is None:
-            ys = torch.empty((xs.shape[0], self.lam), dtype=torch.uint8, device=xs.device)
-        check(_lib.load().dcf_eval_multikey_device(self.prg.handle, self.n_bytes, K, points_per_key, int(bool(b)),
-                                                   _tptr(cwb), _tptr(s0s), _tptr(xs), _tptr(ys),
-                                                   _stream(self.prg.device)))
+            ys = torch.empty((xs.shape[0], lam), dtype=torch.uint8, device=xs.device)
+        py = _dev(ys, "ys", dev, numel=K * points_per_key * lam)
+        check(_lib.load().dcf_eval_multikey_device(self.prg.handle, nb, K, points_per_key, int(bool(b)),
+                                                   pk, ps, px, py, _stream(dev)))
         return ys
 
     def eval_full_domain_device(self, b: bool, cwb, s0, ys=None):
         """`Dcf::eval` at every x in [0, 2^(8N)) (increasing, big-endian x): (2^(8N), LAMBDA) device tensor."""
         import torch
-        npts = 1 << (8 * self.n_bytes)
+        lam, nb, dev = self.lam, self.n_bytes, self.prg.device
+        npts = 1 << (8 * nb)
+        pk = _dev(cwb, "cwb", dev, numel=cwb_bytes(nb, lam, 1))
+        ps = _dev(s0, "s0", dev, numel=lam)
         if ys is None:
-            ys = torch.empty((npts, self.lam), dtype=torch.uint8, device=cwb.device)
-        if ys.numel() != npts * self.lam:
-            raise DcfError(-5, "ys must hold 2^(8N) outputs")
-        check(_lib.load().dcf_eval_full_domain_device(self.prg.handle, self.n_bytes, int(bool(b)), _tptr(cwb),
-                                                      _tptr(s0), _tptr(ys), _stream(self.prg.device)))
+            ys = torch.empty((npts, lam), dtype=torch.uint8, device=cwb.device)
+        py = _dev(ys, "ys", dev, numel=npts * lam)
+        check(_lib.load().dcf_eval_full_domain_device(self.prg.handle, nb, int(bool(b)), pk, ps, py, _stream(dev)))
         return ys
+
+
+def point_slice(total: int, G: int, g: int):
+    """dcf_point_slice: contiguous slice (start, count) of `total` points for slice g of G."""
+    st, ct = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.load().dcf_point_slice(int(total), int(G), int(g), ctypes.byref(st), ctypes.byref(ct))
+    return int(st.value), int(ct.value)
+
+
+class MultiGpuDcf:
+    """`Dcf::eval` of one key over G GPUs in one call (dcf_eval_multi_gpu[_device]): one
+    `DcfImpl` per device, all over PRGs built from the same keys; points are split into G
+    contiguous slices (point_slice).  The reference spreads eval over host cores inside one
+    call (lib.rs:194-199); this spreads it over devices, with no collective."""
+
+    def __init__(self, impls: Sequence[DcfImpl]):
+        if not impls:
+            raise ValueError("need at least one DcfImpl")
+        self.impls = list(impls)
+        self.n_bytes, self.lam = impls[0].n_bytes, impls[0].lam
+        if any(d.n_bytes != self.n_bytes or d.lam != self.lam for d in impls):
+            raise ValueError("DcfImpls disagree on N / LAMBDA")
+        self._prgs = (ctypes.c_void_p * len(impls))(*[d.prg.handle.value for d in impls])
+
+    def eval(self, b: bool, k: Share, xs, ys=None):
+        """Host buffers: like DcfImpl.eval, slices evaluated concurrently on every device."""
+        lam, nb = self.lam, self.n_bytes
+        cwb = share_to_cwb(k, nb, lam)
+        xa = self.impls[0]._as_points(xs)
+        m = xa.shape[0]
+        if ys is None:
+            ys = np.zeros((m, lam), np.uint8)
+        if not (isinstance(ys, np.ndarray) and ys.dtype == np.uint8 and ys.flags["C_CONTIGUOUS"]):
+            raise TypeError("ys must be a contiguous uint8 numpy array")
+        if ys.size != m * lam:
+            raise DcfError(-5, f"xs.len() = {m} does not match ys")
+        check(_lib.load().dcf_eval_multi_gpu(self._prgs, len(self.impls), nb, int(bool(b)), _ptr(cwb), len(cwb),
+                                             _ptr(bytes(k.s0s[0])), _ptr(xa), m, _ptr(ys), ys.size))
+        return ys
+
+    def eval_device(self, b: bool, cwb: bytes, s0: bytes, xs_slices, ys_slices=None, gather=None):
+        """Device slices: xs_slices[g] (m_g, N) on impls[g]'s device -> ys_slices[g];
+        cwb / s0 are host bytes (copied to every device once).  gather: None, or a tensor
+        on impls[0]'s device of (sum m_g, LAMBDA) that receives every slice in order.
+        Queued on each device's current stream; synchronizes them before returning."""
+        import torch
+        lam, nb, G = self.lam, self.n_bytes, len(self.impls)
+        if len(xs_slices) != G:
+            raise DcfError(-5, "one xs slice per device")
+        if ys_slices is None:
+            ys_slices = [torch.empty((x.shape[0], lam), dtype=torch.uint8, device=x.device) for x in xs_slices]
+        ms = (ctypes.c_size_t * G)()
+        xp, yp, sp = (ctypes.c_void_p * G)(), (ctypes.c_void_p * G)(), (ctypes.c_void_p * G)()
+        for g, (d, x, y) in enumerate(zip(self.impls, xs_slices, ys_slices)):
+            m = x.shape[0] if x.dim() == 2 else -1
+            xp[g] = _dev(x, f"xs[{g}]", d.prg.device, shape=(m, nb)).value
+            yp[g] = _dev(y, f"ys[{g}]", d.prg.device, numel=m * lam).value
+            ms[g] = m
+            sp[g] = _stream(d.prg.device).value
+        gp = None
+        if gather is not None:
+            gp = _dev(gather, "gather", self.impls[0].prg.device, numel=sum(ms) * lam)
+        cwb = bytes(cwb)
+        if len(cwb) != cwb_bytes(nb, lam, 1):
+            raise DcfError(-8, "key size does not match 8*N levels (lib.rs:165)")
+        check(_lib.load().dcf_eval_multi_gpu_device(self._prgs, G, nb, int(bool(b)), _ptr(cwb), len(cwb),
+                                                    _ptr(bytes(s0)), xp, ms, yp, sp, gp))
+        for d in self.impls:
+            torch.cuda.current_stream(d.prg.device).synchronize()
+        return ys_slices

@@ -37,13 +37,18 @@
  * Memory: `*_device` entry points take device pointers and a hipStream_t (as
  * void*, NULL = the legacy default stream) and are asynchronous; the library
  * keeps no reference to caller buffers once the stream has passed the call.
- * Host entry points take host pointers and are synchronous.
+ * Host entry points take host pointers and are synchronous: they run on three
+ * streams the dcf_prg owns (copy-in, compute, copy-out) through pinned staging
+ * buffers pooled on the dcf_prg, in chunks whose PCIe copies overlap the
+ * kernels of neighbouring chunks, and they wait for those streams only (never
+ * the whole device).  The GPU never reads or writes caller host memory.
  *
  * Threading: one dcf_prg may be used by one host thread at a time, and its
  * device calls must not overlap on different streams (its work counter and
  * scratch buffers are per dcf_prg; calls queued on one stream are fine);
- * distinct dcf_prg objects are independent.  Multi-GPU = one process (or one dcf_prg)
- * per device; the path shards by points/keys with no collective.
+ * distinct dcf_prg objects are independent.  Multi-GPU: one dcf_prg per device
+ * (all built from the same keys) and dcf_eval_multi_gpu / _device below, or one
+ * process per device; the path shards by points/keys with no collective.
  */
 #ifndef DCF_HIP_H
 #define DCF_HIP_H
@@ -184,6 +189,37 @@ int dcf_eval_device(dcf_prg* prg, size_t n_bytes, int party, const uint8_t* cwb,
  * its output ys[k*P + j]; s0s: K * lambda (k.s0s[0] of each key). */
 int dcf_eval_multikey_device(dcf_prg* prg, size_t n_bytes, size_t num_keys, size_t points_per_key, int party,
                              const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, void* stream);
+
+/* ---- multi-GPU (one call drives G devices) ----
+ * The reference spreads Dcf::eval over every host core inside one call (rayon,
+ * lib.rs:194-199); these spread it over G GPUs.  prgs[g] is a dcf_prg on the
+ * device that evaluates slice g; all G must be built from the same keys (and
+ * kind, lambda) — checked, DCF_ERR_ARG otherwise — and be distinct.  Points are
+ * split into G contiguous slices, slice g = dcf_point_slice(m, G, g): the first
+ * m % G slices hold one extra point.  Every (key, point) is independent, so no
+ * collective runs during evaluation. */
+
+/* Contiguous slice [start, start + count) of `total` items for slice g of G. */
+void dcf_point_slice(size_t total, size_t G, size_t g, size_t* start, size_t* count);
+
+/* Dcf::eval (lib.rs:163-204) of one key over host buffers on G devices: slice g
+ * of xs goes to prgs[g]'s device (one host thread per device, each running the
+ * pipelined host path above) and its outputs land directly in the matching rows
+ * of ys.  Synchronous; same arguments and errors as dcf_eval. */
+int dcf_eval_multi_gpu(dcf_prg* const* prgs, size_t G, size_t n_bytes, int party, const uint8_t* cwb,
+                       size_t cwb_len, const uint8_t* s0, const uint8_t* xs, size_t m, uint8_t* ys, size_t ys_len);
+
+/* Device-resident variant.  cwb (cwb_len bytes) and s0 are HOST pointers: the key
+ * is copied to every device once per call (the broadcast; 4.2 KB at N = LAMBDA =
+ * 16).  xs[g] / ys[g]: ms[g] points / outputs on prgs[g]'s device; streams[g]:
+ * that device's stream (streams may be NULL = each device's default stream).
+ * gather_ys: NULL, or a buffer on prgs[0]'s device of (sum of ms) * lambda bytes
+ * that receives every slice's outputs in slice order (hipMemcpyPeerAsync over
+ * xGMI, queued on streams[g] after slice g's eval).  Asynchronous: the caller
+ * synchronizes every streams[g] before reading ys or gather_ys. */
+int dcf_eval_multi_gpu_device(dcf_prg* const* prgs, size_t G, size_t n_bytes, int party, const uint8_t* cwb,
+                              size_t cwb_len, const uint8_t* s0, const uint8_t* const* xs, const size_t* ms,
+                              uint8_t* const* ys, void* const* streams, uint8_t* gather_ys);
 
 /* ---- key wire format (host only, no GPU) ----
  * `Share` as serialised by serde + bincode 1.x `bincode::serialize` (lib.rs:217-340;

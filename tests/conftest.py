@@ -13,6 +13,13 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libdcf_hip.so on cuda:0)")
+    config.addinivalue_line("markers", "config: full-size BASELINE.json config parity (run last)")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    """Full-size config tests run after everything else, so `-x` still reports the
+    smaller tests first (stable order otherwise)."""
+    items.sort(key=lambda it: it.get_closest_marker("config") is not None)
 
 
 def load_golden(name):
