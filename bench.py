@@ -499,7 +499,7 @@ def run_c5(args, world, rank):
     peak = PEAK_TT_BLOCKS
     achieved = (gen_blocks + eval_blocks) / step_s
     eval_s = phase[1] + phase[2]
-    traffic, traffic_src = traffic_fields("k_gen16+k_cw_keymajor+k_eval16_stream<MULTI>", K * P, nb, lam, 0, alg_bytes)
+    traffic, traffic_src = traffic_fields("k_gen16+2*k_cw_keymajor+2*k_eval16_stream", K * P, nb, lam, 0, alg_bytes)
     out = {"metric": "C5 batched gen + eval (both parties)", "value": evals / wall, "unit": "evals/s",
            "keys_per_s": global_keys * args.steps / wall, "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,

@@ -303,6 +303,73 @@ __device__ __forceinline__ void aes256_tt_gk(uint32_t (&st)[NB][4], const uint4*
   }
 }
 
+// AES-256 with round keys 0..KG-1 from the kernel-argument schedule (SGPRs) and rounds
+// KG..14 from the device copy rkg, each loaded by a uniform global_load_dwordx4 AHEAD
+// rounds before its use.  For kernels whose per-lane loads are issued just before the
+// AES (multi-key stream eval: the CW digest): vmcnt retires in order, so a key load
+// issued in round 1 would make its wait cover those digest loads too (all-global keys:
+// C5 -14 %); by round KG - AHEAD they have landed.  Uses 4 * KG SGPRs of keys instead of
+// 60, which leaves the multi-key stream kernel room for its loop state (no spills).
+template <int NB, int KG, int AHEAD = 3>
+__device__ __forceinline__ void aes256_tt_hk(uint32_t (&st)[NB][4], const RoundKeys& rk,
+                                             const uint4* __restrict__ rkg, const uint32_t* lds, uint32_t lc) {
+  static_assert(KG > AHEAD && KG <= 14, "keys KG..14 are loaded AHEAD rounds early");
+  const char* base = reinterpret_cast<const char*>(rkg);
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] ^= rk.w[j];
+  uint4 kq[15 - KG];
+#pragma unroll
+  for (int r = 1; r < 15; ++r) {
+    // issue the load of round key rn (>= KG) at round rn - AHEAD, after this round's state
+    const int rn = r + AHEAD;
+    if (rn >= KG && rn < 15) {
+      uint32_t zb = 0u;
+      asm volatile("" : "+v"(zb) : "v"(st[0][0]), "v"(st[NB - 1][0]));
+      kq[rn - KG] = *reinterpret_cast<const uint4*>(base + zb + 16 * rn);
+    }
+    uint32_t kw[4];
+    if (r < KG) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) kw[j] = rk.w[4 * r + j];
+    } else {
+      const uint4 k = kq[r - KG];
+      kw[0] = k.x; kw[1] = k.y; kw[2] = k.z; kw[3] = k.w;
+    }
+    uint32_t o[NB][4];
+    if (r < 14) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
+        }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+          const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
+          const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
+          o[b][j] = xor3(lo, hi, kw[j]);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+}
+
 template <int NB>
 __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* const (&rk)[NB], const uint32_t* lds,
                                           uint32_t lc) {

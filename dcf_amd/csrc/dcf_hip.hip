@@ -159,10 +159,14 @@ int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
   return DCF_OK;
 }
 
+// Workgroups of the single-launch table builds (k_prefix_build16, k_wpfx_build): 2^S
+// subtrees under level S, each expanded by one workgroup.
+uint32_t prefix_split(uint32_t levels) { return levels > 18u ? 8u : (levels > 10u ? levels - 10u : 0u); }
+
 // Shared-prefix depth for a single-key stream eval of `total` points (kernels_stream.h
 // PrefixTable): the top tree has 2^D nodes (33 B each, built with 2^(D+1) AES blocks)
 // and saves every point D levels.  Auto: D = log2(total) - 1 (table build < 1 block per
-// point), at most kPrefixMax = 26 (a 2.2 GB table of 32-B rows inside 4.4 GB of build
+// point; Hirose: log2(total)), at most kPrefixMax = 26 (a 2.2 GB table of 32-B rows inside 4.4 GB of build
 // buffers, 2 x 2^26 x 33 B), none below 8, always < 8N.  If the buffers cannot be
 // allocated in auto mode, eval retries 2 levels shallower down to 8, then runs without a
 // table (identical bytes; see try_prefix).  Measured (r01i, C2: 2^24 points, N = 4):
@@ -176,8 +180,10 @@ uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint6
   if (p->prefix_levels > 0) {
     d = std::min((uint32_t)p->prefix_levels, kPrefixMaxForced);
   } else {
+    // Hirose (one-launch build, k_prefix_build16): D = log2(total), r02g sweep C2 (2^24
+    // points) D = 22/23/24/25 -> 3.97/4.08/4.13/3.93 G evals/s; MMO (level kernels): log2 - 1
     const uint32_t lg = 63u - (uint32_t)__builtin_clzll(total | 1u);
-    d = lg > 1u ? lg - 1u : 0u;
+    d = p->kind == 0 ? lg : (lg > 1u ? lg - 1u : 0u);
     if (d < 8u) return 0;
     d = std::min(d, kPrefixMax);
   }
@@ -203,11 +209,15 @@ uint32_t wide_prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t m) {
 }
 
 // Expand the top `levels` levels of one key's tree for the wide stream head (the CW
-// digest p->d_dig must hold this key) into WidePrefix rows in p->d_pfx.
+// digest p->d_dig must hold this key) into WidePrefix rows in p->d_pfx, in one launch
+// (k_wpfx_build): [table 2^D x 80 B | 2 x 2^S regions of 2^(D-1-S) nodes].
 int build_wide_prefix(dcf_prg* p, uint32_t nlev, int party, const uint8_t* s0, uint32_t levels, WidePrefix* out,
                       hipStream_t st) {
-  const size_t half = (((size_t)80 << levels) + 255) & ~(size_t)255;
-  const size_t need = 2 * half;
+  const uint32_t S = prefix_split(levels);
+  const uint32_t R = 1u << (levels - 1u - S);
+  const size_t tab_bytes = (((size_t)80 << levels) + 255) & ~(size_t)255;
+  const size_t region = (size_t)80 * R;
+  const size_t need = tab_bytes + 2 * ((size_t)1 << S) * region;
   if (p->pfx_bytes < need) {
     if (p->d_pfx) {
       HIP_TRY(hipStreamSynchronize(st));
@@ -218,23 +228,19 @@ int build_wide_prefix(dcf_prg* p, uint32_t nlev, int party, const uint8_t* s0, u
     HIP_TRY(hipMalloc(&p->d_pfx, need));
     p->pfx_bytes = need;
   }
-  uint4* a = (uint4*)p->d_pfx;
-  uint4* b = (uint4*)(p->d_pfx + half);
-  hipLaunchKernelGGL(k_wpfx_root, dim3(1), dim3(64), 0, st, s0, (uint32_t)party, a);
+  uint4* table = (uint4*)p->d_pfx;
+  uint4* ba = (uint4*)(p->d_pfx + tab_bytes);
+  uint4* bb = (uint4*)(p->d_pfx + tab_bytes + ((size_t)1 << S) * region);
+  if (p->lambda == 32)
+    hipLaunchKernelGGL(k_wpfx_build<true>, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->d_rk2,
+                       (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, s0, (uint32_t)party, S, levels, ba, bb, R,
+                       table);
+  else
+    hipLaunchKernelGGL(k_wpfx_build<false>, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->d_rk2,
+                       (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, s0, (uint32_t)party, S, levels, ba, bb, R,
+                       table);
   HIP_TRY(hipGetLastError());
-  for (uint32_t lev = 0; lev < levels; ++lev) {
-    const uint64_t parents = 1ull << lev;
-    const dim3 grid((unsigned)grid_for(parents, p->cus));
-    if (p->lambda == 32)
-      hipLaunchKernelGGL(k_wpfx_level<true>, grid, dim3(kBlock), 0, st, p->d_tab, p->d_rk2, (const uint4*)p->d_dig,
-                         p->d_dig + (size_t)nlev * 64, lev, parents, a, b);
-    else
-      hipLaunchKernelGGL(k_wpfx_level<false>, grid, dim3(kBlock), 0, st, p->d_tab, p->d_rk2, (const uint4*)p->d_dig,
-                         p->d_dig + (size_t)nlev * 64, lev, parents, a, b);
-    HIP_TRY(hipGetLastError());
-    std::swap(a, b);
-  }
-  *out = WidePrefix{a, levels};
+  *out = WidePrefix{table, levels};
   return DCF_OK;
 }
 
@@ -248,11 +254,17 @@ int ensure_rk0(dcf_prg* p) {
 
 // Expand the top `levels` levels of the key's tree (s = s0, v = 0, t = party at the
 // root; k_fd_level16 per level, as the full-domain eval does) into p->d_pfx.
+
 int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const uint4* cwv, const uint8_t* cwt,
                  const uint4* np1, const uint8_t* s0, uint32_t levels, PrefixTable* out, hipStream_t st) {
   const uint64_t maxnodes = 1ull << levels;
   const size_t nodeb = 33, half = (maxnodes * nodeb + 255) & ~(size_t)255;
-  const size_t need = 2 * half + 64 * sizeof(uint32_t);
+  // Hirose: [table 2^D x 32 B | 2 x 2^S regions of 2^(D-1-S) nodes]; MMO: two level buffers + counters
+  const uint32_t S = prefix_split(levels);
+  const uint32_t R = 1u << (levels - 1u - S);
+  const size_t region = ((size_t)R * nodeb + 255) & ~(size_t)255;
+  const size_t tab_bytes = (maxnodes * 32 + 255) & ~(size_t)255;
+  const size_t need = p->kind == 0 ? tab_bytes + 2 * ((size_t)1 << S) * region : 2 * half + 64 * sizeof(uint32_t);
   if (p->pfx_bytes < need) {
     if (p->d_pfx) {
       HIP_TRY(hipStreamSynchronize(st));
@@ -267,6 +279,15 @@ int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const 
       return fail(kPrefixNoMem, std::string("prefix table: hipMalloc: ") + hipGetErrorString(e));
     }
     p->pfx_bytes = need;
+  }
+  if (p->kind == 0) {  // one launch: k_prefix_build16
+    uint8_t* ba = p->d_pfx + tab_bytes;
+    hipLaunchKernelGGL(k_prefix_build16, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->rk[0], cws, cwv, cwt,
+                       (const uint4*)s0, (uint32_t)party, S, levels, ba, ba + ((size_t)1 << S) * region,
+                       (uint64_t)region, R, (uint4*)p->d_pfx);
+    HIP_TRY(hipGetLastError());
+    *out = PrefixTable{(const uint4*)p->d_pfx, levels};
+    return DCF_OK;
   }
   uint4* s_a = (uint4*)p->d_pfx;
   uint4* v_a = s_a + maxnodes;
@@ -317,17 +338,30 @@ int try_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const ui
   return DCF_OK;
 }
 
+#ifndef DCF_TAIL_ROUNDS
+#define DCF_TAIL_ROUNDS 0  // r02i A/B on C4: 0 (4096-point ranges) 41.1-41.3 ms, 1 42.2-42.3, 2 41.9-42.1, 4 41.7-41.8
+#endif
 template <int TW, int NCH = 0>
 int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
                 uint32_t lam, uint64_t K, uint64_t key, const uint32_t* tvec, uint64_t cnt, uint8_t* ys,
-                hipStream_t st) {
+                hipStream_t st, int cus) {
   const uint32_t nch = (nlev + 1 + 3) / 4;
   const size_t lds = (size_t)nch * 16 * TW;
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail<TW, NCH>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const dim3 grid((unsigned)((lam + TW - 1) / TW), (unsigned)((cnt + kTailPts - 1) / kTailPts));
+  // Points per workgroup: each workgroup builds its tile's tables once, then streams its
+  // points; DCF_TAIL_ROUNDS > 0 sizes the ranges so the grid is that many workgroups per
+  // CU (fewer table builds and workgroup drains), 0 = fixed kTailPts-point ranges.
+  const uint64_t tiles = (lam + TW - 1) / TW;
+  uint64_t per = kTailPts;
+  if (DCF_TAIL_ROUNDS > 0) {
+    const uint64_t slots = (uint64_t)DCF_TAIL_ROUNDS * (uint64_t)cus;
+    const uint64_t ranges = std::max<uint64_t>(1, slots / tiles);
+    per = std::max<uint64_t>(kTailPts, (((cnt + ranges - 1) / ranges) + 1023) & ~(uint64_t)1023);
+  }
+  const dim3 grid((unsigned)tiles, (unsigned)((cnt + per - 1) / per));
   hipLaunchKernelGGL((k_eval_wide_tail<TW, NCH>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key, tvec,
-                     cnt, kTailPts, ys);
+                     cnt, (uint32_t)per, ys);
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }
@@ -403,9 +437,9 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
                          ys + off * lam, tvec);
     HIP_TRY(hipGetLastError());
     if (lam > 32) {
-      rc = (nch == 33) ? launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st)
-         : (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st)
-                       : launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st);
+      rc = (nch == 33) ? launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus)
+         : (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus)
+                       : launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus);
       if (rc) return rc;
     }
   }

@@ -568,6 +568,120 @@ __global__ void k_prefix_pack(const uint4* __restrict__ s, const uint4* __restri
   }
 }
 
+// One PRG call (A, B) on node (s, v, t) of level `lev` -> both children (lib.rs:176-189
+// with x bit 0 / 1), as in k_fd_level16.
+__device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, const RoundKeys& rk,
+                                            const uint32_t (&csw)[4], const uint32_t (&cvw)[4], uint32_t ct,
+                                            const uint32_t (&s)[4], const uint32_t (&v)[4], uint32_t t,
+                                            uint32_t (&sl)[4], uint32_t (&vl)[4], uint32_t& tl, uint32_t (&sr)[4],
+                                            uint32_t (&vr)[4], uint32_t& tr) {
+  uint32_t st[2][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    st[0][k] = s[k];
+    st[1][k] = ~s[k];
+  }
+  aes256_tt<2>(st, rk, lds, lc);  // A, B
+  const uint32_t tm = 0u - t;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t msk = (k == 3) ? kMaskLast : 0xFFFFFFFFu;
+    sl[k] = ((st[0][k] ^ s[k]) & msk) ^ (tm & csw[k]);
+    sr[k] = (s[k] & msk) ^ (tm & csw[k]);
+    vl[k] = v[k] ^ ((st[1][k] ^ ~s[k]) & msk) ^ (tm & cvw[k]);
+    vr[k] = v[k] ^ ((~s[k]) & msk) ^ (tm & cvw[k]);
+  }
+  tl = ((st[0][0] ^ s[0]) & 1u) ^ (t & ct & 1u);
+  tr = ((st[1][0] ^ ~s[0]) & 1u) ^ (t & (ct >> 1) & 1u);
+}
+
+// Shared-prefix table (PrefixTable rows) of depth D in ONE launch, Hirose PRG.
+// The level-by-level build (k_fd_level16, one launch per level) spends most of its time
+// on the narrow upper levels (C2: 23 launches, ~1 ms of a 5 ms step).  Here workgroup w
+// (2^S of them) owns the subtree under node w of level S: wave 0 walks the root path to
+// it (S PRG calls, bits of w Msb-first), then the workgroup expands its subtree level
+// by level with workgroup barriers only (no grid-wide sync), nodes ping-ponging through
+// the workgroup's own regions of two buffers (SoA: s[R] | v[R] | t[R], R = 2^(D-1-S)),
+// and the last level writes packed 32-B rows of the workgroup's contiguous block of the
+// table directly (no pack pass).  Same bytes as the level kernels + k_prefix_pack.
+__global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ s0,
+    const uint32_t party, const uint32_t S, const uint32_t D, uint8_t* __restrict__ buf_a,
+    uint8_t* __restrict__ buf_b, const uint64_t region_bytes, const uint32_t region_nodes,
+    uint4* __restrict__ table) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint4 root_s, root_v;
+  __shared__ uint32_t root_t;
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint32_t w = blockIdx.x;
+  uint8_t* X = buf_a + (uint64_t)w * region_bytes;
+  uint8_t* Y = buf_b + (uint64_t)w * region_bytes;
+  const uint32_t R = region_nodes;
+  if (threadIdx.x < 64) {  // wave 0: the path root -> node w of level S (every lane the same node)
+    const uint4 sv = s0[0];
+    uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w}, v[4] = {0u, 0u, 0u, 0u}, t = party;
+    for (uint32_t lev = 0; lev < S; ++lev) {
+      const uint4 cs = cw_s[lev], cv = cw_v[lev];
+      const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+      uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
+      fd_children(lds, lc, rk, csw, cvw, cw_t[lev], s, v, t, sl, vl, tl, sr, vr, tr);
+      const bool right = (w >> (S - 1u - lev)) & 1u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s[k] = right ? sr[k] : sl[k];
+        v[k] = right ? vr[k] : vl[k];
+      }
+      t = right ? tr : tl;
+    }
+    if (threadIdx.x == 0) {
+      root_s = make_uint4(s[0], s[1], s[2], s[3]);
+      root_v = make_uint4(v[0], v[1], v[2], v[3]);
+      root_t = t;
+    }
+  }
+  __syncthreads();
+  for (uint32_t lev = S; lev < D; ++lev) {
+    const uint32_t np = 1u << (lev - S);  // this workgroup's parents at level lev
+    const bool last = lev + 1u == D;
+    const uint4 cs = cw_s[lev], cv = cw_v[lev];
+    const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+    const uint32_t ct = cw_t[lev];
+    const uint4* xs_ = reinterpret_cast<const uint4*>(X);
+    const uint4* xv_ = xs_ + R;
+    const uint8_t* xt_ = X + (uint64_t)R * 32u;
+    uint4* ys_ = reinterpret_cast<uint4*>(Y);
+    uint4* yv_ = ys_ + R;
+    uint8_t* yt_ = Y + (uint64_t)R * 32u;
+    for (uint32_t j = threadIdx.x; j < np; j += blockDim.x) {
+      const uint4 sv = lev == S ? root_s : xs_[j], vv = lev == S ? root_v : xv_[j];
+      const uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w}, v[4] = {vv.x, vv.y, vv.z, vv.w};
+      const uint32_t t = lev == S ? root_t : xt_[j];
+      uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
+      fd_children(lds, lc, rk, csw, cvw, ct, s, v, t, sl, vl, tl, sr, vr, tr);
+      if (last) {  // PrefixTable rows: s with t in bit 0 of byte 15 (below the root s is masked there)
+        uint4* row = table + 2ull * (((uint64_t)w << (D - S)) + 2u * j);
+        row[0] = make_uint4(sl[0], sl[1], sl[2], (sl[3] & kMaskLast) | (tl << 24));
+        row[1] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+        row[2] = make_uint4(sr[0], sr[1], sr[2], (sr[3] & kMaskLast) | (tr << 24));
+        row[3] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
+      } else {
+        ys_[2 * j] = make_uint4(sl[0], sl[1], sl[2], sl[3]);
+        ys_[2 * j + 1] = make_uint4(sr[0], sr[1], sr[2], sr[3]);
+        yv_[2 * j] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+        yv_[2 * j + 1] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
+        yt_[2 * j] = (uint8_t)tl;
+        yt_[2 * j + 1] = (uint8_t)tr;
+      }
+    }
+    __syncthreads();  // the workgroup's children are its next parents
+    uint8_t* tmp = X;
+    X = Y;
+    Y = tmp;
+  }
+}
+
 // Root node for full-domain eval: s = s0 (k.s0s[0]), v = 0, t = party.
 __global__ void k_fd_root16(const uint4* __restrict__ s0, const uint32_t party, uint4* __restrict__ s,
                             uint4* __restrict__ v, uint8_t* __restrict__ t) {

@@ -42,6 +42,13 @@ constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wav
 #ifndef DCF_STREAM_GK
 #define DCF_STREAM_GK 1  // 1: single-key stream engine reads round keys from global memory (aes256_tt_gk)
 #endif
+#ifndef DCF_MK_HK
+// multi-key stream eval: 0 = all round keys in SGPRs (some spill to VGPR lanes); k > 3 =
+// keys k..14 from global memory (aes256_tt_hk).  r02h A/B on C5 (same box, 2 runs each):
+// 0: 393.5 M evals/s, 11: 370.6 (-6 %), 8: 362.5 (-8 %) — vmcnt also counts the y
+// stores, so a key load's wait can cover recent stores; the spill reloads cost less.
+#define DCF_MK_HK 0
+#endif
 #ifndef DCF_LDS_KEYS_LATE
 #define DCF_LDS_KEYS_LATE true  // ... read late (per round), so they are not all hoisted into VGPRs
 #endif
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ c
 }
 
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
-template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false>
+template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false, int HK = 0>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -285,6 +292,8 @@ __device__ __forceinline__ void stream_run(
       aes256_tt2<NS>(st, rk, lds, lc);
     } else if (GK) {  // round keys from global memory, loaded DCF_GK_AHEAD rounds ahead
       aes256_tt_gk<NS>(st, rkl, lds, lc);
+    } else if (HK) {  // keys 0..HK-1 from SGPRs, HK..14 from global memory (multi-key)
+      aes256_tt_hk<NS, (HK > 3 ? HK : 4)>(st, rk, rkl, lds, lc);
     } else if (LK) {  // round keys from LDS: one ds_read_b128 per round (see k_eval16_stream)
       const uint4* rkp[NS];
 #pragma unroll
@@ -441,8 +450,11 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   // spill reloads, no LDS traffic; C3 +3.6 %, r01o A/B).  Multi-key runs keep the
   // SGPR schedule (C5 -14 % with GK: its CW digest loads share the vector memory path).
   constexpr bool GK = DCF_STREAM_GK && !MULTI && !TT2;
-  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK>(lds, GK ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys,
-                                                ppk, total, ctr, ys, pf);
+  // Multi-key: keys DCF_MK_HK..14 from global memory (0 = all from SGPRs, which spill)
+  constexpr int HK = (MULTI && !TT2) ? DCF_MK_HK : 0;
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK>(
+      lds, (GK || HK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total, ctr,
+      ys, pf);
 }
 
 }  // namespace

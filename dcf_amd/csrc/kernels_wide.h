@@ -178,6 +178,9 @@ __device__ __forceinline__ uint4 w_row_piece(const uint8_t* __restrict__ cw_s, c
   return w;
 }
 
+#ifndef DCF_TAIL_BATCH
+#define DCF_TAIL_BATCH 2
+#endif
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 // 16 bytes at an LDS byte address: ds_read takes the address as is (a generic
 // pointer into an extern __shared__ array costs a v_add of the array base per read).
@@ -207,12 +210,14 @@ __device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst
   // v_perm builds e * 256 + q * 16 (+ 64 KiB per group of 16 chunks) from the t byte
   // and a lane constant, and c * 4096 mod 64 KiB rides in the ds_read offset field.
   uint32_t qb = 16u * q;
+  // DCF_TAIL_BATCH reads are issued before their XORs (more LDS reads in flight per wave)
+  constexpr uint32_t BT = DCF_TAIL_BATCH;
   for (uint32_t g16 = 0; g16 < nch16; ++g16) {  // full groups of 16 chunks (4 t words)
 #pragma unroll
-    for (uint32_t j = 0; j < 16; j += 2) {
-      uint4 b[2];
+    for (uint32_t j = 0; j < 16; j += BT) {
+      uint4 b[BT];
 #pragma unroll
-      for (uint32_t h = 0; h < 2; ++h) {
+      for (uint32_t h = 0; h < BT; ++h) {
         const uint32_t cc = j + h;
         if (TW == 256) {
           const uint32_t a = __builtin_amdgcn_perm(tq[cc >> 2], qb, 0x0c020000u | ((4u + (cc & 3u)) << 8));
@@ -222,10 +227,16 @@ __device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst
           b[h] = G[((16u * g16 + cc) * 16u + e) * LP + q];
         }
       }
-      acc[0] = xor3(acc[0], b[0].x, b[1].x);
-      acc[1] = xor3(acc[1], b[0].y, b[1].y);
-      acc[2] = xor3(acc[2], b[0].z, b[1].z);
-      acc[3] = xor3(acc[3], b[0].w, b[1].w);
+      // keep the batch's reads ahead of its XORs (the scheduler otherwise interleaves
+      // them two at a time); LDS reads cannot move across a memory clobber
+      if (BT > 2) asm volatile("" ::: "memory");
+#pragma unroll
+      for (uint32_t h = 0; h < BT; h += 2) {
+        acc[0] = xor3(acc[0], b[h].x, b[h + 1].x);
+        acc[1] = xor3(acc[1], b[h].y, b[h + 1].y);
+        acc[2] = xor3(acc[2], b[h].z, b[h + 1].z);
+        acc[3] = xor3(acc[3], b[h].w, b[h + 1].w);
+      }
     }
 #pragma unroll
     for (int k = 0; k < 12; ++k) tq[k] = tq[k + 4];  // word queue: no dynamic register indexing

@@ -307,20 +307,15 @@ __global__ void k_wpfx_root(const uint8_t* __restrict__ s0p, const uint32_t part
   }
 }
 
-// One level of the wide prefix tree: each parent node at depth `lev` -> its two
-// children (out[2 i] left, out[2 i + 1] right), bytes [0,32) of the walk exactly as
+// One wide prefix node (80 B: s[0:32) | v[0:32) | {t, t-vector word 0, partial word, 0})
+// at depth `lev` -> its two children, bytes [0,32) of the walk exactly as
 // k_eval_wide_head_stream updates them: A = E0(s_lo), B = E0(~s_lo) (left),
-// C = E17(s_hi), D = E17(~s_hi) (right), one lane per parent, all four blocks.
+// C = E17(s_hi), D = E17(~s_hi) (right), all four blocks.  rks: the LDS copies of the
+// schedules of ciphers 0 (rks[0..15)) and 17 (rks[23..38)).
 template <bool MASK_HEAD>
-__global__ __launch_bounds__(kBlock, 1) void k_wpfx_level(
-    const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
-    const uint8_t* __restrict__ dig_t, const uint32_t lev, const uint64_t parents, const uint4* __restrict__ in,
-    uint4* __restrict__ out) {
-  __shared__ uint32_t lds[kLdsWords];
-  __shared__ uint4 rks[23 + 15];
-  if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
-  lds_fill_tables(lds, tab);
-  const uint32_t lc = lane_const();
+__device__ __forceinline__ void wpfx_children(const uint32_t* lds, uint32_t lc, const uint4* rks,
+                                              const uint4* __restrict__ dig, const uint8_t* __restrict__ dig_t,
+                                              uint32_t lev, const uint4 (&in)[5], uint4 (&ol)[5], uint4 (&orr)[5]) {
   const uint32_t mlast = MASK_HEAD ? kMaskLast : 0xFFFFFFFFu;
   const uint4* d4 = dig + 4u * lev;
   const uint4 cs0 = d4[0], cs1 = d4[1], cv0 = d4[2], cv1 = d4[3];
@@ -328,64 +323,122 @@ __global__ __launch_bounds__(kBlock, 1) void k_wpfx_level(
   const uint32_t csw[8] = {cs0.x, cs0.y, cs0.z, cs0.w, cs1.x, cs1.y, cs1.z, cs1.w};
   const uint32_t cvw[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
   const uint32_t r = lev + 1u, pos = 8u * ((r >> 2) & 3u) + (r & 3u);
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g - threadIdx.x % 64u < parents; g += stride) {
-    const uint64_t nd = g < parents ? g : parents - 1;  // whole waves stay in the loop (uniform AES)
-    const uint4* pn = in + 5u * nd;
-    const uint4 a0 = pn[0], a1 = pn[1], b0 = pn[2], b1 = pn[3], e = pn[4];
-    const uint32_t sw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const uint32_t vw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    uint32_t ab[2][4], cd[2][4];
+  const uint4 a0 = in[0], a1 = in[1], b0 = in[2], b1 = in[3], e = in[4];
+  const uint32_t sw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const uint32_t vw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  uint32_t ab[2][4], cd[2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ab[0][j] = sw[j];           // A
-      ab[1][j] = ~sw[j];          // B
-      cd[0][j] = sw[4 + j];       // C
-      cd[1][j] = ~sw[4 + j];      // D
-    }
-    const uint4* rk0[2] = {rks, rks};
-    const uint4* rk17[2] = {rks + 23, rks + 23};
-    aes_tt_lk<14, 2, true>(ab, rk0, lds, lc);
-    aes_tt_lk<14, 2, true>(cd, rk17, lds, lc);
-    const uint32_t t = e.x, tm = 0u - t;
-    uint32_t sl[8], vl[8], sr[8], vr[8];
+  for (int j = 0; j < 4; ++j) {
+    ab[0][j] = sw[j];           // A
+    ab[1][j] = ~sw[j];          // B
+    cd[0][j] = sw[4 + j];       // C
+    cd[1][j] = ~sw[4 + j];      // D
+  }
+  const uint4* rk0[2] = {rks, rks};
+  const uint4* rk17[2] = {rks + 23, rks + 23};
+  aes_tt_lk<14, 2, true>(ab, rk0, lds, lc);
+  aes_tt_lk<14, 2, true>(cd, rk17, lds, lc);
+  const uint32_t t = e.x, tm = 0u - t;
+  uint32_t sl[8], vl[8], sr[8], vr[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t dA = ab[0][j] ^ sw[j], dB = ab[1][j] ^ ~sw[j];
-      const uint32_t dC = cd[0][j] ^ sw[4 + j], dD = cd[1][j] ^ ~sw[4 + j];
-      const uint32_t msk = (j == 3) ? mlast : 0xFFFFFFFFu;
-      // left: s = (A^s_lo, s_hi & M), v ^= (B^~s_lo, ~s_hi & M)   (prg.rs:57-68 with the diagonal zip)
-      sl[j] = dA ^ (tm & csw[j]);
-      sl[4 + j] = (sw[4 + j] & msk) ^ (tm & csw[4 + j]);
-      vl[j] = vw[j] ^ dB ^ (tm & cvw[j]);
-      vl[4 + j] = vw[4 + j] ^ (~sw[4 + j] & msk) ^ (tm & cvw[4 + j]);
-      // right: s = (s_lo, (C^s_hi) & M), v ^= (~s_lo, (D^~s_hi) & M)
-      sr[j] = sw[j] ^ (tm & csw[j]);
-      sr[4 + j] = (dC & msk) ^ (tm & csw[4 + j]);
-      vr[j] = vw[j] ^ ~sw[j] ^ (tm & cvw[j]);
-      vr[4 + j] = vw[4 + j] ^ (dD & msk) ^ (tm & cvw[4 + j]);
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t dA = ab[0][j] ^ sw[j], dB = ab[1][j] ^ ~sw[j];
+    const uint32_t dC = cd[0][j] ^ sw[4 + j], dD = cd[1][j] ^ ~sw[4 + j];
+    const uint32_t msk = (j == 3) ? mlast : 0xFFFFFFFFu;
+    // left: s = (A^s_lo, s_hi & M), v ^= (B^~s_lo, ~s_hi & M)   (prg.rs:57-68 with the diagonal zip)
+    sl[j] = dA ^ (tm & csw[j]);
+    sl[4 + j] = (sw[4 + j] & msk) ^ (tm & csw[4 + j]);
+    vl[j] = vw[j] ^ dB ^ (tm & cvw[j]);
+    vl[4 + j] = vw[4 + j] ^ (~sw[4 + j] & msk) ^ (tm & cvw[4 + j]);
+    // right: s = (s_lo, (C^s_hi) & M), v ^= (~s_lo, (D^~s_hi) & M)
+    sr[j] = sw[j] ^ (tm & csw[j]);
+    sr[4 + j] = (dC & msk) ^ (tm & csw[4 + j]);
+    vr[j] = vw[j] ^ ~sw[j] ^ (tm & cvw[j]);
+    vr[4 + j] = vw[4 + j] ^ (dD & msk) ^ (tm & cvw[4 + j]);
+  }
+  // t_L = lsb(A^s)[0], t_R = lsb(B^~s)[0], each ^ t & its cw.t   (lib.rs:179-180)
+  const uint32_t tl = ((ab[0][0] ^ sw[0]) ^ (t & ct)) & 1u;
+  const uint32_t trr = ((ab[1][0] ^ ~sw[0]) ^ (t & (ct >> 1))) & 1u;
+  uint32_t accl = e.z | (tl << pos), accr = e.z | (trr << pos), w0l = e.y, w0r = e.y;
+  if ((r & 15u) == 15u) {  // word r >> 4 of the t-vector is complete (r < 31: word 0)
+    w0l = accl; w0r = accr;
+    accl = accr = 0u;
+  }
+  ol[0] = make_uint4(sl[0], sl[1], sl[2], sl[3]);
+  ol[1] = make_uint4(sl[4], sl[5], sl[6], sl[7]);
+  ol[2] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+  ol[3] = make_uint4(vl[4], vl[5], vl[6], vl[7]);
+  ol[4] = make_uint4(tl, w0l, accl, 0u);
+  orr[0] = make_uint4(sr[0], sr[1], sr[2], sr[3]);
+  orr[1] = make_uint4(sr[4], sr[5], sr[6], sr[7]);
+  orr[2] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
+  orr[3] = make_uint4(vr[4], vr[5], vr[6], vr[7]);
+  orr[4] = make_uint4(trr, w0r, accr, 0u);
+}
+
+// The whole wide prefix tree of depth D in ONE launch (as k_prefix_build16 at LAMBDA = 16):
+// workgroup w (2^S of them) owns the subtree under node w of level S; wave 0 walks the
+// root path (root = k.s0s[0][0:32), v = 0, t = party, t-vector row 0 = party, as
+// k_wpfx_root), then the workgroup expands its subtree level by level with workgroup
+// barriers only, ping-ponging through its own regions (R = 2^(D-1-S) nodes of 80 B) of
+// two buffers; the last level writes the workgroup's contiguous block of the table.
+template <bool MASK_HEAD>
+__global__ __launch_bounds__(kBlock, 1) void k_wpfx_build(
+    const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
+    const uint8_t* __restrict__ dig_t, const uint8_t* __restrict__ s0p, const uint32_t party, const uint32_t S,
+    const uint32_t D, uint4* __restrict__ buf_a, uint4* __restrict__ buf_b, const uint32_t region_nodes,
+    uint4* __restrict__ table) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint4 rks[23 + 15];
+  __shared__ uint4 root[5];
+  if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint32_t w = blockIdx.x;
+  const uint64_t R5 = 5ull * region_nodes;
+  uint4* X = buf_a + (uint64_t)w * R5;
+  uint4* Y = buf_b + (uint64_t)w * R5;
+  if (threadIdx.x < 64) {  // wave 0: root -> node w of level S (every lane the same node)
+    const uint4* s4 = reinterpret_cast<const uint4*>(s0p);
+    uint4 nd[5] = {s4[0], s4[1], make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u),
+                   make_uint4(party, 0u, party, 0u)};
+    for (uint32_t lev = 0; lev < S; ++lev) {
+      uint4 cl[5], cr[5];
+      wpfx_children<MASK_HEAD>(lds, lc, rks, dig, dig_t, lev, nd, cl, cr);
+      const bool right = (w >> (S - 1u - lev)) & 1u;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) nd[q] = right ? cr[q] : cl[q];
     }
-    // t_L = lsb(A^s)[0], t_R = lsb(B^~s)[0], each ^ t & its cw.t   (lib.rs:179-180)
-    const uint32_t tl = ((ab[0][0] ^ sw[0]) ^ (t & ct)) & 1u;
-    const uint32_t trr = ((ab[1][0] ^ ~sw[0]) ^ (t & (ct >> 1))) & 1u;
-    uint32_t accl = e.z | (tl << pos), accr = e.z | (trr << pos), w0l = e.y, w0r = e.y;
-    if ((r & 15u) == 15u) {  // word r >> 4 of the t-vector is complete (r < 31: word 0)
-      w0l = accl; w0r = accr;
-      accl = accr = 0u;
+    if (threadIdx.x == 0)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) root[q] = nd[q];
+  }
+  __syncthreads();
+  for (uint32_t lev = S; lev < D; ++lev) {
+    const uint32_t np = 1u << (lev - S);
+    const bool last = lev + 1u == D;
+    uint4* out = last ? table + 5ull * ((uint64_t)w << (D - S)) : Y;
+    // whole waves stay in the loop (uniform AES); lanes past np compute a copy of node np - 1
+    for (uint32_t g = threadIdx.x; g - (threadIdx.x & 63u) < np; g += blockDim.x) {
+      const uint32_t j = g < np ? g : np - 1u;
+      uint4 in[5];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) in[q] = lev == S ? root[q] : X[5u * j + q];
+      uint4 cl[5], cr[5];
+      wpfx_children<MASK_HEAD>(lds, lc, rks, dig, dig_t, lev, in, cl, cr);
+      if (g < np) {
+        uint4* o = out + 10u * j;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          o[q] = cl[q];
+          o[5 + q] = cr[q];
+        }
+      }
     }
-    if (g < parents) {
-      uint4* o = out + 10u * g;
-      o[0] = make_uint4(sl[0], sl[1], sl[2], sl[3]);
-      o[1] = make_uint4(sl[4], sl[5], sl[6], sl[7]);
-      o[2] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
-      o[3] = make_uint4(vl[4], vl[5], vl[6], vl[7]);
-      o[4] = make_uint4(tl, w0l, accl, 0u);
-      o[5] = make_uint4(sr[0], sr[1], sr[2], sr[3]);
-      o[6] = make_uint4(sr[4], sr[5], sr[6], sr[7]);
-      o[7] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
-      o[8] = make_uint4(vr[4], vr[5], vr[6], vr[7]);
-      o[9] = make_uint4(trr, w0r, accr, 0u);
-    }
+    __syncthreads();  // the workgroup's children are its next parents
+    uint4* tmp = X;
+    X = Y;
+    Y = tmp;
   }
 }
 

@@ -124,8 +124,9 @@ int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
  * else, so eval expands the top D levels once (2^(D+1) AES blocks, 33 B per node,
  * as the full-domain eval does) and starts each point at level D from its node:
  * D fewer levels per point, identical output bytes.
- *   levels = -1: automatic (the default): D = log2(points) - 1, at most 26 (LAMBDA
- *                >= 32: 22), none below 8 or (LAMBDA = 16) for small batches;
+ *   levels = -1: automatic (the default): D = log2(points) (Aes128MatyasMeyerOseasPrg:
+ *                log2(points) - 1), at most 26 (LAMBDA >= 32: log2(points) - 1, at most
+ *                22), none below 8 or (LAMBDA = 16) for small batches;
  *   levels =  0: off;  levels > 0: that depth (capped at 28 (LAMBDA >= 32: 30) and
  *                at 8N - 1).
  * The table lives on the prg (its size follows the largest D used). */

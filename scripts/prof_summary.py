@@ -20,9 +20,9 @@ def short(name: str) -> str:
     return n.split("(")[0][:80]
 
 
-def main(d):
-    print(f"# rocprofv3 summary: {d}\n")
-    for db in glob.glob(os.path.join(d, "trace", "*.db")):
+def main(d, suffix=""):
+    print(f"# rocprofv3 summary: {d} {suffix}\n")
+    for db in glob.glob(os.path.join(d, "trace" + suffix, "*.db")):
         c = sqlite3.connect(db)
         print("## kernel trace (--kernel-trace --stats)\n")
         print("| kernel | calls | total ms | avg ms | % |")
@@ -44,7 +44,7 @@ def main(d):
             seen.add(k)
             print(f"| {k} | {gx} | {wx} | {v} | {a} | {s} | {lds} |")
         print()
-    for sub in sorted(glob.glob(os.path.join(d, "pmc_*"))):
+    for sub in sorted(glob.glob(os.path.join(d, "pmc_*" + suffix))):
         for db in glob.glob(os.path.join(sub, "*.db")):
             c = sqlite3.connect(db)
             agg = defaultdict(lambda: defaultdict(list))
@@ -67,36 +67,67 @@ def main(d):
             print()
 
 
-def pmc_traffic(d, kernel_prefix="k_eval16<0>"):
-    """Per-launch HBM bytes of the dominant kernel: 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B)."""
+def pmc_traffic(d, kernel_prefix="k_eval16<0>", suffix=""):
+    """Per-launch HBM bytes of the dominant kernel: 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B).
+    kernel_prefix may name several kernels joined by '+': their per-dispatch means add up
+    (one 'launch' = one call of each)."""
     out = {}
     for name, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
-        for db in glob.glob(os.path.join(d, name, "*.db")):
+        for db in glob.glob(os.path.join(d, name + suffix, "*.db")):
             c = sqlite3.connect(db)
-            vals = [v for k, cn, v in c.execute("select kernel_name, counter_name, value from counters_collection")
-                    if short(k).startswith(kernel_prefix) and cn == counter]
-            if vals:
-                out[counter] = sum(vals) / len(vals) * 1024
+            rows = list(c.execute("select kernel_name, counter_name, value from counters_collection"))
+            tot = 0.0
+            for kp in kernel_prefix.split("+"):
+                mult = 1.0
+                if "*" in kp:  # "2*k_eval16_stream": two dispatches of that kernel per launch
+                    m, kp = kp.split("*", 1)
+                    mult = float(m)
+                vals = [v for k, cn, v in rows if short(k).startswith(kp) and cn == counter]
+                if vals:
+                    tot += mult * sum(vals) / len(vals)
+            if tot:
+                out[counter] = tot * 1024
     if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
         out["read_bytes_corrected"] = 2 * out["FETCH_SIZE"]
         out["traffic_bytes"] = 2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]
     return out
 
 
+def record_traffic(path, entry):
+    """Add (or replace) one launch shape's entry in profiles/pmc_traffic.json (a list)."""
+    import json
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        t = []
+    t = t if isinstance(t, list) else [t]
+    key = lambda e: (e.get("kernel"), e.get("points_per_launch"), e.get("n_bytes"), e.get("lambda"),  # noqa: E731
+                     e.get("prefix_levels", 0))
+    t = [e for e in t if key(e) != key(entry)] + [entry]
+    with open(path, "w") as f:
+        json.dump(t, f, indent=1)
+
+
 if __name__ == "__main__":
-    # prof_summary.py <run dir> [<pmc_traffic.json out> <kernel prefix>]
-    main(sys.argv[1])
-    if len(sys.argv) > 2:
-        import json
-        prefix = sys.argv[3] if len(sys.argv) > 3 else "k_eval16_stream"
-        t = pmc_traffic(sys.argv[1], prefix)
-        t["source"] = sys.argv[1]
-        t["kernel"] = prefix
-        # the launch shape of scripts/gpu_profile.sh's bench run (bench.py defaults, workload C3)
-        # auto shared-prefix depth 26: x (16 B) + y (16 B) + one 32-byte table row per point
-        t.update({"workload": "C3", "points_per_launch": 1 << 28, "n_bytes": 16, "lambda": 16,
-                  "prefix_levels": 26, "algorithmic_bytes": (1 << 28) * 64,
-                  "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- "
-                             "python bench.py --steps 2 --warmup 1 --no-cpu"})
-        with open(sys.argv[2], "w") as f:
-            json.dump(t, f, indent=1)
+    # prof_summary.py <run dir> [--suffix _c2]
+    # prof_summary.py <run dir> --traffic <json> <kernel prefix(es)> <workload> <points> <n_bytes> <lambda>
+    #                 <prefix_levels> <algorithmic bytes> [--suffix _c2]
+    args = sys.argv[1:]
+    suffix = ""
+    if "--suffix" in args:
+        i = args.index("--suffix")
+        suffix = args[i + 1]
+        del args[i:i + 2]
+    if "--traffic" in args:
+        i = args.index("--traffic")
+        out, prefix, wl, pts, nb, lam, pfx, alg = args[i + 1:i + 9]
+        t = pmc_traffic(args[0], prefix, suffix)
+        t.update({"source": args[0] + "/" + suffix, "kernel": prefix, "workload": wl, "points_per_launch": int(pts),
+                  "n_bytes": int(nb), "lambda": int(lam), "prefix_levels": int(pfx), "algorithmic_bytes": float(alg),
+                  "command": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- "
+                             f"python bench.py --workload {wl.lower()} --steps 2 --warmup 1 --no-cpu --no-compare"})
+        record_traffic(out, t)
+        print(t)
+    else:
+        main(args[0], suffix)

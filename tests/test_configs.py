@@ -152,8 +152,8 @@ def _single_key_device(dcf, nb, m, want_depth, seed, unit):
 
 
 def test_config_c2(dcf):
-    """C2: N = 4 (32-bit x), LAMBDA = 16, one key at 2^24 points, auto shared prefix D = 23."""
-    _single_key_device(dcf, 4, 1 << 24, 23, 0xC2, 256)
+    """C2: N = 4 (32-bit x), LAMBDA = 16, one key at 2^24 points, auto shared prefix D = 24."""
+    _single_key_device(dcf, 4, 1 << 24, 24, 0xC2, 256)
 
 
 def test_config_c3(dcf):
@@ -166,7 +166,7 @@ def test_config_c3(dcf):
 def test_config_c3_strong_slices(dcf):
     """C3 sharded over G = 8 GPUs (strong scaling, bench.py's default): each GPU evaluates
     a contiguous 2^25-point slice of the 2^28 points (dcf_point_slice), with its own auto
-    prefix depth (24 instead of 26).  The first and last slices, evaluated alone, must
+    prefix depth (25 instead of 26).  The first and last slices, evaluated alone, must
     equal the same rows of the whole-batch eval byte for byte."""
     import torch
     nb, lam = 16, 16
@@ -179,7 +179,7 @@ def test_config_c3_strong_slices(dcf):
     whole = d.eval_device(False, cwb, T(s0), xs)
     for sl in (0, G - 1):
         start, cnt = dcf.point_slice(total, G, sl)
-        assert cnt == 1 << 25 and prg.eval_prefix_levels(nb, 1, cnt) == 24
+        assert cnt == 1 << 25 and prg.eval_prefix_levels(nb, 1, cnt) == 25
         part = d.eval_device(False, cwb, T(s0), xs[start:start + cnt])
         torch.cuda.synchronize()
         assert torch.equal(part, whole[start:start + cnt]), sl
