@@ -32,7 +32,8 @@ EXPORTS = [
     "dcf_cwb_bytes", "dcf_cwb_np1_offset", "dcf_gen", "dcf_eval", "dcf_prg_gen",
     "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device", "dcf_eval_full_domain_device",
     "dcf_share_bincode_bytes", "dcf_share_to_bincode", "dcf_share_from_bincode",
-    "dcf_point_slice", "dcf_eval_multi_gpu", "dcf_eval_multi_gpu_device",
+    "dcf_point_slice", "dcf_eval_multi_gpu", "dcf_eval_multi_gpu_device", "dcf_prg_set_prefix_max_bytes",
+    "dcf_prg_device_bytes",
 ]
 
 
@@ -89,6 +90,8 @@ def load(path: str = LIB_PATH):
         "dcf_share_to_bincode": ([sz, sz, u8p, u8p, sz, u8p, sz], i),
         "dcf_share_from_bincode": ([sz, sz, u8p, sz, u8p, u8p, sz, ctypes.POINTER(sz)], i),
         "dcf_point_slice": ([sz, sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)], None),
+        "dcf_prg_set_prefix_max_bytes": ([vp, sz], i),
+        "dcf_prg_device_bytes": ([vp], sz),
         "dcf_eval_multi_gpu": ([ctypes.POINTER(vp), sz, sz, i, u8p, sz, u8p, u8p, sz, u8p, sz], i),
         "dcf_eval_multi_gpu_device": ([ctypes.POINTER(vp), sz, sz, i, u8p, sz, u8p, ctypes.POINTER(vp),
                                        ctypes.POINTER(sz), ctypes.POINTER(vp), ctypes.POINTER(vp), u8p], i),

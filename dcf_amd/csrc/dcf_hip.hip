@@ -137,6 +137,7 @@ struct dcf_prg {
   size_t d_stage_bytes = 0;
   uint8_t* d_mkey = nullptr;  // dcf_eval_multi_gpu_device: this device's copy of the key (CWB + s0)
   size_t mkey_bytes = 0;
+  size_t prefix_cap = 0;      // dcf_prg_set_prefix_max_bytes: cap on the auto table's buffers (0 = none)
 };
 
 namespace {
@@ -174,6 +175,23 @@ uint32_t prefix_split(uint32_t levels) { return levels > 18u ? 8u : (levels > 10
 // C3 (2^28, N = 16): D = 16 / 24 / 26 -> 450 / 477 / ~482 M (397 M without; r01q/r).
 constexpr uint32_t kPrefixMax = 26;       // auto (C3 r01q sweep: 24 519, 25 521, 26 524, 27 524 M evals/s)
 constexpr uint32_t kPrefixMaxForced = 28;  // dcf_prg_set_prefix_levels (2^28 x 33 B x 2 = 17.7 GB)
+// Device bytes of a shared-prefix table of depth d (table + build buffers, as build_prefix /
+// build_wide_prefix allocate them).
+size_t prefix_table_bytes(const dcf_prg* p, uint32_t d) {
+  if (d == 0) return 0;
+  const uint32_t S = prefix_split(d);
+  if (p->lambda > 16) return (((size_t)80 << d) + 255) + 2 * ((size_t)80 << (d - 1u));
+  if (p->kind == 1) return 2 * ((((size_t)33 << d) + 255) & ~(size_t)255) + 256;
+  return ((((size_t)32 << d) + 255) & ~(size_t)255) + 2 * ((size_t)1 << S) * ((((size_t)33 << (d - 1u - S)) + 255) & ~(size_t)255);
+}
+
+// Auto depth under the dcf_prg_set_prefix_max_bytes cap: shallower until it fits (none below 8).
+uint32_t capped_depth(const dcf_prg* p, uint32_t d) {
+  if (!p->prefix_cap) return d;
+  while (d >= 8u && prefix_table_bytes(p, d) > p->prefix_cap) --d;
+  return d >= 8u ? d : 0u;
+}
+
 uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
   if (p->lambda != 16 || num_keys != 1 || p->prefix_levels == 0) return 0;
   uint32_t d;
@@ -186,6 +204,7 @@ uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint6
     d = p->kind == 0 ? lg : (lg > 1u ? lg - 1u : 0u);
     if (d < 8u) return 0;
     d = std::min(d, kPrefixMax);
+    d = capped_depth(p, std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1)));
   }
   return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
 }
@@ -204,6 +223,7 @@ uint32_t wide_prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t m) {
     d = lg > 1u ? lg - 1u : 0u;
     if (d < 8u) return 0;
     d = std::min(d, kWidePrefixMax);
+    d = capped_depth(p, std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1)));
   }
   return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
 }
@@ -609,6 +629,25 @@ int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves, int slab_variant) {
   p->hybrid_tt_waves = ttable_waves;
   p->hybrid_mem = slab_variant;
   return DCF_OK;
+}
+
+int dcf_prg_set_prefix_max_bytes(dcf_prg* p, size_t max_bytes) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  p->prefix_cap = max_bytes;
+  return DCF_OK;
+}
+
+size_t dcf_prg_device_bytes(const dcf_prg* p) {
+  if (!p) return 0;
+  size_t b = 0;
+  if (p->d_tab) b += sizeof(g_tab);
+  if (p->d_km) b += 15 * 4 * 8 * 16;
+  if (p->d_rk128) b += 4 * 44 * 4;
+  if (p->d_rk2) b += 2 * sizeof(RoundKeys);
+  if (p->d_rk0) b += sizeof(RoundKeys);
+  if (p->d_dig) b += (size_t)p->dig_levels * 65;
+  if (p->d_ctr) b += kCtrBytes;
+  return b + p->kdig_bytes + p->ws_bytes + p->pfx_bytes + p->slab_bytes + p->d_stage_bytes + p->mkey_bytes;
 }
 
 int dcf_prg_last_eval_blocks(dcf_prg* p, uint64_t* blocks) {

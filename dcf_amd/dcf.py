@@ -182,6 +182,14 @@ class Aes256HirosePrg:
         -1 automatic (default), 0 off, > 0 that depth.  Output bytes are identical."""
         check(_lib.load().dcf_prg_set_prefix_levels(self._h, int(levels)))
 
+    def set_prefix_max_bytes(self, max_bytes: int) -> None:
+        """Cap the device memory of the automatic shared-prefix table (0 = no cap)."""
+        check(_lib.load().dcf_prg_set_prefix_max_bytes(self._h, int(max_bytes)))
+
+    def device_bytes(self) -> int:
+        """Device memory this prg currently holds (tables, prefix table, scratch, staging)."""
+        return int(_lib.load().dcf_prg_device_bytes(self._h))
+
     def eval_prefix_levels(self, n_bytes: int, num_keys: int, points_per_key: int) -> int:
         """The prefix depth an eval of this shape uses (0 = none)."""
         r = _lib.load().dcf_eval_prefix_levels(self._h, int(n_bytes), int(num_keys), int(points_per_key))

@@ -133,6 +133,13 @@ int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 int dcf_prg_set_prefix_levels(dcf_prg* prg, int levels);
 /* The prefix depth D a dcf_eval* call of this shape would use (0 = none). */
 int dcf_eval_prefix_levels(const dcf_prg* prg, size_t n_bytes, size_t num_keys, size_t points_per_key);
+/* Cap on the device memory the AUTOMATIC prefix depth may allocate (table + build
+ * buffers, which stay resident on the prg until it is freed): the auto depth is lowered
+ * until they fit, and no table is built below depth 8.  0 = no cap (the default: up to
+ * ~4.4 GB at depth 26, LAMBDA = 16).  Forced depths ignore it.  Output bytes never change. */
+int dcf_prg_set_prefix_max_bytes(dcf_prg* prg, size_t max_bytes);
+/* Device memory this dcf_prg currently holds (tables, prefix table, scratch, staging). */
+size_t dcf_prg_device_bytes(const dcf_prg* prg);
 
 /* Hybrid engine tuning (results are identical for every setting):
  *   slab_variant 1: 16-wave workgroups, bitsliced s/v state in a scratch slab;

@@ -174,3 +174,35 @@ def test_device_entry_points_reject_bad_shapes(dcf):
     for f in cases:
         with pytest.raises(dcf.DcfError):
             f()
+
+
+@pytest.mark.gpu
+def test_prefix_memory_cap_and_device_bytes(dcf):
+    """dcf_prg_set_prefix_max_bytes lowers the AUTO shared-prefix depth until its buffers fit
+    (none below depth 8), forced depths ignore it, output bytes never change;
+    dcf_prg_device_bytes reports the resident table."""
+    import torch
+    rng = np.random.default_rng(77)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg = dcf.Aes256HirosePrg(keys, 16)
+    d = dcf.DcfImpl(16, 16, prg)
+    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 26
+    prg.set_prefix_max_bytes(1 << 30)
+    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 23  # 2^23 x ~65 B fits 1 GiB, 2^24 does not
+    prg.set_prefix_max_bytes(1000)
+    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 0
+    prg.set_prefix_levels(12)
+    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 12   # forced: not capped
+    prg.set_prefix_levels(-1)
+    k = d.gen(dcf.CmpFn(rng.bytes(16), rng.bytes(16)), [rng.bytes(16), rng.bytes(16)], dcf.BoundState.LtBeta)
+    T = lambda b: torch.from_numpy(np.frombuffer(b, np.uint8).copy()).cuda()  # noqa: E731
+    xs = torch.from_numpy(rng.integers(0, 256, (1 << 20, 16), dtype=np.uint8)).cuda()
+    cwb, s0 = T(dcf.share_to_cwb(k, 16, 16)), T(k.s0s[0])
+    capped = d.eval_device(False, cwb, s0, xs)            # cap 1000 B: no table
+    torch.cuda.synchronize()
+    small = prg.device_bytes()
+    prg.set_prefix_max_bytes(0)
+    free = d.eval_device(False, cwb, s0, xs)              # auto depth 20
+    torch.cuda.synchronize()
+    assert torch.equal(capped, free)
+    assert prg.device_bytes() >= small + (1 << 20) * 32   # the 2^20-row table is resident
