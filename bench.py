@@ -65,7 +65,7 @@ PEAK_MMO_BLOCKS = CUS * CLK_HZ / (160 / 32 + 11 / 16)
 
 
 def engine_peak(engine: str) -> float:
-    if engine == "mmo":
+    if engine in ("mmo", "mmo-wide"):
         return PEAK_MMO_BLOCKS
     if engine in ("ttable", "ttable-small", "stream"):
         return PEAK_TT_BLOCKS
@@ -294,7 +294,7 @@ def run_eval(args, world, rank):
     rng = np.random.default_rng(0xDCF0001)
     # benches/dcf_batch_eval.rs:7 uses 2 AES keys at LAMBDA = 16; benches/dcf_large_lambda.rs:10 uses 2048.
     if args.prg == "mmo":  # Aes128MatyasMeyerOseasPrg (north_star's PRG; not in the reference): 4 AES-128 keys
-        keys = [rng.bytes(16) for _ in range(4)]
+        keys = [rng.bytes(16) for _ in range(4 * lam // 16)]  # per output and 16-byte block
         prg = dcf_amd.Aes128MatyasMeyerOseasPrg(keys, lam, device=torch.cuda.current_device())
     else:
         keys = [rng.bytes(32) for _ in range(2 if lam == 16 else 2048)]
@@ -338,6 +338,8 @@ def run_eval(args, world, rank):
     total_evals = global_points * args.steps * parties
     value = total_evals / wall
     bpe = blocks_per_eval(nb, lam)
+    if args.prg == "mmo" and lam > 16:
+        bpe = 4 * 8 * nb * (lam // 16)  # the MMO PRG's full output per level: 4 outputs x LAMBDA/16 blocks
     engine = ENGINE[args.eval_mode] if lam == 16 else "ttable"
     if engine in ("hybrid", "bitsliced", "stream-hybrid") and nb > 16:
         engine = "ttable"
@@ -359,7 +361,11 @@ def run_eval(args, world, rank):
         exec_bpe = 2 * (8 * nb - pfx) + (2 ** (pfx + 1) - 2) / m
     else:
         exec_bpe = bpe
-    if lam > 16:
+    if lam > 16 and args.prg == "mmo":
+        # multi-block MMO: the side's s and v blocks for every 16-byte block, every level
+        engine = "mmo-wide"
+        exec_bpe = 2 * 8 * nb * (lam // 16)
+    elif lam > 16:
         # LAMBDA >= 32: the stream head encrypts B, A (left) or B, D, C (right) per level, and the
         # tail writes LAMBDA - 32 output bytes per eval: time bound = AES (LDS) + output (HBM write).
         engine = "stream-head" if args.eval_mode != 1 else "ttable"
@@ -371,6 +377,7 @@ def run_eval(args, world, rank):
     # one 32-byte table row gathered per point (kernels16.h PrefixTable)
     alg_bytes = m * (nb + lam) + (m * 32 if pfx else 0)
     kernel = KERNEL.get(engine, "k_eval16") if lam == 16 else (
+        "k_mmo_wide_eval" if engine == "mmo-wide" else
         "k_eval_wide_head_stream+k_eval_wide_tail" if engine == "stream-head" else "k_eval_wide_head+k_eval_wide_tail")
     peak = engine_peak(engine)
     traffic, traffic_src = traffic_fields(kernel, m, nb, lam, pfx, alg_bytes)
@@ -388,10 +395,10 @@ def run_eval(args, world, rank):
                    "parallelism": f"points sharded over {world} GPU(s) in contiguous slices, "
                                   "no collective in timed region"},
         "aes_blocks_per_s": value * bpe,
-        "roofline": wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine) if lam > 16 else {
-            "bound": "lds" if engine in ("ttable", "ttable-small", "stream", "mmo") else ("valu" if engine == "bitsliced" else "lds+valu"),
+        "roofline": wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine) if (lam > 16 and engine != "mmo-wide") else {
+            "bound": "lds" if engine in ("ttable", "ttable-small", "stream", "mmo", "mmo-wide") else ("valu" if engine == "bitsliced" else "lds+valu"),
             "kernel": kernel, "engine": engine,
-            "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-128 blocks/s" if engine == "mmo" else "G AES-256 blocks/s",
+            "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-128 blocks/s" if engine.startswith("mmo") else "G AES-256 blocks/s",
             "frac": per_gpu_blocks / peak, "traffic": traffic, "traffic_source": traffic_src,
             "algorithmic_bytes": alg_bytes, "kernel_ms": kern_s * 1e3,
             "hbm_GBps": alg_bytes / kern_s / 1e9,
@@ -408,7 +415,7 @@ def run_eval(args, world, rank):
                     "the VALU left over (DESIGN.md section 4)",
         },
     }
-    if lam > 16:
+    if lam > 16 and engine != "mmo-wide":
         out["roofline"]["prefix_levels"] = pfx  # wide stream head below a shared-prefix table
         out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic_fields(
             kernel, m, nb, lam, pfx, m * (nb + lam))

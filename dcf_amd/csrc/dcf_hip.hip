@@ -38,6 +38,7 @@
 #include "kernels_bs.h"
 #include "kernels_stream.h"
 #include "kernels_mmo.h"
+#include "kernels_mmo_wide.h"
 #include "kernels_wide_stream.h"
 #include "kernels_shybrid.h"
 
@@ -214,7 +215,7 @@ uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint6
 // Auto: log2(m) - 1, at most 22 (two 336 MB node buffers at 2^22), none below 8.
 constexpr uint32_t kWidePrefixMax = 22;
 uint32_t wide_prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t m) {
-  if (p->lambda <= 16 || p->prefix_levels == 0 || p->eval_mode == DCF_EVAL_TTABLE || m == 0) return 0;
+  if (p->lambda <= 16 || p->kind != 0 || p->prefix_levels == 0 || p->eval_mode == DCF_EVAL_TTABLE || m == 0) return 0;
   uint32_t d;
   if (p->prefix_levels > 0) {
     d = std::min((uint32_t)p->prefix_levels, 30u);
@@ -466,6 +467,63 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
   return DCF_OK;
 }
 
+// Dcf::eval with the MMO PRG at LAMBDA >= 32 for key `key` (kernels_mmo_wide.h): per pass
+// of up to kWideChunk points, the head walks block 0 (y[0:16), t-vector), then the tail
+// walks blocks 1..nb-1 given the t-vectors.
+int eval_mmo_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
+                  const uint8_t* s0, const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
+  const uint32_t lam = (uint32_t)p->lambda, nb = lam / 16u;
+  if (n_bytes > 31) return fail(DCF_ERR_UNSUPPORTED, "MMO eval at LAMBDA >= 32 supports N <= 31");
+  const size_t n = 8 * n_bytes;
+  const uint8_t* cws = cwb;
+  const uint8_t* cwv = cwb + n * K * lam;
+  const uint8_t* cwt = cwb + 2 * n * K * lam;
+  const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
+  const uint64_t chunk = m < kWideChunk ? m : kWideChunk;
+  if (int rc = ensure_ws(p, chunk * kMmoTWords * 4, st)) return rc;
+  uint32_t* tvec = reinterpret_cast<uint32_t*>(p->d_ws);
+  for (uint64_t off = 0; off < m; off += chunk) {
+    const uint64_t cnt = std::min<uint64_t>(chunk, m - off);
+    const uint64_t groups = (cnt + 63) / 64;
+    const dim3 gh((unsigned)std::min<uint64_t>((groups + 15) / 16, (uint64_t)p->cus));
+    hipLaunchKernelGGL(k_mmo_wide_eval<true>, gh, dim3(kBlock), 0, st, p->d_tab, p->d_rk128, cws, cwv, cwt, np1, s0,
+                       (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes, lam, K, key, cnt, tvec, ys + off * lam);
+    HIP_TRY(hipGetLastError());
+    if (nb > 1) {
+      const uint64_t items = groups * (nb - 1);
+      const dim3 gt((unsigned)std::min<uint64_t>((items + 15) / 16, 4 * (uint64_t)p->cus));
+      hipLaunchKernelGGL(k_mmo_wide_eval<false>, gt, dim3(kBlock), 0, st, p->d_tab, p->d_rk128, cws, cwv, cwt, np1,
+                         s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes, lam, K, key, cnt, tvec,
+                         ys + off * lam);
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  return DCF_OK;
+}
+
+// Batched Dcf::gen with the MMO PRG at LAMBDA >= 32 (kernels_mmo_wide.h): per pass of keys,
+// the head over block 0 of both parties (t-CWs, per-level t bits), then the tail.
+int gen_mmo_wide(dcf_prg* p, size_t n_bytes, uint64_t K, const uint8_t* alpha, const uint8_t* beta,
+                 const uint8_t* s0_0, const uint8_t* s0_1, int bound, uint8_t* cws, uint8_t* cwv, uint8_t* cwt,
+                 uint8_t* np1, hipStream_t st) {
+  const uint32_t lam = (uint32_t)p->lambda, nb = lam / 16u, nlev = (uint32_t)(8 * n_bytes);
+  if (int rc = ensure_ws(p, (size_t)K * nlev * 4, st)) return rc;
+  uint32_t* tinfo = reinterpret_cast<uint32_t*>(p->d_ws);
+  const uint64_t groups = (K + 63) / 64;
+  const dim3 gh((unsigned)std::min<uint64_t>((groups + 15) / 16, (uint64_t)p->cus));
+  hipLaunchKernelGGL(k_mmo_wide_gen<true>, gh, dim3(kBlock), 0, st, p->d_tab, p->d_rk128, alpha, beta, s0_0, s0_1,
+                     (uint32_t)bound, (uint32_t)n_bytes, lam, K, cws, cwv, cwt, np1, tinfo);
+  HIP_TRY(hipGetLastError());
+  if (nb > 1) {
+    const uint64_t items = groups * (nb - 1);
+    const dim3 gt((unsigned)std::min<uint64_t>((items + 15) / 16, 4 * (uint64_t)p->cus));
+    hipLaunchKernelGGL(k_mmo_wide_gen<false>, gt, dim3(kBlock), 0, st, p->d_tab, p->d_rk128, alpha, beta, s0_0,
+                       s0_1, (uint32_t)bound, (uint32_t)n_bytes, lam, K, cws, cwv, cwt, np1, tinfo);
+    HIP_TRY(hipGetLastError());
+  }
+  return DCF_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -529,7 +587,6 @@ int dcf_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int dev
   if (!keys || !out) return fail(DCF_ERR_ARG, "null argument");
   *out = nullptr;
   if (lambda == 0 || lambda % 16 != 0) return fail(DCF_ERR_LAMBDA, "lambda must be a positive multiple of 16");
-  if (lambda != 16) return fail(DCF_ERR_UNSUPPORTED, "Aes128MatyasMeyerOseasPrg: lambda = 16 only");
   if (cipher_n < 4 * (lambda / 16)) return fail(DCF_ERR_CIPHER_N, "MMO PRG needs 4 * lambda / 16 AES-128 keys");
   std::call_once(g_aes_once, aes_init_tables);
   int ndev = 0;
@@ -544,8 +601,10 @@ int dcf_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int dev
   p->cipher_n = cipher_n;
   p->eval_mode = DCF_EVAL_TTABLE;
   p->key_blob.assign(keys, keys + 16 * cipher_n);
-  std::vector<uint32_t> w(4 * 44);
-  for (size_t i = 0; i < 4; i++) aes128_expand_words(keys + 16 * i, w.data() + 44 * i);
+  // schedule b * nb + j for output b (s_L, v_L, s_R, v_R) and 16-byte block j (kernels_mmo_wide.h)
+  const size_t nsched = 4 * (lambda / 16);
+  std::vector<uint32_t> w(nsched * 44);
+  for (size_t i = 0; i < nsched; i++) aes128_expand_words(keys + 16 * i, w.data() + 44 * i);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     p->cus = prop.multiProcessorCount;
@@ -614,6 +673,7 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   // the paths eval_launch takes without a table: small batches (MMO: at auto depth; Hirose: in
   // auto mode), Hirose engines other than the stream engine (MMO ignores the engine setting)
   const bool small = total < (uint64_t)p->cus * kBlock * 2;
+  if (p->kind == 1 && p->lambda > 16) return 0;  // MMO at LAMBDA >= 32: no shared prefix (head/tail per block)
   if (p->kind == 1) return small && p->prefix_levels < 0 ? 0 : (int)prefix_depth(p, n_bytes, num_keys, total);
   if (p->lambda > 16) return n_bytes > 31 ? 0 : (int)wide_prefix_depth(p, n_bytes, points_per_key);
   if (p->eval_mode == DCF_EVAL_AUTO && small) return 0;
@@ -697,6 +757,8 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
   uint8_t* cwv = cwb_out + n * num_keys * lam;
   uint8_t* cwt = cwb_out + 2 * n * num_keys * lam;
   uint8_t* np1 = cwb_out + dcf_cwb_np1_offset(n_bytes, lam, num_keys);
+  if (p->kind == 1 && lam > 16) return gen_mmo_wide(p, n_bytes, num_keys, alpha, beta, s0_0, s0_1, bound, cws, cwv,
+                                                    cwt, np1, (hipStream_t)stream);
   if (p->kind == 1) {  // Aes128MatyasMeyerOseasPrg (LAMBDA = 16)
     hipLaunchKernelGGL(k_gen16_mmo, dim3((unsigned)grid_for(num_keys, p->cus)), dim3(kBlock), 0, (hipStream_t)stream,
                        p->d_tab, p->d_rk128, alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1,
@@ -746,8 +808,10 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   const size_t n = 8 * n_bytes, lam = p->lambda;
   if (lam > 16) {  // head/tail pipeline per key
     for (uint64_t k = 0; k < num_keys; ++k) {
-      int rc = eval_wide(p, n_bytes, num_keys, k, party, cwb, s0s + k * lam, xs + k * ppk * n_bytes, ppk,
-                         ys + k * ppk * lam, (hipStream_t)stream);
+      int rc = p->kind == 1 ? eval_mmo_wide(p, n_bytes, num_keys, k, party, cwb, s0s + k * lam,
+                                            xs + k * ppk * n_bytes, ppk, ys + k * ppk * lam, (hipStream_t)stream)
+                            : eval_wide(p, n_bytes, num_keys, k, party, cwb, s0s + k * lam, xs + k * ppk * n_bytes,
+                                        ppk, ys + k * ppk * lam, (hipStream_t)stream);
       if (rc) return rc;
     }
     return DCF_OK;
@@ -1113,7 +1177,10 @@ static int host_prg_gen(dcf_prg* p, const uint8_t* seeds, size_t m, uint8_t* out
   hipStream_t sc = p->hs[1];
   memcpy(h, seeds, m * lam);
   HIP_TRY(hipMemcpyAsync(d, h, m * lam, hipMemcpyHostToDevice, sc));
-  if (p->kind == 1)
+  if (p->kind == 1 && lam > 16)
+    hipLaunchKernelGGL(k_prg_mmo_wide, dim3((unsigned)grid_for(m * (lam / 16), p->cus)), dim3(kBlock), 0, sc,
+                       p->d_tab, p->d_rk128, (const uint8_t*)d, (uint64_t)m, (uint32_t)lam, d + so);
+  else if (p->kind == 1)
     hipLaunchKernelGGL(k_prg16_mmo, dim3((unsigned)grid_for(m, p->cus)), dim3(kBlock), 0, sc, p->d_tab, p->d_rk128,
                        (const uint4*)d, (uint64_t)m, d + so);
   else if (lam == 16)
@@ -1233,7 +1300,7 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
     HIP_TRY(xs.alloc(npts * n_bytes));
     hipLaunchKernelGGL(k_domain_points, dim3(1024), dim3(256), 0, st, (uint32_t)n_bytes, npts, (uint8_t*)xs.p);
     HIP_TRY(hipGetLastError());
-    int rc = eval_wide(p, n_bytes, 1, 0, party, cwb, s0, (const uint8_t*)xs.p, npts, ys, st);
+    int rc = eval_launch(p, n_bytes, 1, npts, party, cwb, s0, (const uint8_t*)xs.p, ys, st);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(st));  // xs is freed on return
     return DCF_OK;

@@ -99,11 +99,13 @@ int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int 
 /* Aes128MatyasMeyerOseasPrg::<LAMBDA, CIPHER_N>::new(keys) on `device` — the PRG
  * BASELINE.json's north_star names; the reference crate has no such PRG, so the
  * definition is ours (parity UNPINNED by the reference; DESIGN.md §4 "MMO"):
- *   out_b = AES128_{keys[b]}(seed) ^ seed for b = s_L, v_L, s_R, v_R,
- *   t_L / t_R = Lsb0 bit 0 of byte 0 of s_L / s_R, then bit 0 of byte LAMBDA-1
- *   cleared in all four outputs (the Hirose convention of prg.rs:63-68).
- * keys: cipher_n * 16 bytes, cipher_n >= 4; lambda = 16 (else DCF_ERR_UNSUPPORTED).
- * Every gen / eval / prg entry point below accepts either PRG. */
+ *   out_b[j] = AES128_{keys[b * LAMBDA/16 + j]}(seed_j) ^ seed_j for b = s_L, v_L,
+ *   s_R, v_R and every 16-byte block j (one key per output and block: "multi-block
+ *   MMO" at LAMBDA >= 32), t_L / t_R = Lsb0 bit 0 of byte 0 of s_L / s_R, then bit 0
+ *   of byte LAMBDA-1 cleared in all four outputs (the Hirose convention of prg.rs:63-68).
+ * keys: cipher_n * 16 bytes, cipher_n >= 4 * lambda / 16 (else DCF_ERR_CIPHER_N).
+ * Every gen / eval / prg entry point below accepts either PRG (LAMBDA >= 32: N <= 31,
+ * no shared-prefix table). */
 int dcf_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int device, dcf_prg** out);
 
 /* 0 = Aes256HirosePrg, 1 = Aes128MatyasMeyerOseasPrg, -1 = null. */

@@ -203,8 +203,94 @@ def test_gpu_mmo_errors(dcf):
         dcf.Aes128MatyasMeyerOseasPrg([bytes(16)] * 3, 16)
     assert e.value.code == -3
     with pytest.raises(dcf.DcfError) as e:
-        dcf.Aes128MatyasMeyerOseasPrg([bytes(16)] * 8, 32)
-    assert e.value.code == -7
+        dcf.Aes128MatyasMeyerOseasPrg([bytes(16)] * 7, 32)  # LAMBDA = 32 needs 4 * 2 keys
+    assert e.value.code == -3
+    prg = dcf.Aes128MatyasMeyerOseasPrg([bytes(16)] * 8, 32)  # multi-block MMO is supported
+    assert prg.eval_prefix_levels(2, 1, 1 << 20) == 0        # no shared prefix at LAMBDA >= 32
+
+
+def _mmo_keys(lam, seed):
+    rng = np.random.default_rng(seed)
+    return rng, [rng.bytes(16) for _ in range(4 * lam // 16)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lam", [32, 48, 64, 256, 16384])
+def test_gpu_mmo_wide_prg_vs_oracle(dcf, lam):
+    """Multi-block MMO (one AES-128 key per output and 16-byte block) on the GPU PRG hook
+    vs the oracle's definition (checked against the inline restatement above)."""
+    rng, keys = _mmo_keys(lam, lam)
+    prg, P = dcf.Aes128MatyasMeyerOseasPrg(keys, lam), O.OracleMmoPrg(keys, lam)
+    seeds = [rng.bytes(lam) for _ in range(7)]
+    assert prg.gen_many(seeds) == [P.gen(sd) for sd in seeds]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lam,nb,m", [(32, 2, 300), (48, 3, 200), (64, 16, 130), (512, 4, 100), (16384, 16, 70),
+                                      (32, 1, 256), (96, 5, 65)])
+def test_gpu_mmo_wide_gen_eval_vs_oracle(dcf, lam, nb, m):
+    """gen + eval of both parties and both bounds at LAMBDA >= 32 (head over block 0, tail over
+    the others) bit for bit with the oracle, and the reconstruction y0 ^ y1 = beta [x < alpha]
+    (LtBeta) / [x > alpha] (GtBeta) on every point (parity unpinned by the reference)."""
+    rng, keys = _mmo_keys(lam, lam * 3 + nb)
+    prg, P = dcf.Aes128MatyasMeyerOseasPrg(keys, lam), O.OracleMmoPrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    for bound in (0, 1):
+        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+        ok = O.gen(P, alpha, beta, s0, s1, bound)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
+        raw = ok.cw_s.tobytes() + ok.cw_v.tobytes() + ok.cw_t.tobytes()
+        assert dcf.share_to_cwb(k, nb, lam) == raw + bytes((-len(raw)) % 16) + ok.cw_np1.tobytes(), (lam, bound)
+        xs = rng.integers(0, 256, (m, nb), dtype=np.uint8)
+        xs[0] = np.frombuffer(alpha, np.uint8)
+        ys = []
+        for b, s in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+            assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, bound, b)
+            ys.append(got)
+        xi = [int.from_bytes(x.tobytes(), "big") for x in xs]
+        a = int.from_bytes(alpha, "big")
+        for i, x in enumerate(xi):
+            on = (x < a) if bound == 0 else (x > a)
+            assert (ys[0][i] ^ ys[1][i]).tobytes() == (beta if on else bytes(lam)), (i, bound)
+
+
+@pytest.mark.gpu
+def test_gpu_mmo_wide_batch_gen_multikey_and_full_domain(dcf):
+    """Batched gen (64-key waves, a ragged last wave) + multi-key eval at LAMBDA = 64, and the
+    full-domain eval at N = 1, LAMBDA = 32, against the oracle."""
+    import torch
+    lam, nb, K, Pp = 64, 2, 70, 9
+    rng, keys = _mmo_keys(lam, 4242)
+    prg, Po = dcf.Aes128MatyasMeyerOseasPrg(keys, lam), O.OracleMmoPrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    r = lambda *sh: rng.integers(0, 256, sh, dtype=np.uint8)  # noqa: E731
+    alpha, beta, s0, s1 = r(K, nb), r(K, lam), r(K, lam), r(K, lam)
+    T = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    cwb = d.gen_batch_device(T(alpha), T(beta), T(s0), T(s1), dcf.BoundState.GtBeta)
+    xs = r(K * Pp, nb)
+    y0 = d.eval_multikey_device(False, cwb, T(s0), T(xs), Pp)
+    torch.cuda.synchronize()
+    cw, y0h = cwb.cpu().numpy(), y0.cpu().numpy()
+    n = 8 * nb
+    cws = cw[:n * K * lam].reshape(n, K, lam)
+    for key in (0, 1, 63, 64, K - 1):
+        ok = O.gen(Po, alpha[key].tobytes(), beta[key].tobytes(), s0[key].tobytes(), s1[key].tobytes(), 1)
+        assert np.array_equal(cws[:, key], ok.cw_s), key
+        sl = slice(key * Pp, (key + 1) * Pp)
+        assert np.array_equal(y0h[sl], O.eval_(Po, 0, ok, s0[key].tobytes(), xs[sl])), key
+    lam, nb = 32, 1
+    rng, keys = _mmo_keys(lam, 99)
+    prg, Po = dcf.Aes128MatyasMeyerOseasPrg(keys, lam), O.OracleMmoPrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+    ok = O.gen(Po, alpha, beta, s0, s1, 0)
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
+    cwbt = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, nb, lam), np.uint8).copy()).cuda()
+    y = d.eval_full_domain_device(False, cwbt, torch.from_numpy(np.frombuffer(s0, np.uint8).copy()).cuda())
+    torch.cuda.synchronize()
+    xs = np.arange(256, dtype=np.uint8).reshape(256, 1)
+    assert np.array_equal(y.cpu().numpy(), O.eval_(Po, 0, ok, s0, xs))
 
 
 @pytest.mark.gpu
