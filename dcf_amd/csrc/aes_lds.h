@@ -244,12 +244,13 @@ __device__ __forceinline__ void aes_tt_lk(uint32_t (&st)[NB][4], const uint4* co
 // address is base + zb + 16 r, where zb is a zero that an empty asm "redefines"
 // after the previous round's state, so the compiler can neither hoist the
 // 15 loads into 60 live registers nor needs any VALU to form the address.
-template <int NB>
+// PRE: the caller has already XORed round key 0 into st (folded into its own input XOR).
+template <int NB, bool PRE = false>
 __device__ __forceinline__ void aes256_tt_gk(uint32_t (&st)[NB][4], const uint4* __restrict__ rkg,
                                              const uint32_t* lds, uint32_t lc) {
   const char* base = reinterpret_cast<const char*>(rkg);
   uint32_t zb = 0u;
-  {
+  if (!PRE) {
     const uint4 k = *reinterpret_cast<const uint4*>(base);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {

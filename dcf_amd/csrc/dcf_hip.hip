@@ -139,6 +139,8 @@ struct dcf_prg {
   uint8_t* d_mkey = nullptr;  // dcf_eval_multi_gpu_device: this device's copy of the key (CWB + s0)
   size_t mkey_bytes = 0;
   size_t prefix_cap = 0;      // dcf_prg_set_prefix_max_bytes: cap on the auto table's buffers (0 = none)
+  uint8_t* d_rows = nullptr;  // single-key stream eval: 48-byte CW rows (k_cw_rows48)
+  size_t rows_bytes = 0;
 };
 
 namespace {
@@ -646,6 +648,7 @@ void dcf_prg_free(dcf_prg* p) {
     if (p->h_stage) (void)hipHostFree(p->h_stage);
     if (p->d_stage) (void)hipFree(p->d_stage);
     if (p->d_mkey) (void)hipFree(p->d_mkey);
+    if (p->d_rows) (void)hipFree(p->d_rows);
   }
   delete p;
 }
@@ -707,7 +710,8 @@ size_t dcf_prg_device_bytes(const dcf_prg* p) {
   if (p->d_rk0) b += sizeof(RoundKeys);
   if (p->d_dig) b += (size_t)p->dig_levels * 65;
   if (p->d_ctr) b += kCtrBytes;
-  return b + p->kdig_bytes + p->ws_bytes + p->pfx_bytes + p->slab_bytes + p->d_stage_bytes + p->mkey_bytes;
+  return b + p->kdig_bytes + p->ws_bytes + p->pfx_bytes + p->slab_bytes + p->d_stage_bytes + p->mkey_bytes +
+         p->rows_bytes;
 }
 
 int dcf_prg_last_eval_blocks(dcf_prg* p, uint64_t* blocks) {
@@ -978,11 +982,34 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
         int rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
         if (rc) return rc;
       }
+      if (DCF_STREAM_D48) {  // single key: 48-byte CW rows + a zero row (kernels_stream.h k_cw_rows48)
+        const size_t need = (n + 1) * 48;
+        if (p->rows_bytes < need) {
+          if (p->d_rows) {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipFree(p->d_rows));
+            p->d_rows = nullptr;
+            p->rows_bytes = 0;
+          }
+          HIP_TRY(hipMalloc(&p->d_rows, need));
+          p->rows_bytes = need;
+        }
+        hipLaunchKernelGGL(k_cw_rows48, dim3(1), dim3(256), 0, st, cws, cwv, cwt, (uint32_t)n, (uint4*)p->d_rows);
+        HIP_TRY(hipGetLastError());
+        scs = (const uint4*)p->d_rows;
+      }
     }
+    const bool pfx = DCF_STREAM_PFXT && pf.levels != 0;
+#define DCF_STREAM_K(XR, MK, PF, D4)                                                                          \
+  hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK, kBlock, false, PF, D4>), dim3((unsigned)blocks), block, 0, st, \
+                     p->d_tab, p->rk[0], scs, cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, \
+                     (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf, p->d_rk0)
 #define DCF_STREAM(XR, MK)                                                                                    \
-  hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], scs, \
-                     cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys,  \
-                     (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf, p->d_rk0)
+  do {                                                                                                        \
+    if (MK) DCF_STREAM_K(XR, MK, false, false);                                                               \
+    else if (pfx) DCF_STREAM_K(XR, false, true, DCF_STREAM_D48 != 0);                                          \
+    else DCF_STREAM_K(XR, false, false, DCF_STREAM_D48 != 0);                                                  \
+  } while (0)
 #ifdef DCF_STREAM_TT2
     if (xreg && !multi) {
       uint64_t b2 = (units + 9) / 10;
@@ -997,6 +1024,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     else if (multi) DCF_STREAM(false, true);
     else DCF_STREAM(false, false);
 #undef DCF_STREAM
+#undef DCF_STREAM_K
   } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
     const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;

@@ -42,6 +42,20 @@ constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wav
 #ifndef DCF_STREAM_GK
 #define DCF_STREAM_GK 1  // 1: single-key stream engine reads round keys from global memory (aes256_tt_gk)
 #endif
+// VALU trims of the single-key stream kernel.  r02n/r02o A/B (same box, 2 runs each, C3 / C2):
+// all off 523.3 M / 4.20 G evals/s; XOR3 524.1 / 4.19; D48+XOR3 520.8 / 4.17; PFXT+XOR3
+// 522.9 / 4.20; all three 521.4 / 4.22; PFXT alone 444 / 3.81 (register allocation flips).
+// Kernel VALU -4 % (1667 -> 1595 instructions) moved nothing: at ~80 % LDS busy the loop is
+// not VALU-bound.
+#ifndef DCF_STREAM_PFXT
+#define DCF_STREAM_PFXT 0  // separate kernel instance when a shared-prefix table is present (no fresh-word path)
+#endif
+#ifndef DCF_STREAM_D48
+#define DCF_STREAM_D48 0   // single key: CWs from 48-byte level rows (cs | cv | ct), one address per stream
+#endif
+#ifndef DCF_STREAM_XOR3
+#define DCF_STREAM_XOR3 1  // round key 0 folded into the input XOR (one v_bitop3 per word)
+#endif
 #ifndef DCF_MK_HK
 // multi-key stream eval: 0 = all round keys in SGPRs (some spill to VGPR lanes); k > 3 =
 // keys k..14 from global memory (aes256_tt_hk).  r02h A/B on C5 (same box, 2 runs each):
@@ -68,7 +82,7 @@ struct StreamLane {
   bool alive[NS];
 };
 
-template <int NS, bool XREG, bool MULTI>
+template <int NS, bool XREG, bool MULTI, bool PFX = false>
 __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int i, uint64_t p,
                                              const uint4* __restrict__ s0s, const uint4 s0v, uint32_t party,
                                              const uint8_t* __restrict__ xs, uint32_t nbytes, uint64_t ppk,
@@ -91,7 +105,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
     w0 = load_bits32(row, 0, nbytes);
   }
   uint32_t lev0 = 0u;
-  if (!MULTI && pf.levels) {  // start below the shared prefix: its row of the top-tree table
+  if (!MULTI && (PFX || pf.levels)) {  // start below the shared prefix: its row of the top-tree table
     lev0 = pf.levels;
     uint4 sv, vv;
     prefix_row(pf, w0 >> (32u - lev0), sv, vv, L.t[i]);
@@ -111,7 +125,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
   L.pt[i] = p;
   L.alive[i] = true;
   if (XREG) {
-    if (lev0) {  // word 0 is consumed here, shifted past the prefix bits
+    if (PFX || lev0) {  // word 0 is consumed here, shifted past the prefix bits
       L.cur[i] = w0 << lev0;
       L.xw[i][0] = L.xw[i][1]; L.xw[i][1] = L.xw[i][2]; L.xw[i][2] = L.xw[i][3];
       L.fresh[i] = false;
@@ -125,7 +139,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
 
 // Give every lane whose stream i is free (`mine`) a new point, or retire the
 // stream when the counter is exhausted.  Called in wave-uniform control flow.
-template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit>
+template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit, bool PFX = false>
 __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint64_t& unext,
                                               uint64_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
                                               uint64_t nunits, uint64_t total, const uint4* __restrict__ s0s,
@@ -151,7 +165,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
     }
     const uint32_t rank = lane_rank(need);
     const bool take = mine && (uint64_t)rank < uend - unext;
-    if (take) stream_start(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk, pf);
+    if (take) stream_start<NS, XREG, MULTI, PFX>(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk, pf);
     const uint64_t taken = __ballot(take);
     unext += (uint64_t)__popcll(taken);
     need &= ~taken;
@@ -204,8 +218,21 @@ __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ c
   }
 }
 
+// Single-key CW rows for the stream engine (D48): row l = cw_s[l] | cw_v[l] | (cw_t[l], 0, 0, 0),
+// 48 B, and row 8N = zeros, so a stream's current and next level are one address apart.
+__global__ void k_cw_rows48(const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
+                            const uint8_t* __restrict__ cw_t, const uint32_t nlev, uint4* __restrict__ rows) {
+  for (uint32_t l = threadIdx.x; l <= nlev; l += blockDim.x) {
+    const bool z = l == nlev;
+    rows[3 * l] = z ? make_uint4(0u, 0u, 0u, 0u) : cw_s[l];
+    rows[3 * l + 1] = z ? make_uint4(0u, 0u, 0u, 0u) : cw_v[l];
+    rows[3 * l + 2] = make_uint4(z ? 0u : (uint32_t)cw_t[l], 0u, 0u, 0u);
+  }
+}
+
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
-template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false, int HK = 0>
+template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false, int HK = 0,
+          bool PFX = false, bool D48 = false>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -229,8 +256,8 @@ __device__ __forceinline__ void stream_run(
   const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    stream_refill<NS, XREG, MULTI, UNIT>(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v, party, xs,
-                                         nbytes, ppk, pf);
+    stream_refill<NS, XREG, MULTI, UNIT, PFX>(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v,
+                                              party, xs, nbytes, ppk, pf);
 
   uint64_t nblk = 0;  // AES blocks this wave encrypts for live streams (wave-uniform)
   for (;;) {
@@ -249,18 +276,23 @@ __device__ __forceinline__ void stream_run(
     bool maybe[NS];  // the next level's CWs were loaded
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      if (MULTI) {  // cw_s = digest (2 uint4 per level), cw_t = digest t bytes
+      const uint4* row = cw_s + 3 * L.ci[i];  // D48: level rows cs | cv | (ct, 0, 0, 0), plus a zero row 8N
+      if (D48) {
+        cs[i] = row[0];
+        cv[i] = row[1];
+        ct[i] = reinterpret_cast<const uint32_t*>(row + 2)[0];
+      } else if (MULTI) {  // cw_s = digest (2 uint4 per level), cw_t = digest t bytes
         cs[i] = cw_s[2 * L.ci[i]];
         cv[i] = cw_s[2 * L.ci[i] + 1];
       } else {
         cs[i] = cw_s[L.ci[i]];
         cv[i] = cw_v[L.ci[i]];
       }
-      ct[i] = cw_t[L.ci[i]];
+      if (!D48) ct[i] = cw_t[L.ci[i]];
       // XREG: a fresh stream's x word is still in the queue; its first step is a B step
       // at the root, whose seed may be unmasked, so no reuse follows it anyway.
 #ifndef DCF_NO_B_REUSE
-      maybe[i] = L.alive[i] && L.ph[i] == 0u && L.t[i] == 0u && (!XREG || !L.fresh[i]) &&
+      maybe[i] = L.alive[i] && L.ph[i] == 0u && L.t[i] == 0u && (!XREG || PFX || !L.fresh[i]) &&
                  (L.cur[i] >> 31) != 0u && L.lev[i] + 1u < nlev;
 #else
       maybe[i] = false;
@@ -268,22 +300,29 @@ __device__ __forceinline__ void stream_run(
       // Loaded unconditionally (L1-resident): loads under a divergent branch made the
       // compiler wait for them before the AES.
       const uint64_t c2 = L.ci[i] + (L.lev[i] + 1u < nlev ? 1u : 0u);
-      if (MULTI) {
+      if (D48) {  // the next row (row 8N is zeros: no clamp needed)
+        cs2[i] = row[3];
+        cv2[i] = row[4];
+      } else if (MULTI) {
         cs2[i] = cw_s[2 * c2];
         cv2[i] = cw_s[2 * c2 + 1];
       } else {
         cs2[i] = cw_s[c2];
         cv2[i] = cw_v[c2];
       }
-      ct2[i] = cw_t[c2];
+      ct2[i] = D48 ? reinterpret_cast<const uint32_t*>(row + 5)[0] : (uint32_t)cw_t[c2];
     }
     // Slot i encrypts ~s (B) in phase 0 and s (A) in phase 1.
     uint32_t st[NS][4];
+    constexpr bool PRE = GK && DCF_STREAM_XOR3;  // round key 0 folded in here (one 3-input XOR per word)
+    uint4 k0 = make_uint4(0u, 0u, 0u, 0u);
+    if (PRE) k0 = rkl[0];
+    const uint32_t k0w[4] = {k0.x, k0.y, k0.z, k0.w};
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const uint32_t inv = L.ph[i] - 1u;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) st[i][j] = L.s[i][j] ^ inv;
+      for (int j = 0; j < 4; ++j) st[i][j] = PRE ? xor3(L.s[i][j], inv, k0w[j]) : (L.s[i][j] ^ inv);
     }
 #ifdef DCF_PRIO_UPDATE
     __builtin_amdgcn_s_setprio(0);
@@ -291,7 +330,7 @@ __device__ __forceinline__ void stream_run(
     if (TT2) {
       aes256_tt2<NS>(st, rk, lds, lc);
     } else if (GK) {  // round keys from global memory, loaded DCF_GK_AHEAD rounds ahead
-      aes256_tt_gk<NS>(st, rkl, lds, lc);
+      aes256_tt_gk<NS, PRE>(st, rkl, lds, lc);
     } else if (HK) {  // keys 0..HK-1 from SGPRs, HK..14 from global memory (multi-key)
       aes256_tt_hk<NS, (HK > 3 ? HK : 4)>(st, rk, rkl, lds, lc);
     } else if (LK) {  // round keys from LDS: one ds_read_b128 per round (see k_eval16_stream)
@@ -317,7 +356,7 @@ __device__ __forceinline__ void stream_run(
                    "+v"(cv2[i].y), "+v"(cv2[i].z), "+v"(cv2[i].w), "+v"(ct2[i]));
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      if (XREG) {  // next 32 x bits from the word queue (raw loads, byte-swapped here)
+      if (XREG && !PFX) {  // next 32 x bits from the word queue (raw loads, byte-swapped here)
         const bool nw = L.fresh[i];
         L.cur[i] = nw ? bswap32(L.xw[i][0]) : L.cur[i];
         L.xw[i][0] = nw ? L.xw[i][1] : L.xw[i][0];
@@ -417,8 +456,8 @@ __device__ __forceinline__ void stream_run(
                                  L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
       }
       if (__ballot(done))
-        stream_refill<NS, XREG, MULTI, UNIT>(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s, s0v,
-                                             party, xs, nbytes, ppk, pf);
+        stream_refill<NS, XREG, MULTI, UNIT, PFX>(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s,
+                                                  s0v, party, xs, nbytes, ppk, pf);
     }
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
@@ -426,7 +465,7 @@ __device__ __forceinline__ void stream_run(
 }
 
 // TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.
-template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false>
+template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false, bool PFX = false, bool D48 = false>
 __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -452,7 +491,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   constexpr bool GK = DCF_STREAM_GK && !MULTI && !TT2;
   // Multi-key: keys DCF_MK_HK..14 from global memory (0 = all from SGPRs, which spill)
   constexpr int HK = (MULTI && !TT2) ? DCF_MK_HK : 0;
-  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK>(
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48>(
       lds, (GK || HK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total, ctr,
       ys, pf);
 }
