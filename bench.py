@@ -143,14 +143,20 @@ def zero_bits(xs: torch.Tensor, skip_bits: int = 0) -> int:
     return tot
 
 
-def dist_setup(n_gpus: int):
+def dist_setup(n_gpus: int, backend: str = "nccl"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one rank per GPU; with --dist-backend gloo several ranks may share a device (a
+        # rehearsal of the multi-rank path on a one-GPU box)
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     if world != n_gpus:
@@ -337,6 +343,7 @@ def run_eval(args, world, rank):
                      "speedup": w0 / wall}
     total_evals = global_points * args.steps * parties
     value = total_evals / wall
+    check = slice_check(d, cwb, s0, ys, nb, lam, args, world, rank) if args.check else None
     bpe = blocks_per_eval(nb, lam)
     if args.prg == "mmo" and lam > 16:
         bpe = 4 * 8 * nb * (lam // 16)  # the MMO PRG's full output per level: 4 outputs x LAMBDA/16 blocks
@@ -419,6 +426,8 @@ def run_eval(args, world, rank):
         out["roofline"]["prefix_levels"] = pfx  # wide stream head below a shared-prefix table
         out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic_fields(
             kernel, m, nb, lam, pfx, m * (nb + lam))
+    if check is not None:
+        out["slice_check"] = check
     host_ys = None
     if args.host_path or args.workload == "c1":
         share = dcf_amd.cwb_to_share(cwb.cpu().numpy().tobytes(), nb, lam, [])
@@ -440,6 +449,33 @@ def run_eval(args, world, rank):
             out["cpu_baseline_1core"] = cpu_baseline(keys, nb, lam, cwb_h, sd, xs_h, ys_h, args.cpu_seconds / 2,
                                                      args.prg, threads=1, parties=pp)
     return out
+
+
+def ys_digest(ys: torch.Tensor) -> int:
+    """Order-sensitive 64-bit digest of an output slice (row-weighted byte sums)."""
+    y = ys.to(torch.int64)
+    w = torch.arange(1, ys.shape[0] + 1, device=ys.device, dtype=torch.int64).unsqueeze(1)
+    c = torch.arange(1, ys.shape[1] + 1, device=ys.device, dtype=torch.int64)
+    return int(((y * w).sum() + (y.sum(0) * c).sum()).item())
+
+
+def slice_check(d, cwb, s0, ys, nb, lam, args, world, rank):
+    """Multi-rank self-check: every rank's output digest goes to rank 0, which regenerates each
+    rank's slice of points, evaluates it itself and compares."""
+    digs = [ys_digest(ys)]
+    if world > 1:  # all_gather_object: gloo's all_gather takes host tensors only
+        digs = [None] * world
+        dist.all_gather_object(digs, ys_digest(ys))
+    if rank != 0:
+        return None
+    ok = []
+    for r in range(world):
+        st, cnt = (point_slice(args.points, world, r) if args.scaling == "strong" else weak_slice(args.points, r))
+        xr = gen_points(cnt, nb, st, 0xDCF0003)
+        yr = d.eval_device(False, cwb, s0, xr)
+        torch.cuda.synchronize()
+        ok.append(ys_digest(yr) == int(digs[r]))
+    return {"ranks": world, "slices_match": all(ok), "per_rank": ok}
 
 
 def run_c5(args, world, rank):
@@ -686,6 +722,10 @@ def main():
                          "weak: every rank gets the full count (default otherwise)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time dcf_eval on host buffers (PCIe included; always on for c1)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, rank 0 re-evaluates every rank's slice and compares output digests")
     args = ap.parse_args()
     if args.scaling is None:
         args.scaling = "strong" if args.workload in ("c3", "c5") else "weak"
@@ -705,7 +745,7 @@ def main():
     else:
         args.n_bytes = args.n_bytes or 16
         args.points = args.points or (1 << 28)
-    world, rank, _ = dist_setup(args.gpus)
+    world, rank, _ = dist_setup(args.gpus, args.dist_backend)
     if args.workload == "c5":
         out = run_c5(args, world, rank)
     elif args.workload == "fd":

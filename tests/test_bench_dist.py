@@ -1,0 +1,38 @@
+"""bench.py's multi-rank path on the GPU box: two ranks launched exactly as the driver
+launches N > 1 (torch.distributed.run, 127.0.0.1), here on one device with the gloo
+backend (RCCL needs one GPU per rank).  Key broadcast from rank 0, strong-scaled point
+slices (dcf_point_slice), max-over-ranks timing, and --check: rank 0 re-evaluates both
+slices and compares output digests."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from tests.conftest import ROOT
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_strong_scaling_check():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--points", str((1 << 22) + 3), "--no-cpu",
+           "--no-compare", "--dist-backend", "gloo", "--check"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["global_points"] == (1 << 22) + 3
+    assert d["config"]["points_per_gpu"] in ((1 << 21) + 1, (1 << 21) + 2)
+    assert d["value"] > 0
+    assert d["slice_check"]["slices_match"], d["slice_check"]
