@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 B="bench.py --workload $W --steps 2 --warmup 1 --no-cpu --no-compare $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_$W -o trace -- python $B > $OUT/trace_$W.log 2>&1 || { tail -5 $OUT/trace_$W.log; exit 1; }
-tail -1 $OUT/trace_$W.log > $OUT/bench_prof_$W.json
+grep "^{\"metric" $OUT/trace_$W.log > $OUT/bench_prof_$W.json || true
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$W -o pmc -- python $B > $OUT/pmc_fetch_$W.log 2>&1 || { tail -5 $OUT/pmc_fetch_$W.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$W -o pmc -- python $B > $OUT/pmc_write_$W.log 2>&1 || { tail -5 $OUT/pmc_write_$W.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE -d $OUT/pmc_sq_$W -o pmc -- python $B > $OUT/pmc_sq_$W.log 2>&1 || { tail -5 $OUT/pmc_sq_$W.log; exit 1; }
