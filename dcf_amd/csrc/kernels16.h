@@ -654,10 +654,25 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     uint4* ys_ = reinterpret_cast<uint4*>(Y);
     uint4* yv_ = ys_ + R;
     uint8_t* yt_ = Y + (uint64_t)R * 32u;
+    // parents of this thread: j, j + blockDim, ...; the next one's node is loaded before the
+    // current one's PRG call so the load latency hides behind the AES
+    uint4 nsv = make_uint4(0u, 0u, 0u, 0u), nvv = nsv;
+    uint32_t nt = 0u;
+    if (threadIdx.x < np) {
+      nsv = lev == S ? root_s : xs_[threadIdx.x];
+      nvv = lev == S ? root_v : xv_[threadIdx.x];
+      nt = lev == S ? root_t : xt_[threadIdx.x];
+    }
     for (uint32_t j = threadIdx.x; j < np; j += blockDim.x) {
-      const uint4 sv = lev == S ? root_s : xs_[j], vv = lev == S ? root_v : xv_[j];
+      const uint4 sv = nsv, vv = nvv;
       const uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w}, v[4] = {vv.x, vv.y, vv.z, vv.w};
-      const uint32_t t = lev == S ? root_t : xt_[j];
+      const uint32_t t = nt;
+      const uint32_t jn = j + blockDim.x;
+      if (jn < np) {
+        nsv = xs_[jn];
+        nvv = xv_[jn];
+        nt = xt_[jn];
+      }
       uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
       fd_children(lds, lc, rk, csw, cvw, ct, s, v, t, sl, vl, tl, sr, vr, tr);
       if (last) {  // PrefixTable rows: s with t in bit 0 of byte 15 (below the root s is masked there)

@@ -13,8 +13,9 @@
  * include/dcf_hip.h, dcf_mmo_prg_new) and its parity is UNPINNED by the
  * reference; AES-128 itself is pinned by FIPS-197 C.1 in tests/.
  *
- * Parity anchors (the Rust crate cannot be built here: no cargo/rustc, nightly
- * features, un-vendored deps — see DESIGN.md "Oracle"):
+ * PARITY UNPINNED against reference-produced bytes: the Rust crate cannot be built
+ * here (no cargo/rustc, nightly features, un-vendored deps — see DESIGN.md "Oracle")
+ * and its tests hold no output vectors.  Parity anchors instead:
  *   - AES-256 arithmetic: third-party crate `aes` ^0.8.3 (Cargo.toml:36, version
  *     unpinned, not vendored).  Restated from FIPS-197; pinned by the FIPS-197
  *     C.3 known-answer vector and cross-checked against OpenSSL libcrypto and an

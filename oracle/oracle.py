@@ -5,9 +5,12 @@ xymeng16/dcf hot path in ``oracle/dcf_oracle.c``).  Imported only by ``tests/``,
 ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg, as the
 checker; the product (``dcf_amd``) never imports it.
 
-Parity status: pinned by the FIPS-197 AES-256 known-answer vector, libcrypto,
-the independent restatement in ``oracle/pyref.py`` and the reference's own
-reconstruction tests (lib.rs:372-442, prg.rs:86-96).  See DESIGN.md "Oracle".
+Parity status: PARITY UNPINNED against bytes produced by the reference itself (the
+Rust crate cannot be built here and its tests hold no output vectors).  What pins
+it: the FIPS-197 AES-256 known-answer vector, libcrypto, the independent
+restatement in ``oracle/pyref.py`` (every golden vector is written only when both
+agree) and the reference's own reconstruction tests (lib.rs:372-442,
+prg.rs:86-96).  See DESIGN.md "Oracle".
 """
 from __future__ import annotations
 
