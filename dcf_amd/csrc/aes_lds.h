@@ -371,6 +371,75 @@ __device__ __forceinline__ void aes256_tt_hk(uint32_t (&st)[NB][4], const RoundK
   }
 }
 
+// AES-256 with round keys 0..KS-1 from the kernel-argument schedule (SGPRs) and rounds
+// KS..14 from an LDS copy (rkl, 240 B): one broadcast ds_read_b128 per round shared by the
+// NB blocks, issued after the previous round's state (empty asm on the address) so the
+// compiler keeps one LDS key live, not 15 - 4 * KS SGPRs fewer than aes256_tt with no
+// vector-memory wait (LDS results retire in order, counted apart from the CW loads).
+template <int NB, int KS>
+__device__ __forceinline__ void aes256_tt_sl(uint32_t (&st)[NB][4], const RoundKeys& rk,
+                                             const uint4* rkl, const uint32_t* lds, uint32_t lc) {
+  static_assert(KS >= 0 && KS <= 15, "rounds 0..KS-1 from SGPRs");
+  const char* base = reinterpret_cast<const char*>(rkl);
+  {
+    uint32_t kw[4];
+    if (KS > 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) kw[j] = rk.w[j];
+    } else {
+      const uint4 k = rkl[0];
+      kw[0] = k.x; kw[1] = k.y; kw[2] = k.z; kw[3] = k.w;
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] ^= kw[j];
+  }
+#pragma unroll
+  for (int r = 1; r < 15; ++r) {
+    uint32_t kw[4];
+    if (r < KS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) kw[j] = rk.w[4 * r + j];
+    } else {
+      uint32_t zb = 0u;
+      asm volatile("" : "+v"(zb) : "v"(st[0][0]), "v"(st[NB - 1][0]));
+      const uint4 k = *reinterpret_cast<const uint4*>(base + zb + 16 * r);
+      kw[0] = k.x; kw[1] = k.y; kw[2] = k.z; kw[3] = k.w;
+    }
+    uint32_t o[NB][4];
+    if (r < 14) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
+        }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+          const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
+          const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
+          o[b][j] = xor3(lo, hi, kw[j]);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+}
+
 template <int NB>
 __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* const (&rk)[NB], const uint32_t* lds,
                                           uint32_t lc) {

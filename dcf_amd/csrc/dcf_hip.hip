@@ -167,6 +167,19 @@ int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
 // subtrees under level S, each expanded by one workgroup.
 uint32_t prefix_split(uint32_t levels) { return levels > 18u ? 8u : (levels > 10u ? levels - 10u : 0u); }
 
+// Depth-first tail of k_prefix_build16: the last H levels, once the workgroup's level holds
+// at least one node per thread (2^10 = kBlock); DCF_PFX_DFS caps H (0: level by level only).
+#ifndef DCF_PFX_DFS
+#define DCF_PFX_DFS 4
+#endif
+#ifndef DCF_STREAM_NBC
+#define DCF_STREAM_NBC 1  // single-key stream eval instances with the x width fixed (N = 16, N = 4)
+#endif
+uint32_t prefix_dfs_levels(uint32_t levels, uint32_t S) {
+  const uint32_t cap = std::min<uint32_t>(DCF_PFX_DFS, kPfxDfsMax);
+  return levels >= S + 10u + 1u ? std::min<uint32_t>(cap, levels - S - 10u) : 0u;
+}
+
 // Shared-prefix depth for a single-key stream eval of `total` points (kernels_stream.h
 // PrefixTable): the top tree has 2^D nodes (33 B each, built with 2^(D+1) AES blocks)
 // and saves every point D levels.  Auto: D = log2(total) - 1 (table build < 1 block per
@@ -305,8 +318,9 @@ int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const 
   }
   if (p->kind == 0) {  // one launch: k_prefix_build16
     uint8_t* ba = p->d_pfx + tab_bytes;
+    const uint32_t H = prefix_dfs_levels(levels, S);
     hipLaunchKernelGGL(k_prefix_build16, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->rk[0], cws, cwv, cwt,
-                       (const uint4*)s0, (uint32_t)party, S, levels, ba, ba + ((size_t)1 << S) * region,
+                       (const uint4*)s0, (uint32_t)party, S, levels, H, ba, ba + ((size_t)1 << S) * region,
                        (uint64_t)region, R, (uint4*)p->d_pfx);
     HIP_TRY(hipGetLastError());
     *out = PrefixTable{(const uint4*)p->d_pfx, levels};
@@ -1000,14 +1014,20 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
       }
     }
     const bool pfx = DCF_STREAM_PFXT && pf.levels != 0;
-#define DCF_STREAM_K(XR, MK, PF, D4)                                                                          \
-  hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK, kBlock, false, PF, D4>), dim3((unsigned)blocks), block, 0, st, \
+#define DCF_STREAM_KN(XR, MK, PF, D4, NBC)                                                                    \
+  hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK, kBlock, false, PF, D4, NBC>), dim3((unsigned)blocks), block, 0, st, \
                      p->d_tab, p->rk[0], scs, cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, \
                      (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf, p->d_rk0)
+#define DCF_STREAM_K(XR, MK, PF, D4) DCF_STREAM_KN(XR, MK, PF, D4, 0)
+    // single key, x in registers: N = 16 (C1 / C3) and N = 4 (C2) with the x width fixed at
+    // compile time (a point's start loads x without width branches: C2 starts a point every
+    // ~13 AES slots)
 #define DCF_STREAM(XR, MK)                                                                                    \
   do {                                                                                                        \
     if (MK) DCF_STREAM_K(XR, MK, false, false);                                                               \
     else if (pfx) DCF_STREAM_K(XR, false, true, DCF_STREAM_D48 != 0);                                          \
+    else if (XR && DCF_STREAM_NBC && n_bytes == 16) DCF_STREAM_KN(XR, false, false, DCF_STREAM_D48 != 0, 16);    \
+    else if (XR && DCF_STREAM_NBC && n_bytes == 4) DCF_STREAM_KN(XR, false, false, DCF_STREAM_D48 != 0, 4);      \
     else DCF_STREAM_K(XR, false, false, DCF_STREAM_D48 != 0);                                                  \
   } while (0)
 #ifdef DCF_STREAM_TT2
@@ -1025,6 +1045,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     else DCF_STREAM(false, false);
 #undef DCF_STREAM
 #undef DCF_STREAM_K
+#undef DCF_STREAM_KN
   } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
     const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;

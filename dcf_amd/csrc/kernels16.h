@@ -604,10 +604,13 @@ __device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, co
 // the workgroup's own regions of two buffers (SoA: s[R] | v[R] | t[R], R = 2^(D-1-S)),
 // and the last level writes packed 32-B rows of the workgroup's contiguous block of the
 // table directly (no pack pass).  Same bytes as the level kernels + k_prefix_pack.
+// H > 0: the level-by-level part stops at level D - H (one node or more per thread) and
+// each thread expands its nodes' last H levels depth-first (see the tail below).
+constexpr uint32_t kPfxDfsMax = 4;  // H <= 4: a 3-slot stack of 9-word nodes (27 VGPRs; 5 slots spill to scratch)
 __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ s0,
-    const uint32_t party, const uint32_t S, const uint32_t D, uint8_t* __restrict__ buf_a,
+    const uint32_t party, const uint32_t S, const uint32_t D, const uint32_t H, uint8_t* __restrict__ buf_a,
     uint8_t* __restrict__ buf_b, const uint64_t region_bytes, const uint32_t region_nodes,
     uint4* __restrict__ table) {
   __shared__ uint32_t lds[kLdsWords];
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     }
   }
   __syncthreads();
-  for (uint32_t lev = S; lev < D; ++lev) {
+  for (uint32_t lev = S; lev < D - H; ++lev) {
     const uint32_t np = 1u << (lev - S);  // this workgroup's parents at level lev
     const bool last = lev + 1u == D;
     const uint4 cs = cw_s[lev], cv = cw_v[lev];
@@ -694,6 +697,71 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     uint8_t* tmp = X;
     X = Y;
     Y = tmp;
+  }
+  if (H == 0) return;
+  // Depth-first tail: thread j expands node j (j + blockDim, ...) of level B = D - H H
+  // levels down in registers — the right child of every expansion above the bottom waits
+  // on a stack (one slot per depth), the bottom expansion writes two rows — so the last H
+  // levels need neither barriers nor node traffic.  Leaf-parent i (0 .. 2^(H-1) - 1, bits
+  // Msb-first = the choices at depths 0 .. H-2) starts from the right child saved at the
+  // depth of i's lowest set bit, so every node is expanded exactly once.
+  const uint32_t B = D - H, nb = 1u << (B - S), nleafp = 1u << (H - 1u);
+  const uint4* xs_ = reinterpret_cast<const uint4*>(X);
+  const uint4* xv_ = xs_ + R;
+  const uint8_t* xt_ = X + (uint64_t)R * 32u;
+  for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+    uint32_t stk[kPfxDfsMax - 1][9];  // pending right children: s[4] | v[4] | t, by depth
+    uint32_t n[9];
+    {
+      const uint4 sv = xs_[j], vv = xv_[j];
+      n[0] = sv.x; n[1] = sv.y; n[2] = sv.z; n[3] = sv.w;
+      n[4] = vv.x; n[5] = vv.y; n[6] = vv.z; n[7] = vv.w;
+      n[8] = xt_[j];
+    }
+    uint4* rows = table + 2ull * (((uint64_t)w << (D - S)) + ((uint64_t)j << H));
+    for (uint32_t i = 0; i < nleafp; ++i) {
+      uint32_t k = 0;
+      if (i) {  // resume at the right child saved at depth H - 2 - ctz(i) (wave-uniform)
+        const uint32_t d = H - 2u - (uint32_t)__builtin_ctz(i);
+#pragma unroll
+        for (uint32_t q = 0; q + 1 < kPfxDfsMax; ++q)
+          if (q == d)
+#pragma unroll
+            for (int e = 0; e < 9; ++e) n[e] = stk[q][e];
+        k = d + 1u;
+      }
+      for (;; ++k) {  // expand depth k (level B + k)
+        const uint4 cs = cw_s[B + k], cv = cw_v[B + k];
+        const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+        const uint32_t s[4] = {n[0], n[1], n[2], n[3]}, v[4] = {n[4], n[5], n[6], n[7]};
+        uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
+        fd_children(lds, lc, rk, csw, cvw, cw_t[B + k], s, v, n[8], sl, vl, tl, sr, vr, tr);
+        if (k + 1u == H) {  // bottom: leaves 2i, 2i + 1 of this node's block of rows
+          uint4* row = rows + 4u * i;
+          row[0] = make_uint4(sl[0], sl[1], sl[2], (sl[3] & kMaskLast) | (tl << 24));
+          row[1] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+          row[2] = make_uint4(sr[0], sr[1], sr[2], (sr[3] & kMaskLast) | (tr << 24));
+          row[3] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
+          break;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q + 1 < kPfxDfsMax; ++q)
+          if (q == k) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              stk[q][e] = sr[e];
+              stk[q][4 + e] = vr[e];
+            }
+            stk[q][8] = tr;
+          }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          n[e] = sl[e];
+          n[4 + e] = vl[e];
+        }
+        n[8] = tl;
+      }
+    }
   }
 }
 

@@ -63,6 +63,9 @@ constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wav
 // stores, so a key load's wait can cover recent stores; the spill reloads cost less.
 #define DCF_MK_HK 0
 #endif
+#ifndef DCF_MK_SL
+#define DCF_MK_SL -1  // multi-key stream eval: k >= 0 = round keys 0..k-1 from SGPRs, k..14 from LDS (aes256_tt_sl)
+#endif
 #ifndef DCF_LDS_KEYS_LATE
 #define DCF_LDS_KEYS_LATE true  // ... read late (per round), so they are not all hoisted into VGPRs
 #endif
@@ -82,11 +85,12 @@ struct StreamLane {
   bool alive[NS];
 };
 
-template <int NS, bool XREG, bool MULTI, bool PFX = false>
+template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0>
 __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int i, uint64_t p,
                                              const uint4* __restrict__ s0s, const uint4 s0v, uint32_t party,
-                                             const uint8_t* __restrict__ xs, uint32_t nbytes, uint64_t ppk,
+                                             const uint8_t* __restrict__ xs, uint32_t nbytes_rt, uint64_t ppk,
                                              const PrefixTable& pf) {
+  const uint32_t nbytes = NBC ? (uint32_t)NBC : nbytes_rt;  // NBC: x width fixed at compile time
   const uint64_t k = MULTI ? p / ppk : 0;
   const uint8_t* row = xs + p * nbytes;
   uint32_t w0;  // first 32 x bits, Msb0 (lib.rs:181)
@@ -108,7 +112,11 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
   if (!MULTI && (PFX || pf.levels)) {  // start below the shared prefix: its row of the top-tree table
     lev0 = pf.levels;
     uint4 sv, vv;
+#ifdef DCF_EXP_NOGATHER  // timing experiment only (wrong bytes): row address independent of x
+    prefix_row(pf, (uint32_t)p & ((1u << lev0) - 1u), sv, vv, L.t[i]);
+#else
     prefix_row(pf, w0 >> (32u - lev0), sv, vv, L.t[i]);
+#endif
     L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
     L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
   } else {
@@ -139,7 +147,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
 
 // Give every lane whose stream i is free (`mine`) a new point, or retire the
 // stream when the counter is exhausted.  Called in wave-uniform control flow.
-template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit, bool PFX = false>
+template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit, bool PFX = false, int NBC = 0>
 __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint64_t& unext,
                                               uint64_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
                                               uint64_t nunits, uint64_t total, const uint4* __restrict__ s0s,
@@ -165,7 +173,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
     }
     const uint32_t rank = lane_rank(need);
     const bool take = mine && (uint64_t)rank < uend - unext;
-    if (take) stream_start<NS, XREG, MULTI, PFX>(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk, pf);
+    if (take) stream_start<NS, XREG, MULTI, PFX, NBC>(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk, pf);
     const uint64_t taken = __ballot(take);
     unext += (uint64_t)__popcll(taken);
     need &= ~taken;
@@ -232,13 +240,14 @@ __global__ void k_cw_rows48(const uint4* __restrict__ cw_s, const uint4* __restr
 
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
 template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false, int HK = 0,
-          bool PFX = false, bool D48 = false>
+          bool PFX = false, bool D48 = false, int SL = -1, int NBC = 0>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
-    const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes_rt,
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
     uint4* __restrict__ ys, const PrefixTable& pf) {
+  const uint32_t nbytes = NBC ? (uint32_t)NBC : nbytes_rt;
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
   const uint64_t nunits = (total + UNIT - 1) / UNIT;
@@ -256,7 +265,7 @@ __device__ __forceinline__ void stream_run(
   const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    stream_refill<NS, XREG, MULTI, UNIT, PFX>(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v,
+    stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v,
                                               party, xs, nbytes, ppk, pf);
 
   uint64_t nblk = 0;  // AES blocks this wave encrypts for live streams (wave-uniform)
@@ -331,6 +340,8 @@ __device__ __forceinline__ void stream_run(
       aes256_tt2<NS>(st, rk, lds, lc);
     } else if (GK) {  // round keys from global memory, loaded DCF_GK_AHEAD rounds ahead
       aes256_tt_gk<NS, PRE>(st, rkl, lds, lc);
+    } else if (SL >= 0) {  // keys 0..SL-1 from SGPRs, SL..14 from LDS (multi-key)
+      aes256_tt_sl<NS, (SL >= 0 ? SL : 0)>(st, rk, rkl, lds, lc);
     } else if (HK) {  // keys 0..HK-1 from SGPRs, HK..14 from global memory (multi-key)
       aes256_tt_hk<NS, (HK > 3 ? HK : 4)>(st, rk, rkl, lds, lc);
     } else if (LK) {  // round keys from LDS: one ds_read_b128 per round (see k_eval16_stream)
@@ -343,6 +354,14 @@ __device__ __forceinline__ void stream_run(
     }
 #ifdef DCF_PRIO_UPDATE
     __builtin_amdgcn_s_setprio(DCF_PRIO_UPDATE);
+#endif
+#ifdef DCF_EXP_PADVALU  // timing experiment only: K extra VALU instructions per iteration
+    {
+      uint32_t dz = lc;
+#pragma unroll
+      for (int q = 0; q < DCF_EXP_PADVALU; ++q) asm volatile("v_xor_b32 %0, %0, %0" : "+v"(dz));
+      asm volatile("" ::"v"(dz));
+    }
 #endif
     // Pin the CW loads above the update: without this the compiler sinks the
     // cw_t load into the (divergent) level-done path and waits on it there.
@@ -449,14 +468,18 @@ __device__ __forceinline__ void stream_run(
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
+#ifdef DCF_EXP_NOSTORE  // timing experiment only: no y store
+      if (done && L.t[i] == 7u) {
+#else
       if (done) {
+#endif
         const uint4 np = MULTI ? cw_np1[L.key[i]] : np1v;
         const uint32_t tm = 0u - L.t[i];
         ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
                                  L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
       }
       if (__ballot(done))
-        stream_refill<NS, XREG, MULTI, UNIT, PFX>(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s,
+        stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s,
                                                   s0v, party, xs, nbytes, ppk, pf);
     }
   }
@@ -465,7 +488,8 @@ __device__ __forceinline__ void stream_run(
 }
 
 // TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.
-template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false, bool PFX = false, bool D48 = false>
+template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false, bool PFX = false, bool D48 = false,
+          int NBC = 0>
 __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -491,7 +515,8 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   constexpr bool GK = DCF_STREAM_GK && !MULTI && !TT2;
   // Multi-key: keys DCF_MK_HK..14 from global memory (0 = all from SGPRs, which spill)
   constexpr int HK = (MULTI && !TT2) ? DCF_MK_HK : 0;
-  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48>(
+  constexpr int SL = (MULTI && !TT2) ? DCF_MK_SL : -1;
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC>(
       lds, (GK || HK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total, ctr,
       ys, pf);
 }

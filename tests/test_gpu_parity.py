@@ -143,12 +143,14 @@ def test_eval_random_vs_oracle(dcf, nb, mode):
 
 
 @pytest.mark.parametrize("nb,levels", [(1, 1), (1, 7), (2, 9), (2, 15), (3, 23), (4, 8), (4, 24), (5, 1),
-                                        (16, 13), (16, 24), (17, 20), (32, 24), (4, 26), (32, 30)])
+                                        (16, 13), (16, 24), (17, 20), (32, 24), (4, 26), (32, 30),
+                                        (4, 19), (4, 21), (16, 22)])
 def test_eval_prefix_table_vs_oracle(dcf, nb, levels):
     """Shared-prefix eval (stream engine, forced depth): points start at level D from
     the key's expanded top tree; the output must not change.  Covers D = 1, D = 8N - 1
     (the walk's last level only), D across x's word boundary (N = 3: 24 bits) and
-    the 28-level cap on a forced depth (N = 32, D = 30)."""
+    the 28-level cap on a forced depth (N = 32, D = 30); D = 19 / 20 / 21 / 22+ build the
+    last 1 / 2 / 3 / 4 levels depth-first (k_prefix_build16 tail)."""
     rng = np.random.default_rng(700 + 31 * nb + levels)
     keys = [rng.bytes(32) for _ in range(2)]
     prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
