@@ -436,7 +436,7 @@ def run_eval(args, world, rank):
             d, lambda b: dcf_amd.Share([sd[b].tobytes()], share.cws, share.cw_np1), xs, lam, parties,
             max(1, min(args.steps, 3)))
         out["host_path"]["matches_device_path"] = bool(np.array_equal(host_ys[0], ys.cpu().numpy()))
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # cpu_baseline: rank 0 at N=1 only
         ns = min(m, 1 << 26, max(4096, (1 << 30) // lam))  # at most ~1 GiB of outputs copied back
         xs_h = xs[:ns].cpu().numpy()
         ys_h = [ys[:ns].cpu().numpy()] + ([ys1[:ns].cpu().numpy()] if parties == 2 else [])
@@ -567,7 +567,7 @@ def run_c5(args, world, rank):
                         "note": "gen: 4 AES-256 blocks per level per key (k_gen16); eval: blocks the multi-key "
                                 "stream engine encrypts, counted on the device (B every level, A on left levels, "
                                 "minus reused B); peak = T-table LDS bound 87.8 G blocks/s"}}
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # cpu_baseline: rank 0 at N=1 only
         out["cpu_baseline"] = c5_cpu_baseline(keys, nb, lam, alpha, beta, s0, s1, xs, cwb, y0, y1, K, P,
                                               args.cpu_seconds)
     return out
@@ -677,7 +677,7 @@ def run_fd(args, world, rank):
                         "note": (f"{4 if mmo else 2} AES blocks per internal node (both children from one PRG "
                                  f"call), about {4 if mmo else 2} per leaf, vs {4 if mmo else 2} x 8N per point "
                                  "for pointwise eval")}}
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # cpu_baseline: rank 0 at N=1 only
         from oracle import oracle as O
         P = (O.OracleMmoPrg if mmo else O.OraclePrg)(keys, lam)
         cw = cwb.cpu().numpy().tobytes()

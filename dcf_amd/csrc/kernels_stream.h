@@ -66,6 +66,11 @@ constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wav
 #ifndef DCF_MK_SL
 #define DCF_MK_SL -1  // multi-key stream eval: k >= 0 = round keys 0..k-1 from SGPRs, k..14 from LDS (aes256_tt_sl)
 #endif
+#ifndef DCF_STREAM_LATE_STORE
+// 1: y store issued after the refill's loads.  r02 A/B (same box, 2 runs): C3 533.8 vs 538.4,
+// C2 4.06 vs 4.11 G evals/s — slower: the next stream's update still waits vmcnt(0) on it.
+#define DCF_STREAM_LATE_STORE 0
+#endif
 #ifndef DCF_LDS_KEYS_LATE
 #define DCF_LDS_KEYS_LATE true  // ... read late (per round), so they are not all hoisted into VGPRs
 #endif
@@ -464,10 +469,14 @@ __device__ __forceinline__ void stream_run(
 #endif
       L.lev[i] = nl;
     }
-    // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.
+    // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.  (vmcnt counts
+    // stores too, so the refill's wait for its x word also waits for this store; issuing it
+    // after the refill's loads instead, DCF_STREAM_LATE_STORE, measured slower.)
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
+      uint4 yv = make_uint4(0u, 0u, 0u, 0u);
+      uint64_t yp = 0;
 #ifdef DCF_EXP_NOSTORE  // timing experiment only: no y store
       if (done && L.t[i] == 7u) {
 #else
@@ -475,12 +484,18 @@ __device__ __forceinline__ void stream_run(
 #endif
         const uint4 np = MULTI ? cw_np1[L.key[i]] : np1v;
         const uint32_t tm = 0u - L.t[i];
-        ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
-                                 L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
+        yv = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
+                        L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
+        yp = L.pt[i];
+        if (!DCF_STREAM_LATE_STORE) ys[yp] = yv;
       }
       if (__ballot(done))
         stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s,
                                                   s0v, party, xs, nbytes, ppk, pf);
+      if (DCF_STREAM_LATE_STORE && done) {
+        asm volatile("" ::: "memory");  // keep the store below the refill's loads
+        ys[yp] = yv;
+      }
     }
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
