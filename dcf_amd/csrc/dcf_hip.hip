@@ -172,6 +172,14 @@ uint32_t prefix_split(uint32_t levels) { return levels > 18u ? 8u : (levels > 10
 #ifndef DCF_PFX_DFS
 #define DCF_PFX_DFS 4
 #endif
+// Full-domain eval: the last DCF_FD_TAIL levels in registers, depth-first (DCF_FD_DFS = 1,
+// k_fd_dfs16) or breadth-first (k_fd_tail16, 2^D nodes per lane: D <= 3).
+#ifndef DCF_FD_DFS
+#define DCF_FD_DFS 1
+#endif
+#ifndef DCF_FD_TAIL
+#define DCF_FD_TAIL (DCF_FD_DFS ? 4 : 3)  // depth-first 5: 128 VGPRs + scratch spills
+#endif
 #ifndef DCF_STREAM_NBC
 #define DCF_STREAM_NBC 1  // single-key stream eval instances with the x width fixed (N = 16, N = 4)
 #endif
@@ -1357,7 +1365,7 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   // Two ping-pong node buffers: s (16 B), v (16 B), t (1 B) per node.  With the
   // Hirose PRG the last kFdTail levels run in registers (k_fd_tail16), so the widest
   // node level in HBM is 2^(n - kFdTail).
-  constexpr uint32_t kFdTail = 3;
+  constexpr uint32_t kFdTail = DCF_FD_TAIL;
   const bool fused = p->kind == 0 && nlev > kFdTail;
   const uint64_t maxnodes = fused ? (npts >> kFdTail) : npts / 2;
   const size_t nodeb = 33;
@@ -1400,8 +1408,13 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   }
   if (fused) {
     const uint64_t nodes = 1ull << lev_end;
-    hipLaunchKernelGGL(k_fd_tail16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
-                       p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63, DCF_FD_GK ? p->d_rk0 : nullptr);
+    if (DCF_FD_DFS)  // depth-first in registers (k_fd_dfs16)
+      hipLaunchKernelGGL(k_fd_dfs16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                         p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63);
+    else
+      hipLaunchKernelGGL(k_fd_tail16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                         p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63,
+                         DCF_FD_GK ? p->d_rk0 : nullptr);
     HIP_TRY(hipGetLastError());
   }
   return DCF_OK;

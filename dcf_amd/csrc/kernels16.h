@@ -765,6 +765,86 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
   }
 }
 
+// Last H levels of the full-domain expansion depth-first (as k_prefix_build16's tail): one
+// lane per node at level nlev - H expands its subtree with a register stack of pending right
+// children (one 9-word slot per depth above the bottom), so the node state in registers grows
+// with H, not 2^H as in k_fd_tail16, and H = 4..5 fits.  Leaf-parent i (bits Msb-first = the
+// choices at depths 0 .. H-2) resumes from the slot at the depth of i's lowest set bit; its
+// expansion writes y for leaves 2i, 2i + 1 of the node's 2^H contiguous outputs.
+template <int H>
+__global__ __launch_bounds__(kBlock, 1) void k_fd_dfs16(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
+    const uint32_t lev0, const uint64_t nnodes, const uint4* __restrict__ s_in, const uint4* __restrict__ v_in,
+    const uint8_t* __restrict__ t_in, uint4* __restrict__ ys, uint32_t* __restrict__ ctr) {
+  static_assert(H >= 2 && H <= 6, "depth-first tail of 2..6 levels");
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint4 np = cw_np1[0];
+  const uint32_t unit = fd_unit(nnodes);
+  for (uint64_t base = next_unit_base_n(ctr, ~0ull, unit); base < nnodes;
+       base = next_unit_base_n(ctr, base, unit)) {
+    const uint64_t j = base + (threadIdx.x & 63u);
+    const bool live = j < nnodes;
+    const uint64_t jj = live ? j : nnodes - 1;
+    uint32_t stk[H - 1][9];  // pending right children: s[4] | v[4] | t, by depth
+    uint32_t n[9];
+    {
+      const uint4 sv = s_in[jj], vv = v_in[jj];
+      n[0] = sv.x; n[1] = sv.y; n[2] = sv.z; n[3] = sv.w;
+      n[4] = vv.x; n[5] = vv.y; n[6] = vv.z; n[7] = vv.w;
+      n[8] = t_in[jj];
+    }
+    uint4* y = ys + (jj << H);
+    for (uint32_t i = 0; i < (1u << (H - 1)); ++i) {
+      uint32_t k = 0;
+      if (i) {  // resume at the right child saved at depth H - 2 - ctz(i) (wave-uniform)
+        const uint32_t d = (uint32_t)(H - 2) - (uint32_t)__builtin_ctz(i);
+#pragma unroll
+        for (uint32_t q = 0; q + 1 < (uint32_t)H; ++q)
+          if (q == d)
+#pragma unroll
+            for (int e = 0; e < 9; ++e) n[e] = stk[q][e];
+        k = d + 1u;
+      }
+      for (;; ++k) {  // expand depth k (level lev0 + k)
+        const uint4 cs = cw_s[lev0 + k], cv = cw_v[lev0 + k];
+        const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+        const uint32_t s[4] = {n[0], n[1], n[2], n[3]}, v[4] = {n[4], n[5], n[6], n[7]};
+        uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
+        fd_children(lds, lc, rk, csw, cvw, cw_t[lev0 + k], s, v, n[8], sl, vl, tl, sr, vr, tr);
+        if (k + 1u == (uint32_t)H) {  // leaves: y = v ^ s ^ t * cw_np1 (lib.rs:192)
+          if (live) {
+            const uint32_t ml = 0u - tl, mr = 0u - tr;
+            y[2 * i] = make_uint4(vl[0] ^ sl[0] ^ (ml & np.x), vl[1] ^ sl[1] ^ (ml & np.y),
+                                  vl[2] ^ sl[2] ^ (ml & np.z), vl[3] ^ sl[3] ^ (ml & np.w));
+            y[2 * i + 1] = make_uint4(vr[0] ^ sr[0] ^ (mr & np.x), vr[1] ^ sr[1] ^ (mr & np.y),
+                                      vr[2] ^ sr[2] ^ (mr & np.z), vr[3] ^ sr[3] ^ (mr & np.w));
+          }
+          break;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q + 1 < (uint32_t)H; ++q)
+          if (q == k) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              stk[q][e] = sr[e];
+              stk[q][4 + e] = vr[e];
+            }
+            stk[q][8] = tr;
+          }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          n[e] = sl[e];
+          n[4 + e] = vl[e];
+        }
+        n[8] = tl;
+      }
+    }
+  }
+}
+
 // Root node for full-domain eval: s = s0 (k.s0s[0]), v = 0, t = party.
 __global__ void k_fd_root16(const uint4* __restrict__ s0, const uint32_t party, uint4* __restrict__ s,
                             uint4* __restrict__ v, uint8_t* __restrict__ t) {
