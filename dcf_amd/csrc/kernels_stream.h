@@ -117,11 +117,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
   if (!MULTI && (PFX || pf.levels)) {  // start below the shared prefix: its row of the top-tree table
     lev0 = pf.levels;
     uint4 sv, vv;
-#ifdef DCF_EXP_NOGATHER  // timing experiment only (wrong bytes): row address independent of x
-    prefix_row(pf, (uint32_t)p & ((1u << lev0) - 1u), sv, vv, L.t[i]);
-#else
     prefix_row(pf, w0 >> (32u - lev0), sv, vv, L.t[i]);
-#endif
     L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
     L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
   } else {
@@ -360,14 +356,6 @@ __device__ __forceinline__ void stream_run(
 #ifdef DCF_PRIO_UPDATE
     __builtin_amdgcn_s_setprio(DCF_PRIO_UPDATE);
 #endif
-#ifdef DCF_EXP_PADVALU  // timing experiment only: K extra VALU instructions per iteration
-    {
-      uint32_t dz = lc;
-#pragma unroll
-      for (int q = 0; q < DCF_EXP_PADVALU; ++q) asm volatile("v_xor_b32 %0, %0, %0" : "+v"(dz));
-      asm volatile("" ::"v"(dz));
-    }
-#endif
     // Pin the CW loads above the update: without this the compiler sinks the
     // cw_t load into the (divergent) level-done path and waits on it there.
 #pragma unroll
@@ -477,11 +465,7 @@ __device__ __forceinline__ void stream_run(
       const bool done = L.alive[i] && L.lev[i] == nlev;
       uint4 yv = make_uint4(0u, 0u, 0u, 0u);
       uint64_t yp = 0;
-#ifdef DCF_EXP_NOSTORE  // timing experiment only: no y store
-      if (done && L.t[i] == 7u) {
-#else
       if (done) {
-#endif
         const uint4 np = MULTI ? cw_np1[L.key[i]] : np1v;
         const uint32_t tm = 0u - L.t[i];
         yv = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),

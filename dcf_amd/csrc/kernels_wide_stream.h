@@ -295,18 +295,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
   }
 }
 
-// Root of the wide prefix tree: s = k.s0s[0][0:32), v = 0, t = party (lib.rs:167-169);
-// t-vector row 0 = t_0 = party.
-__global__ void k_wpfx_root(const uint8_t* __restrict__ s0p, const uint32_t party, uint4* __restrict__ out) {
-  if (threadIdx.x == 0) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(s0p);
-    out[0] = s4[0];
-    out[1] = s4[1];
-    out[2] = out[3] = make_uint4(0u, 0u, 0u, 0u);
-    out[4] = make_uint4(party, 0u, party, 0u);
-  }
-}
-
 // One wide prefix node (80 B: s[0:32) | v[0:32) | {t, t-vector word 0, partial word, 0})
 // at depth `lev` -> its two children, bytes [0,32) of the walk exactly as
 // k_eval_wide_head_stream updates them: A = E0(s_lo), B = E0(~s_lo) (left),
@@ -378,8 +366,8 @@ __device__ __forceinline__ void wpfx_children(const uint32_t* lds, uint32_t lc, 
 
 // The whole wide prefix tree of depth D in ONE launch (as k_prefix_build16 at LAMBDA = 16):
 // workgroup w (2^S of them) owns the subtree under node w of level S; wave 0 walks the
-// root path (root = k.s0s[0][0:32), v = 0, t = party, t-vector row 0 = party, as
-// k_wpfx_root), then the workgroup expands its subtree level by level with workgroup
+// root path (root = k.s0s[0][0:32), v = 0, t = party, t-vector row 0 = party:
+// lib.rs:167-169), then the workgroup expands its subtree level by level with workgroup
 // barriers only, ping-ponging through its own regions (R = 2^(D-1-S) nodes of 80 B) of
 // two buffers; the last level writes the workgroup's contiguous block of the table.
 template <bool MASK_HEAD>
