@@ -179,6 +179,58 @@ __device__ __forceinline__ void aes256_tt(uint32_t (&st)[NB][4], const RoundKeys
     for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
 }
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// 16 bytes at an LDS byte address: ds_read takes the address as is (a generic
+// pointer into an extern __shared__ array costs a v_add of the array base per read).
+__device__ __forceinline__ uint4 lds_load16(uint32_t a) {
+  const u32x4_t v = *(__attribute__((address_space(3))) const u32x4_t*)(size_t)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// NB independent AES-NR encryptions, each under the round keys at LDS byte address ka[b]
+// (+16 per round: the offset rides in the ds_read_b128 immediate, no address VALU).
+// PRE: the caller has XORed round key 0 into st already (into its own input XOR).
+template <int NR, int NB, bool PRE>
+__device__ __forceinline__ void aes_tt_lka(uint32_t (&st)[NB][4], const uint32_t (&ka)[NB], const uint32_t* lds,
+                                           uint32_t lc) {
+  if (!PRE) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint4 k = lds_load16(ka[b]);
+      st[b][0] ^= k.x; st[b][1] ^= k.y; st[b][2] ^= k.z; st[b][3] ^= k.w;
+    }
+  }
+#pragma unroll
+  for (int r = 1; r <= NR; ++r) {
+    uint32_t o[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const uint4 k = lds_load16(ka[b] + 16u * r);
+      const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (r < NR) {
+          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
+        } else {  // final round: S(x) sits in byte r of T_{(r+2)&3}
+          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(__builtin_amdgcn_perm(c, a, 0x0c0c0500u), __builtin_amdgcn_perm(e, d, 0x07020c0cu), kw[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+}
+
 // NB independent AES encryptions with NR rounds (10: AES-128, 14: AES-256), each
 // under its own key schedule read from LDS: rk[b] points at NR + 1 uint4 round
 // keys (per lane, so a lane may pick its schedule; lanes reading the same

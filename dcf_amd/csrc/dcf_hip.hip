@@ -460,10 +460,13 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
       uint64_t blocks = (units + 15) / 16;
       if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
 #ifndef DCF_WHS_NS
-#define DCF_WHS_NS 1  // points per lane (2 spills: 128 VGPRs)
+#define DCF_WHS_NS 1  // points per lane
+#endif
+#ifndef DCF_WHS_WG
+#define DCF_WHS_WG kBlock  // threads per workgroup (one workgroup per CU: the T-tables fill the LDS)
 #endif
 #define DCF_WHS(MH, XR)                                                                                        \
-  hipLaunchKernelGGL((k_eval_wide_head_stream<DCF_WHS_NS, MH, XR>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab,     \
+  hipLaunchKernelGGL((k_eval_wide_head_stream<DCF_WHS_NS, MH, XR, DCF_WHS_WG>), dim3((unsigned)blocks), dim3(DCF_WHS_WG), 0, st, p->d_tab,     \
                      p->d_rk2, (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
                      lam, K, key, cnt, p->d_ctr, ys + off * lam, tvec, wpf)
       const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16;

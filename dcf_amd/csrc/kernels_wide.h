@@ -181,13 +181,6 @@ __device__ __forceinline__ uint4 w_row_piece(const uint8_t* __restrict__ cw_s, c
 #ifndef DCF_TAIL_BATCH
 #define DCF_TAIL_BATCH 2
 #endif
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-// 16 bytes at an LDS byte address: ds_read takes the address as is (a generic
-// pointer into an extern __shared__ array costs a v_add of the array base per read).
-__device__ __forceinline__ uint4 lds_load16(uint32_t a) {
-  const u32x4_t v = *(__attribute__((address_space(3))) const u32x4_t*)(size_t)a;
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
 
 __device__ __forceinline__ void tail_load_t(uint4 (&d)[4], const uint4* __restrict__ tv4, uint64_t pp, uint64_t p1) {
   pp = min<uint64_t>(pp, p1 - 1);

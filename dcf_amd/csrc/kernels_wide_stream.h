@@ -19,6 +19,16 @@
 
 namespace {
 
+__device__ __forceinline__ uint32_t xand(uint32_t a, uint32_t m, uint32_t c) {  // a ^ (m & c)
+  return __builtin_amdgcn_bitop3_b32(a, m, c, 0x78);
+}
+__device__ __forceinline__ uint32_t xandn(uint32_t a, uint32_t m, uint32_t c) {  // a ^ (m & ~c)
+  return __builtin_amdgcn_bitop3_b32(a, m, c, 0xB4);
+}
+__device__ __forceinline__ uint32_t pick(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b, m = 0 or ~0
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
+}
+
 // Shared prefix for the stream head (as kernels16.h PrefixTable at LAMBDA = 16): the
 // key's top `levels` tree levels expanded once, one 80-byte node per prefix:
 // rows[5 i .. 5 i + 5) = s[0:32) | v[0:32) | {t, t-vector word 0, partial t-vector word, 0}.
@@ -137,8 +147,8 @@ __global__ void k_cw_digest(const uint8_t* __restrict__ cw_s, const uint8_t* __r
 }
 
 // Single key `key` of a num_keys-key CWB; count <= 2^20 points per launch.
-template <int NS, bool MASK_HEAD, bool XREG>
-__global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
+template <int NS, bool MASK_HEAD, bool XREG, int WG = kBlock>
+__global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
     const uint8_t* __restrict__ dig_t, const uint8_t* __restrict__ cw_np1,
     const uint8_t* __restrict__ s0p, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
@@ -150,6 +160,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
   __shared__ uint4 rks[23 + 15];
   if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
   lds_fill_tables(lds, tab);  // its barrier also publishes rks
+  const uint32_t rks_a = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)rks;  // LDS byte address
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
   const uint64_t nunits = (count + kStreamUnit - 1) / kStreamUnit;
@@ -173,39 +184,48 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
 #pragma unroll
     for (int i = 0; i < NS; ++i) any = any || L.alive[i];
     if (!__ballot(any)) break;
-    // Correction words, needed only on the step that ends a level: bytes [0,32) of cw_s /
-    // cw_v from the compact per-key digest (64 B per level, 8 KiB, L1-resident; the CWB
-    // rows are LAMBDA bytes apart, one cache line per lane).  Issued before the AES and
+    // Correction words, used only on the step that ends a level (the update masks them with
+    // am): bytes [0,32) of cw_s / cw_v from the compact per-key digest (64 B per level,
+    // 8 KiB, L1-resident; the CWB rows are LAMBDA bytes apart, one cache line per lane).
+    // Loaded on every step (the level clamped for idle streams): under a branch they cost
+    // 17 zeroing moves per step and the loads issued anyway.  Issued before the AES and
     // pinned after it, so they are waited on long after the last y / t-vector stores
     // (vmcnt is in order: a load issued after a store cannot be waited on alone).
     uint4 cs[NS][2], cv[NS][2];
     uint32_t ct[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
-      const bool end = L.alive[i] && (((ph == 1u) & (xb == 0u)) | (ph == 2u));
-      cs[i][0] = cs[i][1] = cv[i][0] = cv[i][1] = make_uint4(0u, 0u, 0u, 0u);
-      ct[i] = 0u;
-      if (end) {
-        const uint4* d4 = dig + 4u * L.lev[i];
-        cs[i][0] = d4[0]; cs[i][1] = d4[1];
-        cv[i][0] = d4[2]; cv[i][1] = d4[3];
-        ct[i] = dig_t[L.lev[i]];
-      }
+      const uint32_t lv = min(L.lev[i], nlev - 1u);
+      const uint4* d4 = dig + 4u * lv;
+      cs[i][0] = d4[0]; cs[i][1] = d4[1];
+      cv[i][0] = d4[2]; cv[i][1] = d4[3];
+      ct[i] = dig_t[lv];
     }
-    // Block of this step: B (ph 0), then A (ph 1, left) or D (ph 1, right), C (ph 2).
-    uint32_t st[NS][4];
-    const uint4* rk[NS];
+    // Block of this step: B (ph 0), then A (ph 1, left) or D (ph 1, right), C (ph 2).  The
+    // lane's 16-byte half (sel) stays live: d = E(sel ^ inv) ^ sel ^ inv is one 3-input XOR.
+    uint32_t st[NS][4], sel[NS][4], inv[NS];
+    uint32_t ka[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
       const uint32_t hi = (ph != 0u) & xb;                            // D or C: bytes [16,32), cipher 17
-      const uint32_t inv = 0u - ((ph == 0u) | ((ph == 1u) & xb));    // B or D: ~s
-      rk[i] = rks + 23u * hi;
+      inv[i] = 0u - ((ph == 0u) | ((ph == 1u) & xb));                // B or D: ~s
+      // cipher 17's schedule sits 23 slots on.  The empty asm keeps the compiler from
+      // re-associating base + 16 r (rks_a is a link-time symbol: 14 materialised constants and
+      // a v_mad per round); the mask proves the sign bit clear, so +16 r folds into ds_read
+      uint32_t kb = rks_a + 368u * hi;
+      asm volatile("" : "+v"(kb));
+      ka[i] = kb & 0x3FFFFu;
+      const uint32_t hm = 0u - hi;
+      const uint4 k0 = lds_load16(ka[i]);
+      const uint32_t k0w[4] = {k0.x, k0.y, k0.z, k0.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) st[i][j] = (hi ? L.s[i][4 + j] : L.s[i][j]) ^ inv;
+      for (int j = 0; j < 4; ++j) {
+        sel[i][j] = pick(hm, L.s[i][4 + j], L.s[i][j]);
+        st[i][j] = xor3(sel[i][j], inv[i], k0w[j]);  // round key 0 folded in
+      }
     }
-    aes_tt_lk<14, NS>(st, rk, lds, lc);
+    aes_tt_lka<14, NS, true>(st, ka, lds, lc);
 #pragma unroll
     for (int i = 0; i < NS; ++i)
       asm volatile("" : "+v"(cs[i][0].x), "+v"(cs[i][0].y), "+v"(cs[i][0].z), "+v"(cs[i][0].w), "+v"(cs[i][1].x),
@@ -226,30 +246,35 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head_stream(
       // d = E(in) ^ in: the PRG output block (prg.rs:57-62)
       uint32_t d[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t hi = (ph != 0u) & xb;
-        const uint32_t inv = 0u - ((ph == 0u) | ((ph == 1u) & xb));
-        d[j] = st[i][j] ^ ((hi ? L.s[i][4 + j] : L.s[i][j]) ^ inv);
-      }
+      for (int j = 0; j < 4; ++j) d[j] = xor3(st[i][j], sel[i][j], inv[i]);
       L.tR[i] = mB ? (d[0] & 1u) : L.tR[i];  // t_R = lsb(B ^ ~s)[0] (prg.rs:64)
       const uint32_t tb = ((mA ? d[0] : L.tR[i]) & 1u) ^ (L.t[i] & (ct[i] >> xb) & 1u);  // lib.rs:179-180
       const uint32_t csw[8] = {cs[i][0].x, cs[i][0].y, cs[i][0].z, cs[i][0].w,
                                cs[i][1].x, cs[i][1].y, cs[i][1].z, cs[i][1].w};
       const uint32_t cvw[8] = {cv[i][0].x, cv[i][0].y, cv[i][0].z, cv[i][0].w,
                                cv[i][1].x, cv[i][1].y, cv[i][1].z, cv[i][1].w};
+      // Three-input forms (one v_bitop3 each): xand(a, m, c) = a ^ (m & c),
+      // xandn(a, m, c) = a ^ (m & ~c), pick(m, a, b) = m ? a : b (m all-ones or zero).
+      const uint32_t amtm = am & tm;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {  // bytes [0,16): AES on the left branch only
-        // v ^= v_hat: B ^ ~s (left, at the B step) or ~s (right, at the C step); then t*cw.v
-        L.v[i][j] ^= (mBl & d[j]) ^ (mC & ~L.s[i][j]) ^ (am & tm & cvw[j]);
-        const uint32_t sn = mA ? d[j] : L.s[i][j];
-        L.s[i][j] = adv ? (sn ^ (tm & csw[j])) : L.s[i][j];
+        // v ^= v_hat ^ t*cw.v: v_hat = B ^ ~s (left, at the B step) or ~s (right, at the C step)
+        L.v[i][j] = xandn(xand(xand(L.v[i][j], amtm, cvw[j]), mBl, d[j]), mC, L.s[i][j]);
+        // level end: s' = (A ^ s on the left, s on the right) ^ t*cw.s (lib.rs:177-178)
+        L.s[i][j] = xand(pick(mA, d[j], L.s[i][j]), amtm, csw[j]);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {  // bytes [16,32): AES on the right branch only
-        const uint32_t msk = (j == 3) ? mlast : 0xFFFFFFFFu;
-        L.v[i][4 + j] ^= (((mD & d[j]) ^ (mA & ~L.s[i][4 + j])) & msk) ^ (am & tm & cvw[4 + j]);
-        const uint32_t sn = (mC ? d[j] : L.s[i][4 + j]) & msk;
-        L.s[i][4 + j] = adv ? (sn ^ (tm & csw[4 + j])) : L.s[i][4 + j];
+      for (int j = 0; j < 3; ++j) {  // bytes [16,28): AES on the right branch only
+        // v ^= v_hat ^ t*cw.v: v_hat = D ^ ~s (right, at the D step) or ~s (left, at the A step)
+        L.v[i][4 + j] = xandn(xand(xand(L.v[i][4 + j], amtm, cvw[4 + j]), mD, d[j]), mA, L.s[i][4 + j]);
+        // level end: s' = (C ^ s on the right, s on the left) ^ t*cw.s
+        L.s[i][4 + j] = xand(pick(mC, d[j], L.s[i][4 + j]), amtm, csw[4 + j]);
+      }
+      {  // bytes [28,32): as above, with the cleared bit when LAMBDA == 32 (mlast)
+        const uint32_t vh = xandn(mD & d[3], mA, L.s[i][7]) & mlast;
+        L.v[i][7] = xand(L.v[i][7] ^ vh, amtm, cvw[7]);
+        const uint32_t sn = xand(pick(mC, d[3], L.s[i][7]) & mlast, tm, csw[7]);
+        L.s[i][7] = pick(am, sn, L.s[i][7]);  // an idle step keeps s (the root seed may be unmasked)
       }
       L.t[i] = adv ? tb : L.t[i];
       L.ph[i] = mB ? 1u : (mD ? 2u : 0u);
