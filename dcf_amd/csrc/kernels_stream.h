@@ -66,6 +66,10 @@ constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wav
 #ifndef DCF_MK_SL
 #define DCF_MK_SL -1  // multi-key stream eval: k >= 0 = round keys 0..k-1 from SGPRs, k..14 from LDS (aes256_tt_sl)
 #endif
+#ifndef DCF_REFILL_ONCE
+#define DCF_REFILL_ONCE 1  // refill: assign point indices in the loop, start the stream once after it
+                           // (single-key instances with the x width fixed, NBC)
+#endif
 #ifndef DCF_STREAM_LATE_STORE
 // 1: y store issued after the refill's loads.  r02 A/B (same box, 2 runs): C3 533.8 vs 538.4,
 // C2 4.06 vs 4.11 G evals/s — slower: the next stream's update still waits vmcnt(0) on it.
@@ -154,7 +158,42 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
                                               uint64_t nunits, uint64_t total, const uint4* __restrict__ s0s,
                                               const uint4 s0v, uint32_t party, const uint8_t* __restrict__ xs,
                                               uint32_t nbytes, uint64_t ppk, const PrefixTable& pf) {
+  // The loop only hands out point indices; the stream state is written once after it
+  // (DCF_REFILL_ONCE), so it is not a loop-carried value (no copies of it per pass).
   uint64_t need = __ballot(mine);
+  // (single key, x width fixed: the multi-key and runtime-width instances spill VGPRs with it)
+  constexpr bool ONCE = DCF_REFILL_ONCE && !MULTI && NBC != 0;
+  if (ONCE) {
+    uint64_t pnew = 0;
+    bool got = false;
+    while (need) {
+      if (unext >= uend && !exhausted) {
+        const uint32_t u = dequeue_unit(ctr);
+        if (u >= nunits) {
+          exhausted = true;
+        } else {
+          unext = (uint64_t)u * UNIT;
+          uend = min(unext + (uint64_t)UNIT, total);
+        }
+      }
+      if (exhausted && unext >= uend) break;
+      const uint32_t rank = lane_rank(need);
+      const bool take = mine && (uint64_t)rank < uend - unext;
+      pnew = take ? unext + rank : pnew;
+      got = got || take;
+      const uint64_t taken = __ballot(take);
+      unext += (uint64_t)__popcll(taken);
+      need &= ~taken;
+      mine = mine && !take;
+    }
+    if (got) {
+      stream_start<NS, XREG, MULTI, PFX, NBC>(L, i, pnew, s0s, s0v, party, xs, nbytes, ppk, pf);
+    } else if (mine) {  // nothing left: the stream retires
+      L.alive[i] = false;
+      L.ci[i] = 0;  // keep the idle stream's CW loads in bounds
+    }
+    return;
+  }
   while (need) {
     if (unext >= uend && !exhausted) {
       const uint32_t u = dequeue_unit(ctr);
