@@ -122,9 +122,24 @@ struct Sel {
       ((T & 1) ? 1u : 0u) | ((4u + K) << 8) | (((T >> 1) ? 2u : 0x0cu) << 16) | (0x0cu << 24);
 };
 
+#ifndef DCF_T1_BITOP3
+// 1: T1 lookups of the middle rounds address through v_bitop3 instead of v_perm.  Same bytes;
+// A/B (ab_t1, same box, 2 runs, M evals/s): C3 541.8 vs 540.8, C2 4124 vs 4113, C5 397.3 vs
+// 395.2, FD 37496 vs 37557, C4 103.4 vs 104.6, C1 195.4 vs 197.7 — noise: the loops sit at the
+// LDS-issue ceiling of the T-table rounds (scripts/micro/aes_rate.hip: 74.6 vs 75.2 G blocks/s).
+#define DCF_T1_BITOP3 0
+#endif
 template <int T, int K>
 __device__ __forceinline__ uint32_t lk(const uint32_t* lds, uint32_t w, uint32_t lc) {
-  const uint32_t addr = __builtin_amdgcn_perm(w, lc, Sel<T, K>::v);
+  uint32_t addr;
+  if (DCF_T1_BITOP3 && T == 1 && K == 1) {
+    // T1 takes state byte 1, which already sits at address bits 8..15: the address is
+    // (w & 0xFF00) | (T1's lane bits), one v_bitop3 (2 cycles per wave64 on gfx950) instead
+    // of a v_perm (4 cycles).  (lc >> 8) & 0xFF is loop-invariant: the compiler hoists it.
+    addr = __builtin_amdgcn_bitop3_b32(w, 0xFF00u, (lc >> 8) & 0xFFu, 0xEA);  // (a & b) | c
+  } else {
+    addr = __builtin_amdgcn_perm(w, lc, Sel<T, K>::v);
+  }
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + addr);
 }
 

@@ -1,0 +1,153 @@
+// Micro-benchmark: AES-256 throughput of the LDS T-table rounds alone (no DCF walk), one
+// 1024-thread workgroup per CU (as the eval kernels), NB independent chains per lane,
+// round keys from SGPRs (aes256_tt) or per round from global memory (aes256_tt_gk).
+// Tells how much of the stream kernel's gap to the LDS bound is the AES itself.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include scripts/micro/aes_rate.hip -o scripts/micro/aes_rate
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+#include "../../dcf_amd/csrc/aes_lds.h"
+
+constexpr int kIters = 2048;
+
+// T1 lookups of the middle rounds through one v_bitop3 ((w & 0xFF00) | lc1: the state byte
+// already sits at address bits 8..15) instead of a v_perm.
+template <int NB>
+__device__ __forceinline__ void aes256_tt_b(uint32_t (&st)[NB][4], const RoundKeys& rk, const uint32_t* lds,
+                                            uint32_t lc, uint32_t lc1) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] ^= rk.w[j];
+#pragma unroll
+  for (int r = 1; r < 14; ++r) {
+    uint32_t o[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+        const uint32_t ad = __builtin_amdgcn_bitop3_b32(st[b][(j + 1) & 3], 0xFF00u, lc1, 0xEA);
+        const uint32_t c = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + ad);
+        const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+        const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+        o[b][j] = xor3(xor3(a, c, d), e, rk.w[4 * r + j]);
+      }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+  uint32_t o[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+      const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+      const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+      const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+      const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
+      const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
+      o[b][j] = xor3(lo, hi, rk.w[56 + j]);
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+}
+
+template <int NB, int MODE>
+__global__ __launch_bounds__(1024, 1) void k_aes(const uint32_t* __restrict__ tab, const RoundKeys rk,
+                                                 const uint4* __restrict__ rkg, uint32_t* out) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint32_t lc1 = (lc >> 8) & 0xFFu;  // T1's lane bits, state byte 1 goes to bits 8..15
+  uint32_t st[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] = (blockIdx.x * 1024 + threadIdx.x) * 0x9E3779B9u + 77u * b + j;
+  for (int it = 0; it < kIters; ++it) {
+    if (MODE == 0) aes256_tt<NB>(st, rk, lds, lc);
+    if (MODE == 1) aes256_tt_gk<NB>(st, rkg, lds, lc);
+    if (MODE == 2) aes256_tt_b<NB>(st, rk, lds, lc, lc1);
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r ^= st[b][j];
+  if (out) out[blockIdx.x * 1024 + threadIdx.x] = r;
+}
+
+template <int NB, int MODE>
+void run(const char* name, int cus, const uint32_t* dtab, const RoundKeys& rk, const uint4* rkg, uint32_t* out,
+         int wgs_per_cu) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const int grid = cus * wgs_per_cu;
+  for (int rep = 0; rep < 2; ++rep) {
+    hipEventRecord(e0);
+    hipLaunchKernelGGL((k_aes<NB, MODE>), dim3(grid), dim3(1024), 0, 0, dtab, rk, rkg, out);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (rep == 1) {
+      const double blocks = (double)grid * 1024 * NB * kIters;
+      printf("%-28s NB=%d %8.3f ms  %6.2f G blocks/s  (%.3f of the 87.8 LDS bound)\n", name, NB, ms,
+             blocks / (ms * 1e-3) / 1e9, blocks / (ms * 1e-3) / 87.77e9);
+    }
+  }
+}
+
+int main() {
+  int cus = 0;
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  std::call_once(g_aes_once, aes_init_tables);
+  uint8_t key[32];
+  for (int i = 0; i < 32; ++i) key[i] = (uint8_t)(i * 7 + 1);
+  RoundKeys rk;
+  aes256_expand_words(key, &rk);
+  uint32_t *dtab, *out;
+  uint4* rkg;
+  hipMalloc(&dtab, sizeof(g_tab));
+  hipMalloc(&rkg, 240);
+  hipMalloc(&out, (size_t)cus * 16 * 1024 * 4);
+  hipMemcpy(dtab, g_tab, sizeof(g_tab), hipMemcpyHostToDevice);
+  hipMemcpy(rkg, rk.w, 240, hipMemcpyHostToDevice);
+  printf("CUs %d\n", cus);
+  for (int w : {4, 16}) {
+    printf("-- %d workgroups per CU (work items in flight)\n", w);
+    run<1, 0>("sgpr keys", cus, dtab, rk, rkg, out, w);
+    run<2, 0>("sgpr keys", cus, dtab, rk, rkg, out, w);
+    run<3, 0>("sgpr keys", cus, dtab, rk, rkg, out, w);
+    run<4, 0>("sgpr keys", cus, dtab, rk, rkg, out, w);
+    run<2, 1>("global keys (3 ahead)", cus, dtab, rk, rkg, out, w);
+    run<3, 1>("global keys (3 ahead)", cus, dtab, rk, rkg, out, w);
+    run<4, 1>("global keys (3 ahead)", cus, dtab, rk, rkg, out, w);
+    run<2, 2>("sgpr keys, T1 by bitop3", cus, dtab, rk, rkg, out, w);
+    run<3, 2>("sgpr keys, T1 by bitop3", cus, dtab, rk, rkg, out, w);
+  }
+  // same outputs as the v_perm rounds?
+  {
+    const int n = cus * 1024;
+    uint32_t* o2;
+    hipMalloc(&o2, n * 4);
+    hipLaunchKernelGGL((k_aes<2, 0>), dim3(cus), dim3(1024), 0, 0, dtab, rk, rkg, out);
+    hipLaunchKernelGGL((k_aes<2, 2>), dim3(cus), dim3(1024), 0, 0, dtab, rk, rkg, o2);
+    std::vector<uint32_t> h1(n), h2(n);
+    hipMemcpy(h1.data(), out, n * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(h2.data(), o2, n * 4, hipMemcpyDeviceToHost);
+    int bad = 0;
+    for (int i = 0; i < n; ++i) bad += h1[i] != h2[i];
+    printf("T1-by-bitop3 outputs vs v_perm rounds: %d of %d differ\n", bad, n);
+  }
+  return 0;
+}
