@@ -371,6 +371,68 @@ __device__ __forceinline__ void aes256_tt_gk(uint32_t (&st)[NB][4], const uint4*
   }
 }
 
+// AES-256 with round keys read per round by scalar loads (s_load_dwordx4 through the scalar
+// cache) from the device copy of the schedule, AHEAD rounds before use: 4 * AHEAD SGPRs of
+// keys instead of 60, and no vector-memory traffic (the multi-key stream kernel's CW digest
+// loads keep vmcnt to themselves).  The address is base + zs + 16 r with zs a zero that an
+// empty asm redefines after each round's state, so the compiler cannot hoist the loads.
+// Scalar loads count in lgkmcnt with the LDS reads and return out of order, so a key's first
+// use waits lgkmcnt(0): issued AHEAD rounds early it has long landed by then.
+template <int NB, int AHEAD = 2>
+__device__ __forceinline__ void aes256_tt_sk(uint32_t (&st)[NB][4], const uint4* __restrict__ rkg,
+                                             const uint32_t* lds, uint32_t lc) {
+  const char* base = reinterpret_cast<const char*>(rkg);
+  uint4 kq[AHEAD];
+  {
+    const uint4 k = rkg[0];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      st[b][0] ^= k.x; st[b][1] ^= k.y; st[b][2] ^= k.z; st[b][3] ^= k.w;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < AHEAD - 1; ++q) kq[q] = rkg[q + 1];
+#pragma unroll
+  for (int r = 1; r < 15; ++r) {
+    uint32_t zs = 0u;
+    asm volatile("" : "+s"(zs) : "v"(st[0][0]), "v"(st[NB - 1][0]));
+    const int rn = r + AHEAD - 1;  // the round whose key is loaded now
+    if (rn < 15) kq[(rn - 1) % AHEAD] = *reinterpret_cast<const uint4*>(base + zs + 16 * rn);
+    const uint4 k = kq[(r - 1) % AHEAD];
+    const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+    uint32_t o[NB][4];
+    if (r < 14) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
+        }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+          const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
+          const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
+          o[b][j] = xor3(lo, hi, kw[j]);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+}
+
 // AES-256 with round keys 0..KG-1 from the kernel-argument schedule (SGPRs) and rounds
 // KG..14 from the device copy rkg, each loaded by a uniform global_load_dwordx4 AHEAD
 // rounds before its use.  For kernels whose per-lane loads are issued just before the

@@ -63,12 +63,24 @@ constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wav
 // stores, so a key load's wait can cover recent stores; the spill reloads cost less.
 #define DCF_MK_HK 0
 #endif
+#ifndef DCF_MK_SK
+// multi-key stream eval: k > 0 = round keys by scalar loads k rounds ahead (aes256_tt_sk): no SGPR
+// spills (105 SGPRs), but r02 ab_sk (same box, 2 runs): C5 391.7 vs 350.5 (k = 2) / 351.6 (k = 3) M
+// evals/s, -10 %: a scalar load shares lgkmcnt with the LDS lookups, so its wait drains them all.
+#define DCF_MK_SK 0
+#endif
 #ifndef DCF_MK_SL
 #define DCF_MK_SL -1  // multi-key stream eval: k >= 0 = round keys 0..k-1 from SGPRs, k..14 from LDS (aes256_tt_sl)
 #endif
 #ifndef DCF_REFILL_ONCE
 #define DCF_REFILL_ONCE 1  // refill: assign point indices in the loop, start the stream once after it
                            // (single-key instances with the x width fixed, NBC)
+#endif
+#ifndef DCF_REFILL_BATCH
+#define DCF_REFILL_BATCH 0  // 1: per stream, y stored after the new point's x load (vmcnt order); A/B r02 ab_batch: C3 -0.6 %, C2 / C1 noise
+#endif
+#ifndef DCF_BATCH_FENCE
+#define DCF_BATCH_FENCE asm volatile("" ::: "memory")
 #endif
 #ifndef DCF_STREAM_LATE_STORE
 // 1: y store issued after the refill's loads.  r02 A/B (same box, 2 runs): C3 533.8 vs 538.4,
@@ -94,7 +106,21 @@ struct StreamLane {
   bool alive[NS];
 };
 
-template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0>
+// The point's x words into the stream's queue (as loaded; byte-swapped on use).
+template <int NS, bool XREG, bool MULTI>
+__device__ __forceinline__ void stream_load_x(StreamLane<NS, XREG, MULTI>& L, int i, const uint8_t* row,
+                                              uint32_t nbytes) {
+  if (nbytes == 16) {
+    const uint4 x = *reinterpret_cast<const uint4*>(row);
+    L.xw[i][0] = x.x; L.xw[i][1] = x.y; L.xw[i][2] = x.z; L.xw[i][3] = x.w;
+  } else {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) L.xw[i][w] = (4u * w < nbytes) ? reinterpret_cast<const uint32_t*>(row)[w] : 0u;
+  }
+}
+
+// XLOADED: the caller has already loaded the point's x words into L.xw[i] (stream_load_x).
+template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0, bool XLOADED = false>
 __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int i, uint64_t p,
                                              const uint4* __restrict__ s0s, const uint4 s0v, uint32_t party,
                                              const uint8_t* __restrict__ xs, uint32_t nbytes_rt, uint64_t ppk,
@@ -104,14 +130,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
   const uint8_t* row = xs + p * nbytes;
   uint32_t w0;  // first 32 x bits, Msb0 (lib.rs:181)
   if (XREG) {
-    if (nbytes == 16) {
-      const uint4 x = *reinterpret_cast<const uint4*>(row);
-      L.xw[i][0] = x.x; L.xw[i][1] = x.y; L.xw[i][2] = x.z; L.xw[i][3] = x.w;
-    } else {
-#pragma unroll
-      for (int w = 0; w < 4; ++w)
-        L.xw[i][w] = (4u * w < nbytes) ? reinterpret_cast<const uint32_t*>(row)[w] : 0u;
-    }
+    if (!XLOADED) stream_load_x(L, i, row, nbytes);
     w0 = bswap32(L.xw[i][0]);
   } else {
     L.xp[i] = row;
@@ -191,6 +210,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
     } else if (mine) {  // nothing left: the stream retires
       L.alive[i] = false;
       L.ci[i] = 0;  // keep the idle stream's CW loads in bounds
+      L.lev[i] = 0;
     }
     return;
   }
@@ -208,6 +228,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
       if (mine) {
         L.alive[i] = false;
         L.ci[i] = 0;  // keep the idle stream's CW loads in bounds
+        L.lev[i] = 0;
       }
       return;
     }
@@ -218,6 +239,41 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
     unext += (uint64_t)__popcll(taken);
     need &= ~taken;
     mine = mine && !take;
+  }
+}
+
+// Hand the next point index to every lane whose stream i is free (`mine`): got / pnew, or
+// retire the stream when the counter is exhausted.  Called in wave-uniform control flow;
+// issues no memory access but the work-counter atomic (the stream is started by the caller).
+template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit>
+__device__ __forceinline__ void stream_claim(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint64_t& unext,
+                                             uint64_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
+                                             uint64_t nunits, uint64_t total, uint64_t& pnew, bool& got) {
+  uint64_t need = __ballot(mine);
+  while (need) {
+    if (unext >= uend && !exhausted) {
+      const uint32_t u = dequeue_unit(ctr);
+      if (u >= nunits) {
+        exhausted = true;
+      } else {
+        unext = (uint64_t)u * UNIT;
+        uend = min(unext + (uint64_t)UNIT, total);
+      }
+    }
+    if (exhausted && unext >= uend) break;
+    const uint32_t rank = lane_rank(need);
+    const bool take = mine && (uint64_t)rank < uend - unext;
+    pnew = take ? unext + rank : pnew;
+    got = got || take;
+    const uint64_t taken = __ballot(take);
+    unext += (uint64_t)__popcll(taken);
+    need &= ~taken;
+    mine = mine && !take;
+  }
+  if (mine) {  // nothing left: the stream retires
+    L.alive[i] = false;
+    L.ci[i] = 0;  // keep the idle stream's CW loads in bounds
+    L.lev[i] = 0;
   }
 }
 
@@ -280,7 +336,7 @@ __global__ void k_cw_rows48(const uint4* __restrict__ cw_s, const uint4* __restr
 
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
 template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false, int HK = 0,
-          bool PFX = false, bool D48 = false, int SL = -1, int NBC = 0>
+          bool PFX = false, bool D48 = false, int SL = -1, int NBC = 0, int SK = 0>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -290,6 +346,8 @@ __device__ __forceinline__ void stream_run(
   const uint32_t nbytes = NBC ? (uint32_t)NBC : nbytes_rt;
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
+  // batched refill (single key, x width fixed, x words queued in registers)
+  constexpr bool BATCH = DCF_REFILL_BATCH && DCF_REFILL_ONCE && XREG && !MULTI && NBC != 0 && !DCF_STREAM_LATE_STORE;
   const uint64_t nunits = (total + UNIT - 1) / UNIT;
   uint64_t unext = 0, uend = 0;
   bool exhausted = false;
@@ -300,6 +358,7 @@ __device__ __forceinline__ void stream_run(
     L.fresh[i] = false;
     L.alive[i] = false;
     L.ci[i] = 0;
+    L.lev[i] = 0;
     L.ph[i] = 0u;
   }
   const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
@@ -325,19 +384,22 @@ __device__ __forceinline__ void stream_run(
     bool maybe[NS];  // the next level's CWs were loaded
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      const uint4* row = cw_s + 3 * L.ci[i];  // D48: level rows cs | cv | (ct, 0, 0, 0), plus a zero row 8N
+      // CW row: the key-major digest row (MULTI); for one key the row is the level itself (a
+      // 32-bit index: ci only mirrors lev there, and a retired stream's lev is reset to 0)
+      const uint64_t cwi = MULTI ? L.ci[i] : (uint64_t)L.lev[i];
+      const uint4* row = cw_s + 3 * cwi;  // D48: level rows cs | cv | (ct, 0, 0, 0), plus a zero row 8N
       if (D48) {
         cs[i] = row[0];
         cv[i] = row[1];
         ct[i] = reinterpret_cast<const uint32_t*>(row + 2)[0];
       } else if (MULTI) {  // cw_s = digest (2 uint4 per level), cw_t = digest t bytes
-        cs[i] = cw_s[2 * L.ci[i]];
-        cv[i] = cw_s[2 * L.ci[i] + 1];
+        cs[i] = cw_s[2 * cwi];
+        cv[i] = cw_s[2 * cwi + 1];
       } else {
-        cs[i] = cw_s[L.ci[i]];
-        cv[i] = cw_v[L.ci[i]];
+        cs[i] = MULTI ? cw_s[cwi] : cw_s[L.lev[i]];
+        cv[i] = MULTI ? cw_v[cwi] : cw_v[L.lev[i]];
       }
-      if (!D48) ct[i] = cw_t[L.ci[i]];
+      if (!D48) ct[i] = MULTI ? cw_t[cwi] : cw_t[L.lev[i]];
       // XREG: a fresh stream's x word is still in the queue; its first step is a B step
       // at the root, whose seed may be unmasked, so no reuse follows it anyway.
 #ifndef DCF_NO_B_REUSE
@@ -348,7 +410,7 @@ __device__ __forceinline__ void stream_run(
 #endif
       // Loaded unconditionally (L1-resident): loads under a divergent branch made the
       // compiler wait for them before the AES.
-      const uint64_t c2 = L.ci[i] + (L.lev[i] + 1u < nlev ? 1u : 0u);
+      const uint64_t c2 = cwi + (L.lev[i] + 1u < nlev ? 1u : 0u);
       if (D48) {  // the next row (row 8N is zeros: no clamp needed)
         cs2[i] = row[3];
         cv2[i] = row[4];
@@ -380,6 +442,8 @@ __device__ __forceinline__ void stream_run(
       aes256_tt2<NS>(st, rk, lds, lc);
     } else if (GK) {  // round keys from global memory, loaded DCF_GK_AHEAD rounds ahead
       aes256_tt_gk<NS, PRE>(st, rkl, lds, lc);
+    } else if (SK) {  // round keys by scalar loads, SK rounds ahead (multi-key)
+      aes256_tt_sk<NS, (SK > 0 ? SK : 1)>(st, rkl, lds, lc);
     } else if (SL >= 0) {  // keys 0..SL-1 from SGPRs, SL..14 from LDS (multi-key)
       aes256_tt_sl<NS, (SL >= 0 ? SL : 0)>(st, rk, rkl, lds, lc);
     } else if (HK) {  // keys 0..HK-1 from SGPRs, HK..14 from global memory (multi-key)
@@ -496,9 +560,32 @@ __device__ __forceinline__ void stream_run(
 #endif
       L.lev[i] = nl;
     }
-    // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.  (vmcnt counts
-    // stores too, so the refill's wait for its x word also waits for this store; issuing it
-    // after the refill's loads instead, DCF_STREAM_LATE_STORE, measured slower.)
+    // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.
+    if constexpr (BATCH) {
+      // Per stream: claim the new point, load its x words, store the finished y (the old state
+      // is still in place), then load the new point's table row.  vmcnt retires in issue order
+      // and counts stores, so the x wait no longer covers the y store.
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const bool dn = L.alive[i] && L.lev[i] == nlev;
+        if (!__ballot(dn)) continue;
+        bool got = false;
+        uint64_t pnew = 0;
+        stream_claim<NS, XREG, MULTI, UNIT>(L, i, dn, unext, uend, exhausted, ctr, nunits, total, pnew, got);
+        if (got) stream_load_x(L, i, xs + pnew * nbytes, nbytes);
+        DCF_BATCH_FENCE;
+        if (dn) {
+          const uint32_t tm = 0u - L.t[i];
+          ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np1v.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np1v.y),
+                                   L.v[i][2] ^ L.s[i][2] ^ (tm & np1v.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np1v.w));
+        }
+        DCF_BATCH_FENCE;
+        if (got) stream_start<NS, XREG, MULTI, PFX, NBC, true>(L, i, pnew, s0s, s0v, party, xs, nbytes, ppk, pf);
+      }
+      continue;
+    }
+    // (vmcnt counts stores too, so the refill's wait for its x word also waits for this store;
+    // issuing it after the refill's loads instead, DCF_STREAM_LATE_STORE, measured slower.)
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
@@ -554,9 +641,10 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   // Multi-key: keys DCF_MK_HK..14 from global memory (0 = all from SGPRs, which spill)
   constexpr int HK = (MULTI && !TT2) ? DCF_MK_HK : 0;
   constexpr int SL = (MULTI && !TT2) ? DCF_MK_SL : -1;
-  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC>(
-      lds, (GK || HK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total, ctr,
-      ys, pf);
+  constexpr int SK = (MULTI && !TT2) ? DCF_MK_SK : 0;
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC, SK>(
+      lds, (GK || HK || SK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total,
+      ctr, ys, pf);
 }
 
 }  // namespace

@@ -1,4 +1,5 @@
-"""Print mean-per-dispatch PMC values of the eval kernels in gpurun_out/<tag>/*/ (scripts/pmc_engines.sh)."""
+"""Print mean-per-dispatch PMC values of the eval kernels (PMC_KERNELS: comma-separated name
+filters, default k_eval) in gpurun_out/<tag>/*/ (scripts/pmc_engines.sh, pmc_stall.sh)."""
 import glob
 import os
 import sqlite3
@@ -10,7 +11,7 @@ for d in sorted(glob.glob(os.path.join(sys.argv[1], "*/"))):
         c = sqlite3.connect(db)
         agg = defaultdict(lambda: defaultdict(list))
         for k, cn, v in c.execute("select kernel_name, counter_name, value from counters_collection"):
-            if "k_eval" in k:
+            if any(f in k for f in os.environ.get("PMC_KERNELS", "k_eval").split(",")):
                 agg[k.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:40]][cn].append(v)
         for k, cs in agg.items():
             print(os.path.basename(d.rstrip("/")), k, {cn: "%.4g" % (sum(v) / len(v)) for cn, v in sorted(cs.items())})
