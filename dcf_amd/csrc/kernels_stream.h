@@ -76,6 +76,13 @@ constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wav
 #define DCF_REFILL_ONCE 1  // refill: assign point indices in the loop, start the stream once after it
                            // (single-key instances with the x width fixed, NBC)
 #endif
+#ifndef DCF_REUSE_CHAIN
+// 1: B reuse over whole runs of right steps at t = 0 (see the reuse block).  Bit-exact, fewer
+// blocks (C3 132.2 -> 126.3 per eval, C2 12.52 -> 12.15), but slower: r02 ab_chain (same box, 2
+// runs): C3 520.9 vs 531.9 M evals/s (the N = 16 instance spills 20 VGPRs), C2 4.55 vs 4.60 G,
+// C5 382.7 vs 391.1 M — its ~25 VALU per stream and iteration cost more than 3-5 % of the blocks.
+#define DCF_REUSE_CHAIN 0
+#endif
 #ifndef DCF_REFILL_BATCH
 #define DCF_REFILL_BATCH 0  // 1: per stream, y stored after the new point's x load (vmcnt order); A/B r02 ab_batch: C3 -0.6 %, C2 / C1 noise
 #endif
@@ -534,6 +541,28 @@ __device__ __forceinline__ void stream_run(
         L.cur[i] <<= (rr & 1u);
         L.ci[i] += rr & 1u;
         if (rr && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+        if (DCF_REUSE_CHAIN) {
+          // Chain: the reused right step ran at t = 0 and B's bit b = lsb(B^~s) is 0, so t' = b = 0
+          // and s is unchanged again — and so on for every further right step: each one is
+          // v ^= ~s & M with no CW (t = 0) and no AES (lib.rs:176-185).  Take the whole run of 1
+          // bits at once, up to the end of the current x word (or of x); a 0 bit ending the run
+          // inside the word is a left step whose B half (B^~s) & M = d & M is applied now, A next.
+          const uint32_t zm = rr & (tm1 ^ 0xFFFFFFFFu) & ((d0 & 1u) - 1u);  // all ones: chain
+          const uint32_t room = min(32u - (nl & 31u), nlev - nl);          // levels left in this word
+          const uint32_t run = min((uint32_t)__clz((int)~L.cur[i]), room) & zm;
+          const uint32_t om = 0u - (run & 1u);                                // odd run: v ^= ~s & M once
+          const uint32_t lm = zm & (0u - (uint32_t)(run < room));            // the run ends at a left step
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+            L.v[i][j] ^= ((om & ~L.s[i][j]) ^ (lm & d[j])) & msk;
+          }
+          nl += run;
+          L.cur[i] = run >= 32u ? 0u : (L.cur[i] << run);
+          L.ci[i] += run;
+          L.ph[i] = lm ? 1u : L.ph[i];
+          if (run && run == room && nl < nlev) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+        }
       }
 #else
       if (reuse) {  // level nl with B known: its B half now, without an AES slot

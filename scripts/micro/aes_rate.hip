@@ -85,6 +85,30 @@ __global__ __launch_bounds__(1024, 1) void k_aes(const uint32_t* __restrict__ ta
   if (out) out[blockIdx.x * 1024 + threadIdx.x] = r;
 }
 
+// ds_read_b32 alone: 16 independent conflict-free lookups per iteration at addresses an empty
+// asm redefines (no address VALU, no dependency between iterations): the LDS issue ceiling.
+__global__ __launch_bounds__(1024, 1) void k_lds_only(const uint32_t* __restrict__ tab, uint32_t* out) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  uint32_t a[16], acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    a[j] = __builtin_amdgcn_perm(threadIdx.x * 0x9E3779B9u + j, lc, 0x0c020501u);
+    acc[j] = 0u;
+  }
+  for (int it = 0; it < kIters * 14 * 2 * 16 / 16 / 8; ++it) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(a[j]));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] ^= *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + a[j]);
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) r ^= acc[j];
+  if (out) out[blockIdx.x * 1024 + threadIdx.x] = r;
+}
+
 template <int NB, int MODE>
 void run(const char* name, int cus, const uint32_t* dtab, const RoundKeys& rk, const uint4* rkg, uint32_t* out,
          int wgs_per_cu) {
@@ -134,6 +158,23 @@ int main() {
     run<4, 1>("global keys (3 ahead)", cus, dtab, rk, rkg, out, w);
     run<2, 2>("sgpr keys, T1 by bitop3", cus, dtab, rk, rkg, out, w);
     run<3, 2>("sgpr keys, T1 by bitop3", cus, dtab, rk, rkg, out, w);
+  }
+  {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const int iters = kIters * 14 * 2 * 16 / 16 / 8;
+    for (int rep = 0; rep < 2; ++rep) {
+      hipEventRecord(e0);
+      hipLaunchKernelGGL(k_lds_only, dim3(cus * 4), dim3(1024), 0, 0, dtab, out);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      const double lookups = (double)cus * 4 * 1024 * iters * 16;
+      if (rep) printf("ds_read_b32 only: %.3f ms, %.2f lookups/clk/CU at 2.4 GHz (%.3f of 32)\n", ms,
+                      lookups / (ms * 1e-3) / 2.4e9 / cus, lookups / (ms * 1e-3) / 2.4e9 / cus / 32);
+    }
   }
   // same outputs as the v_perm rounds?
   {
