@@ -62,6 +62,16 @@ KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "ttable-smal
 
 # MMO (AES-128, kernels_mmo.h): 10 rounds x 16 lookups + 11 round-key ds_read_b128 (16 lanes/clk) per block
 PEAK_MMO_BLOCKS = CUS * CLK_HZ / (160 / 32 + 11 / 16)
+# Measured ceiling of the T-table AES-256 rounds alone on MI355X (scripts/micro/aes_rate.hip, r02):
+# 74-75 G blocks/s for 1-4 blocks per lane, = 0.85 of PEAK_TT_BLOCKS (ds_read_b32 alone: 0.863).
+MEASURED_TT_BLOCKS = 74.6e9
+
+
+def measured_ceiling(achieved_blocks_per_s: float) -> dict:
+    """The T-table AES rounds' practical ceiling beside the nominal LDS peak."""
+    return {"value": MEASURED_TT_BLOCKS / 1e9, "unit": "G AES-256 blocks/s",
+            "frac": achieved_blocks_per_s / MEASURED_TT_BLOCKS,
+            "source": "scripts/micro/aes_rate.hip: T-table AES-256 rounds alone, 16 waves/CU (0.85 of peak)"}
 
 
 def engine_peak(engine: str) -> float:
@@ -410,6 +420,7 @@ def run_eval(args, world, rank):
             "algorithmic_bytes": alg_bytes, "kernel_ms": kern_s * 1e3,
             "hbm_GBps": alg_bytes / kern_s / 1e9,
             "ttable_only_peak": PEAK_TT_BLOCKS / 1e9,
+            "measured_ceiling": None if engine.startswith("mmo") else measured_ceiling(per_gpu_blocks),
             "executed_blocks_per_eval": exec_bpe, "reference_blocks_per_eval": bpe,
             "prefix_levels": pfx, "no_prefix": no_prefix,
             "note": "achieved = AES blocks the kernel encrypts per second (stream engine: B every "
@@ -559,7 +570,8 @@ def run_c5(args, world, rank):
                         "engine": "stream (multi-key)", "achieved": achieved / 1e9, "peak": peak / 1e9,
                         "unit": "G AES-256 blocks/s", "frac": achieved / peak,
                         "eval_only": {"achieved": eval_blocks / eval_s / 1e9, "frac": eval_blocks / eval_s / peak,
-                                      "executed_blocks_per_eval": eval_blocks / (2 * K * P)},
+                                      "executed_blocks_per_eval": eval_blocks / (2 * K * P),
+                                      "measured_ceiling": measured_ceiling(eval_blocks / eval_s)},
                         "gen_only": {"achieved": gen_blocks / phase[0] / 1e9, "frac": gen_blocks / phase[0] / peak},
                         "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": alg_bytes,
                         "kernel_ms": step_s * 1e3, "hbm_GBps": alg_bytes / step_s / 1e9,
@@ -671,8 +683,9 @@ def run_fd(args, world, rank):
                                   f"party 0; replicas on {world} GPU(s)"},
            "roofline": {"bound": "lds", "engine": "ttable",
                         "kernel": ("k_fd_level16_mmo (8N launches)" if mmo
-                                   else "k_fd_level16 (8N-3 launches) + k_fd_tail16<3>"),
+                                   else "k_fd_level16 (8N-4 launches) + k_fd_dfs16<4>"),
                         "achieved": blocks / kern_s / 1e9, "peak": peak / 1e9,
+                        "measured_ceiling": None if mmo else measured_ceiling(blocks / kern_s),
                         "unit": f"G AES-{128 if mmo else 256} blocks/s", "frac": blocks / kern_s / peak, "kernel_ms": kern_s * 1e3,
                         "note": (f"{4 if mmo else 2} AES blocks per internal node (both children from one PRG "
                                  f"call), about {4 if mmo else 2} per leaf, vs {4 if mmo else 2} x 8N per point "

@@ -327,9 +327,11 @@ int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const 
   if (p->kind == 0) {  // one launch: k_prefix_build16
     uint8_t* ba = p->d_pfx + tab_bytes;
     const uint32_t H = prefix_dfs_levels(levels, S);
+    if (DCF_PFX_GK)
+      if (int rc = ensure_rk0(p)) return rc;
     hipLaunchKernelGGL(k_prefix_build16, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->rk[0], cws, cwv, cwt,
                        (const uint4*)s0, (uint32_t)party, S, levels, H, ba, ba + ((size_t)1 << S) * region,
-                       (uint64_t)region, R, (uint4*)p->d_pfx);
+                       (uint64_t)region, R, (uint4*)p->d_pfx, DCF_PFX_GK ? p->d_rk0 : nullptr);
     HIP_TRY(hipGetLastError());
     *out = PrefixTable{(const uint4*)p->d_pfx, levels};
     return DCF_OK;

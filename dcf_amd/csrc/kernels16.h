@@ -570,18 +570,23 @@ __global__ void k_prefix_pack(const uint4* __restrict__ s, const uint4* __restri
 
 // One PRG call (A, B) on node (s, v, t) of level `lev` -> both children (lib.rs:176-189
 // with x bit 0 / 1), as in k_fd_level16.
+// GKB: round keys read per round from the device copy rkg (aes256_tt_gk) instead of SGPRs.
+template <bool GKB = false>
 __device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, const RoundKeys& rk,
                                             const uint32_t (&csw)[4], const uint32_t (&cvw)[4], uint32_t ct,
                                             const uint32_t (&s)[4], const uint32_t (&v)[4], uint32_t t,
                                             uint32_t (&sl)[4], uint32_t (&vl)[4], uint32_t& tl, uint32_t (&sr)[4],
-                                            uint32_t (&vr)[4], uint32_t& tr) {
+                                            uint32_t (&vr)[4], uint32_t& tr, const uint4* __restrict__ rkg = nullptr) {
   uint32_t st[2][4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     st[0][k] = s[k];
     st[1][k] = ~s[k];
   }
-  aes256_tt<2>(st, rk, lds, lc);  // A, B
+  if (GKB)
+    aes256_tt_gk<2>(st, rkg, lds, lc);  // A, B
+  else
+    aes256_tt<2>(st, rk, lds, lc);  // A, B
   const uint32_t tm = 0u - t;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -606,13 +611,17 @@ __device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, co
 // table directly (no pack pass).  Same bytes as the level kernels + k_prefix_pack.
 // H > 0: the level-by-level part stops at level D - H (one node or more per thread) and
 // each thread expands its nodes' last H levels depth-first (see the tail below).
+#ifndef DCF_PFX_GK
+#define DCF_PFX_GK 1  // table build: AES round keys per round from the device copy (no SGPR spills)
+#endif
 constexpr uint32_t kPfxDfsMax = 4;  // H <= 4: a 3-slot stack of 9-word nodes (27 VGPRs; 5 slots spill to scratch)
 __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ s0,
     const uint32_t party, const uint32_t S, const uint32_t D, const uint32_t H, uint8_t* __restrict__ buf_a,
     uint8_t* __restrict__ buf_b, const uint64_t region_bytes, const uint32_t region_nodes,
-    uint4* __restrict__ table) {
+    uint4* __restrict__ table, const uint4* __restrict__ rkg) {
+  constexpr bool GKB = DCF_PFX_GK != 0;
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint4 root_s, root_v;
   __shared__ uint32_t root_t;
@@ -629,7 +638,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
       const uint4 cs = cw_s[lev], cv = cw_v[lev];
       const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
       uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
-      fd_children(lds, lc, rk, csw, cvw, cw_t[lev], s, v, t, sl, vl, tl, sr, vr, tr);
+      fd_children<GKB>(lds, lc, rk, csw, cvw, cw_t[lev], s, v, t, sl, vl, tl, sr, vr, tr, rkg);
       const bool right = (w >> (S - 1u - lev)) & 1u;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -677,7 +686,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
         nt = xt_[jn];
       }
       uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
-      fd_children(lds, lc, rk, csw, cvw, ct, s, v, t, sl, vl, tl, sr, vr, tr);
+      fd_children<GKB>(lds, lc, rk, csw, cvw, ct, s, v, t, sl, vl, tl, sr, vr, tr, rkg);
       if (last) {  // PrefixTable rows: s with t in bit 0 of byte 15 (below the root s is masked there)
         uint4* row = table + 2ull * (((uint64_t)w << (D - S)) + 2u * j);
         row[0] = make_uint4(sl[0], sl[1], sl[2], (sl[3] & kMaskLast) | (tl << 24));
@@ -735,7 +744,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
         const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
         const uint32_t s[4] = {n[0], n[1], n[2], n[3]}, v[4] = {n[4], n[5], n[6], n[7]};
         uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
-        fd_children(lds, lc, rk, csw, cvw, cw_t[B + k], s, v, n[8], sl, vl, tl, sr, vr, tr);
+        fd_children<GKB>(lds, lc, rk, csw, cvw, cw_t[B + k], s, v, n[8], sl, vl, tl, sr, vr, tr, rkg);
         if (k + 1u == H) {  // bottom: leaves 2i, 2i + 1 of this node's block of rows
           uint4* row = rows + 4u * i;
           row[0] = make_uint4(sl[0], sl[1], sl[2], (sl[3] & kMaskLast) | (tl << 24));
