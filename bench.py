@@ -387,8 +387,11 @@ def run_eval(args, world, rank):
         # tail writes LAMBDA - 32 output bytes per eval: time bound = AES (LDS) + output (HBM write).
         engine = "stream-head" if args.eval_mode != 1 else "ttable"
         if engine == "stream-head":
-            # below a shared prefix of pfx levels (k_wpfx_level: 4 blocks per parent node)
-            exec_bpe = 3 * (8 * nb - pfx) - zero_bits(xs, pfx) / m + 4 * (2 ** pfx - 1) / m
+            # below a shared prefix of pfx levels (k_wpfx_build: 4 blocks per parent node); the
+            # walk's blocks are counted by the kernel (B reuse after a right step at t = 0 skips
+            # some B blocks, kernels_wide_stream.h), else 2 per left and 3 per right level
+            walk = dev_blocks / m if dev_blocks else 3 * (8 * nb - pfx) - zero_bits(xs, pfx) / m
+            exec_bpe = walk + 4 * (2 ** pfx - 1) / m
     per_gpu_blocks = m * exec_bpe / kern_s
     # HBM bytes per launch of the dominant kernel: x in, y out, and with a shared prefix
     # one 32-byte table row gathered per point (kernels16.h PrefixTable)

@@ -246,6 +246,54 @@ __device__ __forceinline__ void aes_tt_lka(uint32_t (&st)[NB][4], const uint32_t
   }
 }
 
+// NB independent AES-NR encryptions, each under the schedule at byte offset ko[b] of a buffer
+// (round key r at ko[b] + 16 r; lanes may pick different schedules), read through the vector
+// L1 by one buffer_load_dwordx4 per round and block, AHEAD rounds before its use, instead of
+// an LDS read: the LDS serves only the T-table lookups.  kq[b][(r - 1) % AHEAD] holds round
+// key r; the caller has loaded keys 1 .. AHEAD - 1 and XORed key 0 into st.  ko is
+// "redefined" by an empty asm after each round's state, so the compiler cannot hoist the loads
+// (the offset 16 r rides in the instruction).
+template <int NR, int NB, int AHEAD>
+__device__ __forceinline__ void aes_tt_bk(uint32_t (&st)[NB][4], uint32_t (&ko)[NB], __amdgpu_buffer_rsrc_t rs,
+                                          uint4 (&kq)[NB][AHEAD], const uint32_t* lds, uint32_t lc) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int r = 1; r <= NR; ++r) {
+    uint32_t o[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int rn = r + AHEAD - 1;  // the round whose key is loaded now
+      if (rn <= NR) {
+        asm volatile("" : "+v"(ko[b]) : "v"(st[b][0]));
+        const v4u k = __builtin_amdgcn_raw_buffer_load_b128(rs, ko[b] + 16u * rn, 0, 0);
+        kq[b][(rn - 1) % AHEAD] = make_uint4(k.x, k.y, k.z, k.w);
+      }
+      const uint4 k = kq[b][(r - 1) % AHEAD];
+      const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (r < NR) {
+          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
+        } else {  // final round: S(x) sits in byte r of T_{(r+2)&3}
+          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(__builtin_amdgcn_perm(c, a, 0x0c0c0500u), __builtin_amdgcn_perm(e, d, 0x07020c0cu), kw[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+}
+
 // NB independent AES encryptions with NR rounds (10: AES-128, 14: AES-256), each
 // under its own key schedule read from LDS: rk[b] points at NR + 1 uint4 round
 // keys (per lane, so a lane may pick its schedule; lanes reading the same

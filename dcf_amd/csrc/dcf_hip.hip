@@ -413,6 +413,54 @@ int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, cons
   return DCF_OK;
 }
 
+// Paired-slot tail (k_eval_wide_tail2, 128-byte tiles, 6/5-bit chunks): the t-vectors are
+// repacked into chunk bytes in place, then the tail runs as launch_tail does.
+template <int R6, int R5>
+int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
+                 uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st) {
+  using L = Tail2Layout<R6, R5>;
+  if (nlev + 1 > L::rows()) return fail(DCF_ERR_UNSUPPORTED, "tail2 layout too small");
+  hipLaunchKernelGGL((k_tvec_chunks<R6, R5>), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tvec, nlev, cnt);
+  HIP_TRY(hipGetLastError());
+  const size_t lds = L::lds_bytes();
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+#ifndef DCF_TAIL2_PTS
+#define DCF_TAIL2_PTS 32768  // points per workgroup (one table build each; C4 A/B: 4096 37.8-38.0 ms, 8192 37.0-37.4, 16384 36.9-37.0, 32768 36.7-37.0, 65536 36.4-36.8)
+#endif
+  const uint64_t tiles = (lam + 127) / 128, per = DCF_TAIL2_PTS;
+  const dim3 grid((unsigned)tiles, (unsigned)((cnt + per - 1) / per));
+  hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key,
+                     tvec, cnt, (uint32_t)per, ys);
+  HIP_TRY(hipGetLastError());
+  return DCF_OK;
+}
+
+#ifndef DCF_TAIL2
+#define DCF_TAIL2 1  // 0: the 4-bit 256-byte-tile tail for every N
+#endif
+// The tail for n = nlev levels: the paired-slot tail when one of its instances covers the
+// n + 1 rows with fewer LDS reads than the 4-bit tail's ceil((n + 1) / 4), else the 4-bit one.
+int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
+             uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
+             int cus) {
+  const uint32_t nrows = nlev + 1, nch = (nrows + 3) / 4;
+  if (DCF_TAIL2 && lam % 128 == 0) {
+#define DCF_T2(A, B)                                                                            \
+  if (nrows <= Tail2Layout<A, B>::rows() && 2u * (A + B) < nch)                                 \
+    return launch_tail2<A, B>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
+    DCF_T2(1, 0)   // N = 1: 9 rows, 2 reads (4-bit: 3)
+    DCF_T2(1, 1)   // N = 2: 17 rows, 4 reads (5)
+    DCF_T2(2, 1)   // N = 3, 4: 25 / 33 rows, 6 reads (7 / 9)
+    DCF_T2(3, 3)   // N = 6..8: 49..65 rows, 12 reads (13..17)
+    DCF_T2(5, 7)   // N = 12..16: 97..129 rows, 24 reads (25..33)
+#undef DCF_T2
+  }
+  return (nch == 33) ? launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus)
+       : (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus)
+                     : launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus);
+}
+
 // Dcf::eval at LAMBDA >= 32 for key `key` of a K-key CWB (see kernels_wide.h).
 int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb, const uint8_t* s0,
               const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
@@ -427,14 +475,14 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
   int rc = ensure_ws(p, chunk * kTWords * 4, st);
   if (rc) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(p->d_ws);
-  const uint32_t nch = (nlev + 1 + 3) / 4;
   WidePrefix wpf{nullptr, 0u};
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = (m - off < chunk) ? m - off : chunk;
     const dim3 grid((unsigned)grid_for(cnt, p->cus));
     if (p->eval_mode != DCF_EVAL_TTABLE) {  // stream head: 2.5 AES blocks per level instead of 4
       if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
-      HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
+      // the work counter every pass, the block count (dcf_prg_last_eval_blocks) once per call
+      HIP_TRY(hipMemsetAsync(p->d_ctr, 0, off == 0 ? kCtrBytes : 8, st));
       if (!p->d_rk2) {  // round keys of ciphers 0 and 17 (2 x 15 x 16 B), read into LDS by the kernel
         HIP_TRY(hipMalloc(&p->d_rk2, 2 * sizeof(RoundKeys)));
         HIP_TRY(hipMemcpy(p->d_rk2, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice));
@@ -487,9 +535,7 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
                          ys + off * lam, tvec);
     HIP_TRY(hipGetLastError());
     if (lam > 32) {
-      rc = (nch == 33) ? launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus)
-         : (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus)
-                       : launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus);
+      rc = run_tail(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus);
       if (rc) return rc;
     }
   }

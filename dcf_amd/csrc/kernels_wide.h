@@ -347,6 +347,253 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
 }
 
 // ------------------------------------------------------------------------
+// Tail with wide chunks ("paired-slot" four-Russians): 128-byte tiles, 6- and 5-bit chunks.
+//
+// The 4-bit tail above reads 33 table entries per 16 bytes of y (N = 16): its tables are
+// 16 x 256 B per chunk and a chunk's entry must span all 64 banks for 16 lanes to read it
+// conflict-free, so 160 KB of LDS cannot hold wider chunks.  Here a tile is 128 bytes (8
+// lanes per point; 128-B tiles still write whole cache lines: 5.6 TB/s vs 3.75 at 64 B and
+// 0.71 at 32 B, scripts/micro/tile_write_bw.hip) and two chunks share a 256-byte LDS row:
+// region m holds chunks 2m and 2m+1, entry e of both in row e (chunk 2m in bytes [0,128),
+// 2m+1 in [128,256)).  A 16-lane LDS pass holds two points (pi = 0, 1); at step i of region
+// m the point pi reads chunk 2m + (i ^ pi), so the two points always sit in opposite halves
+// of the bank span — conflict-free for any data.  With chunks of 6 bits (regions of 16 KiB)
+// and 5 bits (8 KiB), N = 16's 129 rows take 5 + 7 regions = 24 reads per 16 bytes of y
+// (136 KiB of LDS) instead of 33.
+//
+// t-vector ("chunk bytes", produced from the head's nibble format by k_tvec_chunks): byte k =
+// the index of chunk k: chunks 0 .. 2 R6 - 1 are 6 rows each from row 0, then 5-row chunks.
+// Rows past n + 1 are zero.  Kept in place in the head's 64-byte t-vector rows (first 32 B).
+// ------------------------------------------------------------------------
+template <int R6, int R5>
+struct Tail2Layout {
+  static constexpr int R = R6 + R5, NC = 2 * R;
+  static_assert(NC <= 32, "t-vector holds 32 chunk bytes");
+  static constexpr uint32_t width(int k) { return k < 2 * R6 ? 6u : 5u; }
+  static constexpr uint32_t start(int k) { return k < 2 * R6 ? 6u * k : 12u * R6 + 5u * (k - 2 * R6); }
+  static constexpr uint32_t region(int m) { return m < R6 ? 16384u * m : 16384u * R6 + 8192u * (m - R6); }
+  static constexpr uint32_t rows() { return 12u * R6 + 10u * R5; }
+  static constexpr uint32_t lds_bytes() { return region(R); }
+};
+
+// Old nibble t-vector (row r at byte r >> 2, bit r & 3; words 0 .. nlev >> 4 valid) -> chunk
+// bytes of Tail2Layout<R6, R5>, in place (bytes [0, 32) of each 64-byte row).  One thread
+// per point: 36 of 64 bytes read, 32 written.
+template <int R6, int R5>
+__global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, const uint64_t count) {
+  using L = Tail2Layout<R6, R5>;
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= count) return;
+  uint32_t* row = tvec + p * kTWords;
+  const uint32_t nw = (nlev >> 4) + 1u;  // nibble words written by the head
+  uint32_t pk[6] = {0u, 0u, 0u, 0u, 0u, 0u};  // rows as a plain bit string, row r = bit r
+#pragma unroll
+  for (uint32_t j = 0; j < 12; ++j) {
+    if (j < nw && 16u * j < L::rows()) {
+      uint32_t x = row[j] & 0x0F0F0F0Fu;
+      x = (x | (x >> 4)) & 0x00FF00FFu;
+      x = (x | (x >> 8)) & 0x0000FFFFu;
+      pk[j >> 1] |= x << (16u * (j & 1u));
+    }
+  }
+  const uint32_t nrows = nlev + 1u;  // clear rows past t_n (never written by the head)
+#pragma unroll
+  for (uint32_t w = 0; w < 6; ++w) {
+    const uint32_t lo = 32u * w;
+    pk[w] &= nrows >= lo + 32u ? 0xFFFFFFFFu : (nrows <= lo ? 0u : ((1u << (nrows - lo)) - 1u));
+  }
+  uint32_t out[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int k = 0; k < L::NC; ++k) {
+    const uint32_t s = L::start(k), w = L::width(k);
+    const uint32_t lo = pk[s >> 5], hi = (s >> 5) + 1 < 6 ? pk[(s >> 5) + 1] : 0u;
+    const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31u)) & ((1u << w) - 1u);
+    out[k >> 2] |= v << (8 * (k & 3));
+  }
+  uint4* o4 = reinterpret_cast<uint4*>(row);
+  o4[0] = make_uint4(out[0], out[1], out[2], out[3]);
+  o4[1] = make_uint4(out[4], out[5], out[6], out[7]);
+}
+
+#ifndef DCF_TAIL2_BATCH
+#define DCF_TAIL2_BATCH 2
+#endif
+template <int R6, int R5>
+__global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __restrict__ cw_s,
+                                                             const uint8_t* __restrict__ cw_v,
+                                                             const uint8_t* __restrict__ cw_np1,
+                                                             const uint8_t* __restrict__ s0, const uint32_t nlev,
+                                                             const uint32_t lam, const uint64_t num_keys,
+                                                             const uint64_t key, const uint32_t* __restrict__ tvec,
+                                                             const uint64_t count, const uint32_t pts_per_block,
+                                                             uint8_t* __restrict__ ys) {
+  using L = Tail2Layout<R6, R5>;
+  constexpr int TW = 128, LP = 8;
+  extern __shared__ uint4 G[];
+  if ((uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)G != 0u) __builtin_trap();
+  const uint32_t byte0 = (uint32_t)blockIdx.x * TW;
+  // Tables: item (chunk k, piece q, group g of 8 entries): the group's base (rows of the
+  // entry bits >= 3) then its 8 entries in Gray-code order, one XOR each.
+  {
+    constexpr uint32_t items6 = 2 * R6 * LP * 8, items = items6 + 2 * R5 * LP * 4;
+    char* gb = reinterpret_cast<char*>(G);
+    for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+      uint32_t k, rest, w;
+      if (it < items6) { k = it / (LP * 8); rest = it % (LP * 8); w = 6u; }
+      else { k = 2 * R6 + (it - items6) / (LP * 4); rest = (it - items6) % (LP * 4); w = 5u; }
+      const uint32_t q = rest % LP, g = rest / LP;
+      const uint32_t st = k < 2u * R6 ? 6u * k : 12u * R6 + 5u * (k - 2u * R6);
+      const uint32_t off = byte0 + 16u * q;
+      // W rows st .. st + 5 (row st + b used if b < w): all 12 loads issued before any is
+      // used (w_row_piece's branches would serialise them), addresses clamped, then masked.
+      uint4 wr[6];
+      {
+        const bool offok = off >= 32u && off < lam;
+        uint4 cv[6], cs[6];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+          const uint32_t r = st + b;
+          const bool isn = r == nlev;  // row n: cw_np1
+          const uint32_t rr = (r < nlev && offok) ? r : 0u;
+          const uint32_t o = offok ? off : 32u;
+          const uint64_t ro = ((uint64_t)rr * num_keys + key) * lam + o;
+          cv[b] = *reinterpret_cast<const uint4*>((isn && offok ? cw_np1 + key * lam + o : cw_v + ro));
+          cs[b] = *reinterpret_cast<const uint4*>(cw_s + ro);
+        }
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+          const uint32_t r = st + b, l = r + 1;
+          const bool valid = offok && (uint32_t)b < w && r <= nlev;
+          const uint32_t vm = valid ? 0xFFFFFFFFu : 0u;
+          const uint32_t even = (r < nlev && !(l & 1u)) ? vm : 0u;  // cw_s joins W_l on even l (row n: np1 only)
+          uint4 x = make_uint4((cv[b].x & vm) ^ (cs[b].x & even), (cv[b].y & vm) ^ (cs[b].y & even),
+                               (cv[b].z & vm) ^ (cs[b].z & even), (cv[b].w & vm) ^ (cs[b].w & even));
+          if (off + 16 == lam && r < nlev) {  // bit 0 of byte LAMBDA-1: cw_s joins only at l == n
+            const uint32_t bit = (cv[b].w ^ ((l == nlev) ? cs[b].w : 0u)) & 0x01000000u & vm;
+            x.w = (x.w & ~0x01000000u) | bit;
+          }
+          wr[b] = x;
+        }
+      }
+      uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int b = 3; b < 6; ++b)
+        if ((g >> (b - 3)) & 1u) { acc.x ^= wr[b].x; acc.y ^= wr[b].y; acc.z ^= wr[b].z; acc.w ^= wr[b].w; }
+      const uint32_t m = k >> 1;
+      const uint32_t rbase = m < (uint32_t)R6 ? 16384u * m : 16384u * R6 + 8192u * (m - R6);
+      char* dst = gb + rbase + (k & 1u) * 128u + 16u * q;
+#pragma unroll
+      for (uint32_t i = 0; i < 8; ++i) {
+        if (i) {
+          const uint4 x = wr[__builtin_ctz(i)];
+          acc.x ^= x.x; acc.y ^= x.y; acc.z ^= x.z; acc.w ^= x.w;
+        }
+        const uint32_t e = 8u * g + (i ^ (i >> 1));
+        *reinterpret_cast<uint4*>(dst + 256u * e) = acc;
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t q = threadIdx.x % LP;
+  const uint32_t pi = (threadIdx.x >> 3) & 1u;   // the point's half of a 16-lane LDS pass
+  const uint32_t off = byte0 + 16 * q;
+  const bool lane_live = off >= 32u && off < lam;
+  uint4 cst = make_uint4(0u, 0u, 0u, 0u);
+  if (lane_live) {
+    cst = *reinterpret_cast<const uint4*>(s0 + off);
+    if (off + 16 == lam) cst.w &= kMaskLast;
+  }
+  // lane constants (address byte 0 = slot, byte 2 = 64 KiB group): step i of a region reads
+  // chunk 2m + (i ^ pi), whose entry sits in bytes [(i ^ pi) 128, +128) of the 256-B row
+  const uint32_t lc0 = pi * 128u + 16u * q, lc1 = (pi ^ 1u) * 128u + 16u * q;
+  const uint32_t rsel = pi ? 0x02030001u : 0x03020100u;  // pi = 1: swap the chunk bytes of each region
+  const uint64_t p0 = (uint64_t)blockIdx.y * pts_per_block;
+  const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
+  const uint32_t pstep = blockDim.x / LP;
+  const uint32_t pin = (threadIdx.x & 63u) / LP;
+  const uint4* tv4 = reinterpret_cast<const uint4*>(tvec);
+  auto load_t = [&](uint4 (&d)[2], uint64_t pp) {
+    pp = min<uint64_t>(pp, p1 - 1);
+    d[0] = tv4[4 * pp];
+    d[1] = tv4[4 * pp + 1];
+  };
+  constexpr int NW = (L::NC + 3) / 4;  // chunk-byte words
+  auto rotate = [&](const uint4 (&t)[2], uint32_t (&tw)[NW]) {
+    const uint32_t w[8] = {t[0].x, t[0].y, t[0].z, t[0].w, t[1].x, t[1].y, t[1].z, t[1].w};
+#pragma unroll
+    for (int j = 0; j < NW; ++j) tw[j] = __builtin_amdgcn_perm(w[j], w[j], rsel);
+  };
+  // entry read for step i of region m of the point whose rotated chunk words are tw
+  auto rd = [&](const uint32_t (&tw)[NW], int m, int i) {
+    const uint32_t rb = L::region(m);
+    const uint32_t grp = (rb >> 16) << 16;  // compile-time per m: the 64 KiB group in address byte 2
+    const int c = 2 * m + i;               // byte of the rotated chunk vector
+    const uint32_t a = __builtin_amdgcn_perm(tw[c >> 2], (i ? lc1 : lc0) | grp, 0x0c020000u | ((4u + (c & 3)) << 8));
+    return lds_load16(a + (rb & 0xFFFFu));  // the rest of the region base rides in the offset field
+  };
+  // Two points per lane and iteration (A = p, B = p + pstep): their 2 x 24 reads are
+  // independent, so each wave keeps more LDS reads in flight.  The loop condition is
+  // wave-uniform (the wave's first point): no branch around a vector-memory instruction, so
+  // the compiler counts vmcnt exactly — the t-vectors, loaded at the end of an iteration, are
+  // waited on at the end of the next one (vmcnt(2): past the two y stores).  Past-the-end lanes load a clamped row and
+  // their stores are dropped (offset past num_records).
+  const uint32_t dead = 0x80000000u;
+  const uint32_t kill = lane_live ? 0u : dead;
+  uint64_t p = p0 + threadIdx.x / LP;
+  const uint64_t pw0 = p0 + (threadIdx.x / 64u) * (64u / LP);
+  uint4 ta[2], tb[2];
+  uint32_t twa[NW], twb[NW];
+  load_t(ta, p);
+  load_t(tb, p + pstep);
+  rotate(ta, twa);
+  rotate(tb, twb);
+  load_t(ta, p + 2 * pstep);
+  load_t(tb, p + 3 * pstep);
+  for (uint64_t pw = pw0; pw < p1; pw += 2 * pstep, p += 2 * pstep) {
+    uint32_t aa[4] = {cst.x, cst.y, cst.z, cst.w}, ab[4] = {cst.x, cst.y, cst.z, cst.w};
+    // DCF_TAIL2_BATCH regions (4 reads each) are issued before their XORs: the compiler
+    // otherwise waits after every two reads, ~3 reads in flight per wave
+#pragma unroll
+    for (int m0 = 0; m0 < L::R; m0 += DCF_TAIL2_BATCH) {
+      uint4 rb[DCF_TAIL2_BATCH][4];
+#pragma unroll
+      for (int k = 0; k < DCF_TAIL2_BATCH; ++k)
+        if (m0 + k < L::R) {
+          rb[k][0] = rd(twa, m0 + k, 0); rb[k][1] = rd(twa, m0 + k, 1);
+          rb[k][2] = rd(twb, m0 + k, 0); rb[k][3] = rd(twb, m0 + k, 1);
+        }
+      // the batch's reads are all issued before the first result is used: a memory clobber
+      // keeps them above, and one empty asm per read (issued in order) makes each XOR wait
+      // for its own read only (lgkmcnt counts down in order)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < DCF_TAIL2_BATCH; ++k)
+        if (m0 + k < L::R)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            asm volatile("" : "+v"(rb[k][j].x), "+v"(rb[k][j].y), "+v"(rb[k][j].z), "+v"(rb[k][j].w));
+#pragma unroll
+      for (int k = 0; k < DCF_TAIL2_BATCH; ++k)
+        if (m0 + k < L::R) {
+          const uint4 a0 = rb[k][0], a1 = rb[k][1], b0 = rb[k][2], b1 = rb[k][3];
+          aa[0] = xor3(aa[0], a0.x, a1.x); aa[1] = xor3(aa[1], a0.y, a1.y);
+          aa[2] = xor3(aa[2], a0.z, a1.z); aa[3] = xor3(aa[3], a0.w, a1.w);
+          ab[0] = xor3(ab[0], b0.x, b1.x); ab[1] = xor3(ab[1], b0.y, b1.y);
+          ab[2] = xor3(ab[2], b0.z, b1.z); ab[3] = xor3(ab[3], b0.w, b1.w);
+        }
+    }
+    tail_store<LP>(ys, p - pin, pin, lam, off, kill | (p < p1 ? 0u : dead), make_uint4(aa[0], aa[1], aa[2], aa[3]));
+    const uint64_t pb = p + pstep;
+    tail_store<LP>(ys, pb - pin, pin, lam, off, kill | (pb < p1 ? 0u : dead), make_uint4(ab[0], ab[1], ab[2], ab[3]));
+    // the next iteration's t-vectors (loaded one iteration ago, before these two stores)
+    rotate(ta, twa);
+    rotate(tb, twb);
+    load_t(ta, p + 4 * pstep);
+    load_t(tb, p + 5 * pstep);
+  }
+}
+
+// ------------------------------------------------------------------------
 // Gen at LAMBDA >= 32: one workgroup per key; thread i owns 16-byte pieces
 // i, i+blockDim, ... of s_0, s_1, v_alpha (kept in `ws`, 3*LAMBDA per key).
 // Per level 8 AES blocks (E0/E17 on s_p and ~s_p, p = 0, 1) by lanes 0..7.

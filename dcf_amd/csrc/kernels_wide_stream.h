@@ -40,6 +40,7 @@ struct WidePrefix {
 template <int NS>
 struct WideLane {
   uint32_t s[NS][8], v[NS][8];           // bytes [0,32) of the seed and of the v accumulator
+  uint32_t dB[NS][4];                    // this level's B ^ ~s[0:16) (DCF_WHS_REUSE)
   uint32_t t[NS], ph[NS], lev[NS], cur[NS], tR[NS], tacc[NS];
   uint32_t xq[NS][3];                    // XREG: the point's next raw x words (byte-swapped on use)
   uint32_t pt[NS];                       // point index within this launch (<= 2^20); x row = xs + pt * N
@@ -146,6 +147,13 @@ __global__ void k_cw_digest(const uint8_t* __restrict__ cw_s, const uint8_t* __r
   if (q == 0) dig_t[l] = cw_t[ci];
 }
 
+#ifndef DCF_WHS_REUSE
+#define DCF_WHS_REUSE 1  // skip the B block after a right step at t = 0 (same output bytes)
+#endif
+#ifndef DCF_WHS_GK
+#define DCF_WHS_GK 0  // 1: round keys by buffer loads (vector L1) instead of LDS reads (C4 A/B: 38.4-38.5 vs 36.5 ms: the
+                      // key waits retire in order behind the CW loads)
+#endif
 // Single key `key` of a num_keys-key CWB; count <= 2^20 points per launch.
 template <int NS, bool MASK_HEAD, bool XREG, int WG = kBlock>
 __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
@@ -161,6 +169,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
   lds_fill_tables(lds, tab);  // its barrier also publishes rks
   const uint32_t rks_a = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)rks;  // LDS byte address
+  const __amdgpu_buffer_rsrc_t rkrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(rk2), (short)0, 480, 0x00020000);
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
   const uint64_t nunits = (count + kStreamUnit - 1) / kStreamUnit;
@@ -168,6 +177,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   uint64_t unext = 0, uend = 0;
   bool exhausted = false;
   WideLane<NS> L;
+  uint64_t nblk = 0;  // AES blocks this wave encrypts for live streams (wave-uniform)
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     L.alive[i] = false;
@@ -184,6 +194,8 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
 #pragma unroll
     for (int i = 0; i < NS; ++i) any = any || L.alive[i];
     if (!__ballot(any)) break;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) nblk += (uint64_t)__popcll(__ballot(L.alive[i]));
     // Correction words, used only on the step that ends a level (the update masks them with
     // am): bytes [0,32) of cw_s / cw_v from the compact per-key digest (64 B per level,
     // 8 KiB, L1-resident; the CWB rows are LAMBDA bytes apart, one cache line per lane).
@@ -191,6 +203,23 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     // 17 zeroing moves per step and the loads issued anyway.  Issued before the AES and
     // pinned after it, so they are waited on long after the last y / t-vector stores
     // (vmcnt is in order: a load issued after a store cannot be waited on alone).
+    // DCF_WHS_GK: the lane's round keys through the vector L1 (rounds 0 .. 2 loaded here, before
+    // the CW loads, so waiting for them never waits for those; later rounds 3 ahead in the AES)
+    uint32_t ko[NS];
+    uint4 kq[NS][3], k0g[NS];
+    if (DCF_WHS_GK) {
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        ko[i] = 240u * ((L.ph[i] != 0u) & (L.cur[i] >> 31));  // cipher 17's schedule: 15 keys on
+        const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rkrs, ko[i], 0, 0);
+        const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rkrs, ko[i] + 16u, 0, 0);
+        const v4u c = __builtin_amdgcn_raw_buffer_load_b128(rkrs, ko[i] + 32u, 0, 0);
+        k0g[i] = make_uint4(a.x, a.y, a.z, a.w);
+        kq[i][0] = make_uint4(b.x, b.y, b.z, b.w);
+        kq[i][1] = make_uint4(c.x, c.y, c.z, c.w);
+      }
+    }
     uint4 cs[NS][2], cv[NS][2];
     uint32_t ct[NS];
 #pragma unroll
@@ -213,11 +242,16 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       // cipher 17's schedule sits 23 slots on.  The empty asm keeps the compiler from
       // re-associating base + 16 r (rks_a is a link-time symbol: 14 materialised constants and
       // a v_mad per round); the mask proves the sign bit clear, so +16 r folds into ds_read
-      uint32_t kb = rks_a + 368u * hi;
-      asm volatile("" : "+v"(kb));
-      ka[i] = kb & 0x3FFFFu;
+      uint4 k0;
+      if (DCF_WHS_GK) {
+        k0 = k0g[i];
+      } else {
+        uint32_t kb = rks_a + 368u * hi;
+        asm volatile("" : "+v"(kb));
+        ka[i] = kb & 0x3FFFFu;
+        k0 = lds_load16(ka[i]);
+      }
       const uint32_t hm = 0u - hi;
-      const uint4 k0 = lds_load16(ka[i]);
       const uint32_t k0w[4] = {k0.x, k0.y, k0.z, k0.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -225,7 +259,10 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
         st[i][j] = xor3(sel[i][j], inv[i], k0w[j]);  // round key 0 folded in
       }
     }
-    aes_tt_lka<14, NS, true>(st, ka, lds, lc);
+    if (DCF_WHS_GK)
+      aes_tt_bk<14, NS, 3>(st, ko, rkrs, kq, lds, lc);
+    else
+      aes_tt_lka<14, NS, true>(st, ka, lds, lc);
 #pragma unroll
     for (int i = 0; i < NS; ++i)
       asm volatile("" : "+v"(cs[i][0].x), "+v"(cs[i][0].y), "+v"(cs[i][0].z), "+v"(cs[i][0].w), "+v"(cs[i][1].x),
@@ -248,6 +285,13 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
 #pragma unroll
       for (int j = 0; j < 4; ++j) d[j] = xor3(st[i][j], sel[i][j], inv[i]);
       L.tR[i] = mB ? (d[0] & 1u) : L.tR[i];  // t_R = lsb(B ^ ~s)[0] (prg.rs:64)
+      if (DCF_WHS_REUSE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) L.dB[i][j] = pick(mB, d[j], L.dB[i][j]);
+      }
+      // B reuse: a right step at t = 0 leaves s[0:16) as it is (s_R = s with only [16:32)
+      // replaced, ^ 0 cw_s), so the next level's B = E0(~s[0:16)) is this level's
+      const uint32_t ru = DCF_WHS_REUSE ? (mC & (L.t[i] - 1u)) : 0u;
       const uint32_t tb = ((mA ? d[0] : L.tR[i]) & 1u) ^ (L.t[i] & (ct[i] >> xb) & 1u);  // lib.rs:179-180
       const uint32_t csw[8] = {cs[i][0].x, cs[i][0].y, cs[i][0].z, cs[i][0].w,
                                cs[i][1].x, cs[i][1].y, cs[i][1].z, cs[i][1].w};
@@ -278,6 +322,8 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       }
       L.t[i] = adv ? tb : L.t[i];
       L.ph[i] = mB ? 1u : (mD ? 2u : 0u);
+      const bool reuse = ru != 0u && L.lev[i] + adv != nlev;
+      L.ph[i] = reuse ? 1u : L.ph[i];  // the next level starts at A / D
       // t-vector: row r = lev + 1 gets t_r (byte r >> 2, bit r & 3), as k_eval_wide_head writes it
       const uint32_t r = L.lev[i] + adv;
       L.tacc[i] |= (am & L.t[i]) << (8u * ((r >> 2) & 3u) + (r & 3u));
@@ -309,6 +355,11 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
         y4[0] = make_uint4(y[0], y[1], y[2], y[3]);
         y4[1] = make_uint4(y[4], y[5], y[6], y[7]);
       }
+      if (DCF_WHS_REUSE) {  // the skipped B step of the next level: v[0:16) ^= B ^ ~s when it goes left
+        const uint32_t ml = 0u - (uint32_t)(reuse & ((L.cur[i] >> 31) == 0u));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) L.v[i][j] = xand(L.v[i][j], ml, L.dB[i][j]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -318,6 +369,8 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
                               tvec);
     }
   }
+  // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks), accumulated over passes
+  if ((threadIdx.x & 63u) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, (unsigned long long)nblk);
 }
 
 // One wide prefix node (80 B: s[0:32) | v[0:32) | {t, t-vector word 0, partial word, 0})

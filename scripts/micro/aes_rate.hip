@@ -60,6 +60,62 @@ __device__ __forceinline__ void aes256_tt_b(uint32_t (&st)[NB][4], const RoundKe
     for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
 }
 
+// Lookup of T_T at state byte K through the vector L1 instead of the LDS: the compact 4 KiB
+// T0..T3 image in global memory (L1-resident), offset (byte << 2) by a shift and a mask.
+template <int T, int K>
+__device__ __forceinline__ uint32_t lkg(const uint32_t* __restrict__ gt, uint32_t w) {
+  const uint32_t off = (K == 0 ? (w << 2) : (w >> (8 * K - 2))) & 0x3FCu;
+  // buffer load: 32-bit VGPR offset, resource in SGPRs (no 64-bit address VALU)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(gt), 0, 4096, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(rs, off, T * 1024, 0);
+}
+
+// Middle rounds with GN of the 16 lookups per round through the vector L1 (column j's T3
+// lookup for j < GN, then column j - 4's T2 lookup): LDS and L1 share the lookups.
+template <int NB, int GN>
+__device__ __forceinline__ void aes256_tt_mix(uint32_t (&st)[NB][4], const RoundKeys& rk, const uint32_t* lds,
+                                              uint32_t lc, const uint32_t* __restrict__ gt) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] ^= rk.w[j];
+#pragma unroll
+  for (int r = 1; r < 14; ++r) {
+    uint32_t o[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+        const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+        const uint32_t d = (j + 4 < GN) ? lkg<2, 2>(gt, st[b][(j + 2) & 3]) : lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+        const uint32_t e = (j < GN) ? lkg<3, 3>(gt, st[b][(j + 3) & 3]) : lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+        o[b][j] = xor3(xor3(a, c, d), e, rk.w[4 * r + j]);
+      }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+  uint32_t o[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+      const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+      const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+      const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+      const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
+      const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
+      o[b][j] = xor3(lo, hi, rk.w[56 + j]);
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+}
+
 template <int NB, int MODE>
 __global__ __launch_bounds__(1024, 1) void k_aes(const uint32_t* __restrict__ tab, const RoundKeys rk,
                                                  const uint4* __restrict__ rkg, uint32_t* out) {
@@ -76,6 +132,7 @@ __global__ __launch_bounds__(1024, 1) void k_aes(const uint32_t* __restrict__ ta
     if (MODE == 0) aes256_tt<NB>(st, rk, lds, lc);
     if (MODE == 1) aes256_tt_gk<NB>(st, rkg, lds, lc);
     if (MODE == 2) aes256_tt_b<NB>(st, rk, lds, lc, lc1);
+    if (MODE >= 10) aes256_tt_mix<NB, MODE - 10>(st, rk, lds, lc, tab);
   }
   uint32_t r = 0;
 #pragma unroll
@@ -131,7 +188,7 @@ void run(const char* name, int cus, const uint32_t* dtab, const RoundKeys& rk, c
   }
 }
 
-int main() {
+int main(int argc, char** argv) {
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   std::call_once(g_aes_once, aes_init_tables);
@@ -147,6 +204,33 @@ int main() {
   hipMemcpy(dtab, g_tab, sizeof(g_tab), hipMemcpyHostToDevice);
   hipMemcpy(rkg, rk.w, 240, hipMemcpyHostToDevice);
   printf("CUs %d\n", cus);
+  if (argc > 1 && !strcmp(argv[1], "mix")) {
+    // LDS + vector-L1 split of the lookups, and the outputs against the all-LDS rounds
+    for (int w : {4, 16}) {
+      printf("-- %d workgroups per CU\n", w);
+      run<2, 0>("all LDS", cus, dtab, rk, rkg, out, w);
+      run<2, 11>("1 of 16 via L1", cus, dtab, rk, rkg, out, w);
+      run<2, 12>("2 of 16 via L1", cus, dtab, rk, rkg, out, w);
+      run<2, 13>("3 of 16 via L1", cus, dtab, rk, rkg, out, w);
+      run<2, 14>("4 of 16 via L1", cus, dtab, rk, rkg, out, w);
+      run<2, 16>("6 of 16 via L1", cus, dtab, rk, rkg, out, w);
+      run<2, 18>("8 of 16 via L1", cus, dtab, rk, rkg, out, w);
+      run<3, 12>("2 of 16 via L1", cus, dtab, rk, rkg, out, w);
+      run<3, 14>("4 of 16 via L1", cus, dtab, rk, rkg, out, w);
+    }
+    const int n = cus * 1024;
+    uint32_t* o2;
+    hipMalloc(&o2, n * 4);
+    hipLaunchKernelGGL((k_aes<2, 0>), dim3(cus), dim3(1024), 0, 0, dtab, rk, rkg, out);
+    hipLaunchKernelGGL((k_aes<2, 16>), dim3(cus), dim3(1024), 0, 0, dtab, rk, rkg, o2);
+    std::vector<uint32_t> h1(n), h2(n);
+    hipMemcpy(h1.data(), out, n * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(h2.data(), o2, n * 4, hipMemcpyDeviceToHost);
+    int bad = 0;
+    for (int i = 0; i < n; ++i) bad += h1[i] != h2[i];
+    printf("6-via-L1 outputs vs all-LDS rounds: %d of %d differ\n", bad, n);
+    return 0;
+  }
   for (int w : {4, 16}) {
     printf("-- %d workgroups per CU (work items in flight)\n", w);
     run<1, 0>("sgpr keys", cus, dtab, rk, rkg, out, w);

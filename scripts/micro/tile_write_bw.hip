@@ -47,6 +47,9 @@ int main() {
   uint8_t* ys = nullptr;
   if (hipMalloc(&ys, count * lam) != hipSuccess) return 1;
   run<256>(ys, lam, count);
+  run<32>(ys, lam, count, 135168);   // narrower tiles: partial 128-B lines per workgroup
+  run<64>(ys, lam, count, 135168);
+  run<128>(ys, lam, count, 135168);
   run<256>(ys, lam, count, 135168);  // the tail's LDS: one 1024-thread workgroup per CU
   run<256>(ys, lam, count, 66000);
   run<512>(ys, lam, count);
