@@ -278,9 +278,9 @@ def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P, mode):
                                       (4096, 16, 12), (272, 5, 600), (512, 16, 5000), (16384, 16, 150)])
 def test_wide_eval_random_vs_oracle(dcf, lam, nb, m, mode):
     """LAMBDA >= 32: head/tail kernels vs the literal oracle, both parties, both bounds.
-    mode 0: stream head (default), mode 1: lockstep T-table head.  N = 16 runs the
-    compile-time 33-chunk tail; 5000 points cross tail workgroups (4096 points each)
-    and the two-ahead t-vector prefetch, 16384 covers 64 tiles per point."""
+    mode 0: stream head (default), mode 1: lockstep T-table head.  LAMBDA % 128 == 0 runs the
+    paired-slot tail (k_eval_wide_tail2), (64, 16) the compile-time 33-chunk 4-bit tail and
+    (48, 3), (112, 4), (272, 5) the runtime-chunk one; 16384 covers 128 tiles per point."""
     rng = np.random.default_rng(lam * 7 + nb)
     keys = [rng.bytes(32) for _ in range(18)]
     prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
@@ -292,6 +292,28 @@ def test_wide_eval_random_vs_oracle(dcf, lam, nb, m, mode):
         k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
         raw = ok.cw_s.tobytes() + ok.cw_v.tobytes() + ok.cw_t.tobytes()
         assert dcf.share_to_cwb(k, nb, lam) == raw + bytes((-len(raw)) % 16) + ok.cw_np1.tobytes()
+        xs = _rand(rng, (m, nb))
+        xs[0] = np.frombuffer(alpha, np.uint8)
+        for b, s in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+            assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, b, bound)
+
+
+@pytest.mark.parametrize("lam,nb,m", [(128, 1, 300), (256, 3, 200), (128, 4, 500), (384, 6, 300), (128, 8, 40000),
+                                      (256, 12, 150), (128, 16, 33000), (256, 5, 100)])
+def test_wide_tail2_layouts_vs_oracle(dcf, lam, nb, m):
+    """The paired-slot tail (k_eval_wide_tail2, LAMBDA % 128 == 0) in each instantiated chunk
+    layout: N = 1 (1,0), 3 and 4 (2,1), 6 and 8 (3,3), 12 and 16 (5,7), plus N = 5, which keeps
+    the 4-bit tail; 40000 / 33000 points cross the 32768-point workgroup ranges, and the t-vector
+    repack (k_tvec_chunks) runs in place on the head's rows."""
+    rng = np.random.default_rng(lam * 13 + nb)
+    keys = [rng.bytes(32) for _ in range(18)]
+    prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    for bound in (0, 1):
+        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+        ok = O.gen(P, alpha, beta, s0, s1, bound)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
         xs = _rand(rng, (m, nb))
         xs[0] = np.frombuffer(alpha, np.uint8)
         for b, s in ((0, s0), (1, s1)):
