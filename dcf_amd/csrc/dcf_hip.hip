@@ -506,7 +506,7 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
           if (rc) return rc;
         }
       }
-      const uint64_t units = (cnt + kStreamUnit - 1) / kStreamUnit;
+      const uint64_t units = (cnt + kWideUnit - 1) / kWideUnit;
       uint64_t blocks = (units + 15) / 16;
       if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
 #ifndef DCF_WHS_NS

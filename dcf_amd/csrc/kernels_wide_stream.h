@@ -98,6 +98,14 @@ __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, c
   }
 }
 
+// Points per refill of a wave.  A lane of C4 runs only ~16 points per launch (2^22 over 2^18
+// lanes), so the last units decide when the grid drains: 256-point units (4 per lane) left
+// ~11 % of the head's LDS instructions to lanes idling at the end (PMC: 265 per block vs 239).
+#ifndef DCF_WIDE_UNIT
+#define DCF_WIDE_UNIT 64
+#endif
+constexpr uint32_t kWideUnit = DCF_WIDE_UNIT;
+
 template <int NS, bool XREG>
 __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, uint64_t& unext, uint64_t& uend,
                                             bool& exhausted, uint32_t* __restrict__ ctr, uint64_t nunits,
@@ -111,8 +119,8 @@ __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, u
       if (u >= nunits) {
         exhausted = true;
       } else {
-        unext = (uint64_t)u * kStreamUnit;
-        uend = min(unext + kStreamUnit, count);
+        unext = (uint64_t)u * kWideUnit;
+        uend = min(unext + kWideUnit, count);
       }
     }
     if (exhausted && unext >= uend) {
@@ -172,7 +180,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   const __amdgpu_buffer_rsrc_t rkrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(rk2), (short)0, 480, 0x00020000);
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
-  const uint64_t nunits = (count + kStreamUnit - 1) / kStreamUnit;
+  const uint64_t nunits = (count + kWideUnit - 1) / kWideUnit;
   const uint32_t mlast = MASK_HEAD ? kMaskLast : 0xFFFFFFFFu;  // LAMBDA == 32: byte 31 is the cleared byte
   uint64_t unext = 0, uend = 0;
   bool exhausted = false;
