@@ -374,7 +374,8 @@ def run_eval(args, world, rank):
         # t = 0 (kernels_stream.h): counted by the kernel itself, plus the prefix table
         walk = dev_blocks / m if dev_blocks else (8 * nb - pfx) + zero_bits(xs, pfx) / m
         exec_bpe = walk + (2 ** (pfx + 1) - 2) / m
-    elif engine == "mmo":
+    elif engine == "mmo" or (engine == "ttable-small" and pfx):
+        # lockstep walks (A and B every level) below a forced shared prefix
         exec_bpe = 2 * (8 * nb - pfx) + (2 ** (pfx + 1) - 2) / m
     else:
         exec_bpe = bpe

@@ -233,6 +233,29 @@ uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint6
   return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
 }
 
+// Shared-prefix depth for the small-batch pair path (k_eval16_pair, auto mode, fewer points than
+// two per lane of the GPU): a C1-size batch walks its 8N levels back to back, so the table's
+// one-launch build (a few microseconds) is paid once against D levels saved on every point.
+// Auto (off by default, see below): log2(total) - DCF_SMALL_PFX_SUB from 2^DCF_SMALL_PFX_MIN
+// points; forced depths (dcf_prg_set_prefix_levels) always apply.
+#ifndef DCF_SMALL_PFX_SUB
+#define DCF_SMALL_PFX_SUB 1
+#endif
+#ifndef DCF_SMALL_PFX_MIN
+#define DCF_SMALL_PFX_MIN -1  // < 0: never in auto mode.  C1 A/B (same box, 300 steps, M evals/s): no table
+                              // 226.3-226.4, D = 14 / 15 / 16: 221.1-221.5 / 221.2-221.5 / 221.8-222.1 — the
+                              // build's D sequential levels on few workgroups cost what the walk saves
+#endif
+uint32_t small_prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t total) {
+  if (p->lambda != 16 || p->kind != 0 || p->prefix_levels == 0) return 0;
+  if (p->prefix_levels > 0) return std::min<uint32_t>(std::min((uint32_t)p->prefix_levels, kPrefixMaxForced),
+                                                      (uint32_t)(8 * n_bytes - 1));
+  if (DCF_SMALL_PFX_MIN < 0 || total < (1ull << (DCF_SMALL_PFX_MIN < 0 ? 0 : DCF_SMALL_PFX_MIN))) return 0;
+  const uint32_t lg = 63u - (uint32_t)__builtin_clzll(total | 1u);
+  if (lg < 8u + DCF_SMALL_PFX_SUB) return 0;
+  return capped_depth(p, std::min<uint32_t>(lg - DCF_SMALL_PFX_SUB, (uint32_t)(8 * n_bytes - 1)));
+}
+
 // Shared-prefix depth for the LAMBDA >= 32 stream head over m points of one key
 // (kernels_wide_stream.h WidePrefix): 80 B per node, 4 AES blocks per parent.
 // Auto: log2(m) - 1, at most 22 (two 336 MB node buffers at 2^22), none below 8.
@@ -752,7 +775,7 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   if (p->kind == 1 && p->lambda > 16) return 0;  // MMO at LAMBDA >= 32: no shared prefix (head/tail per block)
   if (p->kind == 1) return small && p->prefix_levels < 0 ? 0 : (int)prefix_depth(p, n_bytes, num_keys, total);
   if (p->lambda > 16) return n_bytes > 31 ? 0 : (int)wide_prefix_depth(p, n_bytes, points_per_key);
-  if (p->eval_mode == DCF_EVAL_AUTO && small) return 0;
+  if (p->eval_mode == DCF_EVAL_AUTO && small) return num_keys == 1 ? (int)small_prefix_depth(p, n_bytes, total) : 0;
   if (p->eval_mode != DCF_EVAL_AUTO && p->eval_mode != DCF_EVAL_STREAM && p->eval_mode != DCF_EVAL_STREAM_HYBRID)
     return 0;
   return (int)prefix_depth(p, n_bytes, num_keys, total);
@@ -936,6 +959,14 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #define DCF_SMALL_PAIR 1
 #endif
     if (int rc = ensure_rk0(p)) return rc;
+    PrefixTable spf{nullptr, 0u};
+    if (DCF_SMALL_PAIR && num_keys == 1) {
+      const uint32_t d = small_prefix_depth(p, n_bytes, total);
+      if (d) {
+        int rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &spf, st);
+        if (rc) return rc;
+      }
+    }
     const uint64_t lanes_per_point = DCF_SMALL_PAIR ? 2 : 1;
     uint64_t threads = (total * lanes_per_point + p->cus - 1) / p->cus;
     threads = ((threads + 63) / 64) * 64;
@@ -945,7 +976,7 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #define DCF_SMALL(MODE)                                                                                           \
   hipLaunchKernelGGL(k_eval16_pair<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,                  \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk,  \
-                     (uint4*)ys, p->d_rk0)
+                     (uint4*)ys, p->d_rk0, MODE == 0 ? spf : PrefixTable{nullptr, 0u})
 #else
 #define DCF_SMALL(MODE)                                                                                           \
   hipLaunchKernelGGL(k_eval16<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s,    \

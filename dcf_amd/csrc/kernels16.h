@@ -136,6 +136,26 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16(
   }
 }
 
+// Shared prefix (single key): the walk's state after its first `levels` levels depends
+// only on those bits of x, so the host expands that top tree once (the full-domain
+// level kernels, k_fd_level16 / k_fd_level16_mmo) into a table indexed by the prefix, and a point
+// starts at level `levels` from its table row.  levels = 0: no table.
+// Row i is 32 contiguous bytes, sv[2i] = s and sv[2i+1] = v, with t in s's bit 0 of
+// byte 15: below the root s is always masked there (s' = side & M ^ t*cw.s, and cw.s
+// is a XOR of two masked seeds, lib.rs:119-121 / prg.rs:63-68), so a point's start
+// is one 32-byte gather (one cache line) instead of three arrays' lines.
+struct PrefixTable {
+  const uint4* sv;
+  uint32_t levels;  // < 32 and < 8N
+};
+
+__device__ __forceinline__ void prefix_row(const PrefixTable& pf, uint32_t idx, uint4& s, uint4& v, uint32_t& t) {
+  s = pf.sv[2u * idx];
+  v = pf.sv[2u * idx + 1u];
+  t = (s.w >> 24) & 1u;
+  s.w &= kMaskLast;
+}
+
 // Small batches, two lanes per point: lane 2k encrypts A = AES(s), lane 2k + 1
 // B = AES(~s), they swap the result (DPP quad_perm 1,0,3,2) and both run the level
 // update (lib.rs:174-189).  Twice the waves of k_eval16 for the same points, each
@@ -151,7 +171,7 @@ __device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, 
                                               const uint8_t* __restrict__ cw_t, const uint4 np, const uint4 sv,
                                               uint32_t party, const uint8_t* __restrict__ x, uint32_t nbytes,
                                               uint64_t num_keys, uint64_t key, uint32_t odd,
-                                              const uint4* __restrict__ rkg) {
+                                              const uint4* __restrict__ rkg, const PrefixTable& pf) {
   const uint32_t nlev = 8u * nbytes;
   const uint32_t nchunk = (nbytes + 3u) >> 2;
   const uint32_t inv = 0u - odd;  // odd lane: ~s (B)
@@ -159,10 +179,18 @@ __device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, 
   uint32_t v[4] = {0u, 0u, 0u, 0u};
   uint32_t t = party;
   uint32_t lev = 0;
-  for (uint32_t c = 0; c < nchunk; ++c) {
-    uint32_t cur = load_bits32(x, c, nbytes);
+  if (pf.levels) {  // start at level D from the row named by x's first D bits (Msb0)
+    uint4 s4, v4;
+    prefix_row(pf, load_bits32(x, 0, nbytes) >> (32u - pf.levels), s4, v4, t);
+    s[0] = s4.x; s[1] = s4.y; s[2] = s4.z; s[3] = s4.w;
+    v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
+    lev = pf.levels;
+  }
+  for (uint32_t c = lev >> 5; c < nchunk; ++c) {
+    const uint32_t b0 = (32u * c < lev) ? (lev & 31u) : 0u;
+    uint32_t cur = load_bits32(x, c, nbytes) << b0;
     const uint32_t lend = min(32u, nlev - 32u * c);
-    for (uint32_t b = 0; b < lend; ++b, ++lev) {
+    for (uint32_t b = b0; b < lend; ++b, ++lev) {
       uint32_t st[1][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[0][j] = s[j] ^ inv;
@@ -210,7 +238,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_pair(
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys,
-    const uint4* __restrict__ rkg) {
+    const uint4* __restrict__ rkg, const PrefixTable pf) {
   __shared__ uint32_t lds[kLdsWords];
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
@@ -225,7 +253,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_pair(
     if (MODE == 2) key = gg / points_per_key;
     const uint32_t odd = threadIdx.x & 1u;
     const uint4 y = tt_eval_pair(lds, lc, rk, cw_s, cw_v, cw_t, cw_np1[key], s0s[key], party, xs + gg * nbytes,
-                                 nbytes, num_keys, key, odd, rkg);
+                                 nbytes, num_keys, key, odd, rkg, pf);
     if (live && !odd) ys[g] = y;
   }
 }
@@ -535,26 +563,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_tail16(
       }
     }
   }
-}
-
-// Shared prefix (single key): the walk's state after its first `levels` levels depends
-// only on those bits of x, so the host expands that top tree once (the full-domain
-// level kernels, k_fd_level16 / k_fd_level16_mmo) into a table indexed by the prefix, and a point
-// starts at level `levels` from its table row.  levels = 0: no table.
-// Row i is 32 contiguous bytes, sv[2i] = s and sv[2i+1] = v, with t in s's bit 0 of
-// byte 15: below the root s is always masked there (s' = side & M ^ t*cw.s, and cw.s
-// is a XOR of two masked seeds, lib.rs:119-121 / prg.rs:63-68), so a point's start
-// is one 32-byte gather (one cache line) instead of three arrays' lines.
-struct PrefixTable {
-  const uint4* sv;
-  uint32_t levels;  // < 32 and < 8N
-};
-
-__device__ __forceinline__ void prefix_row(const PrefixTable& pf, uint32_t idx, uint4& s, uint4& v, uint32_t& t) {
-  s = pf.sv[2u * idx];
-  v = pf.sv[2u * idx + 1u];
-  t = (s.w >> 24) & 1u;
-  s.w &= kMaskLast;
 }
 
 // Pack the prefix level's (s, v, t) arrays into PrefixTable rows.

@@ -299,6 +299,33 @@ def test_wide_eval_random_vs_oracle(dcf, lam, nb, m, mode):
             assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, b, bound)
 
 
+@pytest.mark.parametrize("nb,levels,m", [(16, 9, 3000), (16, 15, 20000), (16, 31, 5000), (4, 12, 4000), (3, 23, 2000),
+                                         (1, 5, 700), (5, 33, 1500), (16, -1, 20000), (2, -1, 40000)])
+def test_small_pair_prefix_vs_oracle(dcf, nb, levels, m):
+    """Small batches (auto engine: the two-lanes-per-point path, k_eval16_pair) below a
+    shared-prefix table: forced depths (D = 5 .. 31, x-word boundary at N = 3, 5); auto (-1)
+    builds none there (measured slower at C1); both parties and bounds, vs the oracle."""
+    rng = np.random.default_rng(4000 + 37 * nb + levels)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    prg.set_prefix_levels(levels)
+    want_d = min(levels, 28, 8 * nb - 1) if levels > 0 else 0  # auto: no table on the small path
+    assert prg.eval_prefix_levels(nb, 1, m) == want_d
+    d = dcf.DcfImpl(nb, 16, prg)
+    for bound in (0, 1):
+        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
+        ok = O.gen(P, alpha, beta, s0, s1, bound)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
+        xs = _rand(rng, (m, nb))
+        a = np.frombuffer(alpha, np.uint8)
+        xs[0] = a
+        xs[3:40] = a
+        xs[3:40, -1] = rng.integers(0, 256, 37, dtype=np.uint8)
+        for b, s in ((0, s0), (1, s1)):
+            got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+            assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (nb, levels, m, bound, b)
+
+
 @pytest.mark.parametrize("lam,nb,m", [(128, 1, 300), (256, 3, 200), (128, 4, 500), (384, 6, 300), (128, 8, 40000),
                                       (256, 12, 150), (128, 16, 33000), (256, 5, 100)])
 def test_wide_tail2_layouts_vs_oracle(dcf, lam, nb, m):
