@@ -246,6 +246,9 @@ __device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst
   return make_uint4(acc[0], acc[1], acc[2], acc[3]);
 }
 
+#ifndef DCF_TAIL_NT
+#define DCF_TAIL_NT 1  // C4 A/B (r02z, paired-slot tail): nt 36.0-36.2 ms, plain 36.9-37.0
+#endif
 // Non-temporal (written once, never re-read here: measured 4 % faster) buffer store of
 // a y piece; `kill` != 0 puts the lane's offset past num_records, which drops it.
 template <int LP>
@@ -257,7 +260,7 @@ __device__ __forceinline__ void tail_store(uint8_t* ys, uint64_t pw, uint32_t pi
   uint8_t* wb = reinterpret_cast<uint8_t*>((uintptr_t)(((uint64_t)hi << 32) | lo));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(wb, (short)0, (int)((64 / LP) * lam), 0x00020000);
   const u32x4 v = {y.x, y.y, y.z, y.w};
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (pin * lam + off) | kill, 0, 2 /* nt */);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (pin * lam + off) | kill, 0, DCF_TAIL_NT ? 2 /* nt */ : 0);
 }
 
 // ------------------------------------------------------------------------
@@ -506,7 +509,9 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   // lane constants (address byte 0 = slot, byte 2 = 64 KiB group): step i of a region reads
   // chunk 2m + (i ^ pi), whose entry sits in bytes [(i ^ pi) 128, +128) of the 256-B row
   const uint32_t lc0 = pi * 128u + 16u * q, lc1 = (pi ^ 1u) * 128u + 16u * q;
-  const uint32_t rsel = pi ? 0x02030001u : 0x03020100u;  // pi = 1: swap the chunk bytes of each region
+  // pi = 1: swap the chunk bytes of each region (stored pre-swapped by k_tvec_chunks instead, the
+  // tail has 6 fewer v_perm per point: C4 A/B 34.8-35.1 vs 34.5-34.8 ms, no gain — kept here)
+  const uint32_t rsel = pi ? 0x02030001u : 0x03020100u;
   const uint64_t p0 = (uint64_t)blockIdx.y * pts_per_block;
   const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
   const uint32_t pstep = blockDim.x / LP;
