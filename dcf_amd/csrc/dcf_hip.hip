@@ -440,7 +440,8 @@ int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, cons
 // repacked into chunk bytes in place, then the tail runs as launch_tail does.
 template <int R6, int R5>
 int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
-                 uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st) {
+                 uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
+                 int cus) {
   using L = Tail2Layout<R6, R5>;
   if (nlev + 1 > L::rows()) return fail(DCF_ERR_UNSUPPORTED, "tail2 layout too small");
   hipLaunchKernelGGL((k_tvec_chunks<R6, R5>), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tvec, nlev, cnt);
@@ -451,7 +452,18 @@ int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, con
 #ifndef DCF_TAIL2_PTS
 #define DCF_TAIL2_PTS 32768  // points per workgroup (one table build each; C4 A/B: 4096 37.8-38.0 ms, 8192 37.0-37.4, 16384 36.9-37.0, 32768 36.7-37.0, 65536 36.4-36.8)
 #endif
-  const uint64_t tiles = (lam + 127) / 128, per = DCF_TAIL2_PTS;
+  const uint64_t tiles = (lam + 127) / 128;
+  uint64_t per = DCF_TAIL2_PTS;
+#ifndef DCF_TAIL2_ONE_ROUND
+#define DCF_TAIL2_ONE_ROUND 1  // C4 A/B (same box, ms): 34.36-34.38 vs 34.78-35.01 with 32768-point ranges
+#endif
+  // One workgroup per CU: the batch split into cus / tiles ranges, so the tiles of a range
+  // build their tables once and walk its points together (the rows being written at any time
+  // stay few) instead of 128 workgroups per CU each building tables for 32768 points.
+  if (DCF_TAIL2_ONE_ROUND) {
+    const uint64_t ranges = std::max<uint64_t>(1, (uint64_t)cus / tiles);
+    per = std::max<uint64_t>(per, (((cnt + ranges - 1) / ranges) + 255) & ~(uint64_t)255);
+  }
   const dim3 grid((unsigned)tiles, (unsigned)((cnt + per - 1) / per));
   hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key,
                      tvec, cnt, (uint32_t)per, ys);
@@ -471,7 +483,7 @@ int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const u
   if (DCF_TAIL2 && lam % 128 == 0) {
 #define DCF_T2(A, B)                                                                            \
   if (nrows <= Tail2Layout<A, B>::rows() && 2u * (A + B) < nch)                                 \
-    return launch_tail2<A, B>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
+    return launch_tail2<A, B>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus);
     DCF_T2(1, 0)   // N = 1: 9 rows, 2 reads (4-bit: 3)
     DCF_T2(1, 1)   // N = 2: 17 rows, 4 reads (5)
     DCF_T2(2, 1)   // N = 3, 4: 25 / 33 rows, 6 reads (7 / 9)
