@@ -118,8 +118,9 @@ size_t dcf_prg_lambda(const dcf_prg* prg);
  * test knob only: every engine returns identical bytes. */
 int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 
-/* Shared prefix for single-key eval at LAMBDA = 16 (Hirose PRG: stream engine;
- * Aes128MatyasMeyerOseasPrg: every engine setting) and, per key, for the LAMBDA >= 32
+/* Shared prefix for single-key eval at LAMBDA = 16 (Hirose PRG: stream engine, and the
+ * automatic engine's small-batch path at forced depths; Aes128MatyasMeyerOseasPrg: every
+ * engine setting) and, per key, for the LAMBDA >= 32
  * stream head (bytes [0,32) of the walk and the t-vector rows, 80 B per node).
  * Every point's walk (lib.rs:174-189) passes through the node of the key's GGM
  * tree named by its first D bits, and that node's (s, v, t) depends on nothing
@@ -157,10 +158,11 @@ int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves, int slab_variant);
  *   priority:         1 = stream waves issue at raised priority (s_setprio). */
 int dcf_prg_set_stream_hybrid(dcf_prg* prg, unsigned ttable_wave_mask, int priority);
 
-/* AES blocks the last LAMBDA = 16 stream-engine eval on this prg encrypted for live
- * points (DCF_EVAL_STREAM / _STREAM_HYBRID's stream waves; not counting a shared-prefix
- * table build), counted on the device.  Measurement hook for the bench; call after
- * the eval's stream has been synchronized.  0 before any such eval. */
+/* AES blocks the last stream-engine eval on this prg encrypted for live points (LAMBDA = 16:
+ * DCF_EVAL_STREAM / _STREAM_HYBRID's stream waves; LAMBDA >= 32: the stream head over all of
+ * the call's passes; not counting a shared-prefix table build), counted on the device.
+ * Measurement hook for the bench; call after the eval's stream has been synchronized.  0
+ * before any such eval. */
 int dcf_prg_last_eval_blocks(dcf_prg* prg, uint64_t* blocks);
 
 /* CWB layout helpers (see above). */
