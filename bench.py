@@ -10,7 +10,7 @@ points are split into contiguous per-rank slices (strong scaling, dcf_point_slic
 generated once on rank 0 and broadcast over RCCL before timing; there is no
 collective inside the timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5|fd]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5|fd|lat]
                   [--scaling strong|weak] [--host-path]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
@@ -713,12 +713,98 @@ def run_fd(args, world, rank):
     return out
 
 
+def run_latency(args, world, rank):
+    """benches/dcf.rs: one gen, and one eval of ONE point, per call (criterion's bench_gen /
+    bench_eval, N = 16, lambda = 16) through the host-pointer entry points a Rust caller's
+    DcfHip would use (dcf_gen / dcf_eval: H2D, kernel, D2H, stream sync).  Reported as
+    microseconds per call, with and without building the PRG inside the call as the
+    reference's bench does (Aes256HirosePrg::new + DcfImpl::new per iteration; here that is
+    dcf_prg_new: key schedules, tables and device buffers).  CPU beside it: the C restatement,
+    1 thread, same calls.  Latency, not throughput: the GPU's launch and PCIe round trips
+    bound it."""
+    from oracle import oracle as O
+    nb, lam = 16, 16
+    rng = np.random.default_rng(0xDCF0005)
+    keys = [rng.bytes(32) for _ in range(2)]
+    dev = torch.cuda.current_device()
+    prg = dcf_amd.Aes256HirosePrg(keys, lam, device=dev)
+    d = dcf_amd.DcfImpl(nb, lam, prg)
+    s0s = [rng.bytes(lam), rng.bytes(lam)]
+    f = dcf_amd.CmpFn(rng.bytes(nb), rng.bytes(lam))
+    k = d.gen(f, s0s, dcf_amd.BoundState.LtBeta)
+    share0 = dcf_amd.Share([s0s[0]], k.cws, k.cw_np1)
+    x = [rng.bytes(nb)]
+    iters = max(50, args.steps * 40)
+
+    def per_call(fn, n):
+        for _ in range(max(5, n // 10)):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        return (time.perf_counter() - t0) / n * 1e6
+
+    # the C ABI calls a Rust DcfHip makes (dcf_gen / dcf_eval on host buffers), buffers packed once
+    from dcf_amd._lib import check
+    from dcf_amd.dcf import _ptr
+    lib = dcf_amd.load()
+    h = prg.handle
+    a_b, b_b, s0_b, s1_b = bytes(f.alpha), bytes(f.beta), bytes(s0s[0]), bytes(s0s[1])
+    cwb = np.frombuffer(dcf_amd.share_to_cwb(k, nb, lam), np.uint8).copy()
+    cw_out = np.zeros_like(cwb)
+    xb = np.frombuffer(x[0], np.uint8).copy()
+    yb = np.zeros(lam, np.uint8)
+
+    def c_gen():
+        check(lib.dcf_gen(h, nb, _ptr(a_b), _ptr(b_b), _ptr(s0_b), _ptr(s1_b), 0, _ptr(cw_out)))
+
+    def c_eval():
+        check(lib.dcf_eval(h, nb, 0, _ptr(cwb), cwb.size, _ptr(s0_b), _ptr(xb), 1, _ptr(yb), lam))
+
+    gen_us = per_call(c_gen, iters)
+    eval_us = per_call(c_eval, iters)
+    assert np.array_equal(cw_out, cwb), "dcf_gen bytes differ from DcfImpl.gen's"
+    y_gpu = yb.reshape(1, lam).copy()
+    py_gen_us = per_call(lambda: d.gen(f, s0s, dcf_amd.BoundState.LtBeta), max(20, iters // 4))
+    py_eval_us = per_call(lambda: d.eval(False, share0, x), max(20, iters // 4))
+
+    def gen_fresh():
+        pr = dcf_amd.Aes256HirosePrg(keys, lam, device=dev)
+        dcf_amd.DcfImpl(nb, lam, pr).gen(f, s0s, dcf_amd.BoundState.LtBeta)  # pr freed on return
+
+    def eval_fresh():
+        pr = dcf_amd.Aes256HirosePrg(keys, lam, device=dev)
+        dcf_amd.DcfImpl(nb, lam, pr).eval(False, share0, x)  # pr freed on return
+
+    gen_fresh_us = per_call(gen_fresh, max(20, iters // 20))
+    eval_fresh_us = per_call(eval_fresh, max(20, iters // 20))
+    P = O.OraclePrg(keys, lam)
+    ok = O.gen(P, f.alpha, f.beta, s0s[0], s0s[1], 0)
+    xs = np.frombuffer(x[0], np.uint8).reshape(1, nb).copy()
+    cpu_gen_us = per_call(lambda: O.gen(P, f.alpha, f.beta, s0s[0], s0s[1], 0), iters)
+    cpu_eval_us = per_call(lambda: O.eval_(P, 0, ok, s0s[0], xs, nthreads=1), iters)
+    match = bool(np.array_equal(np.asarray(y_gpu), O.eval_(P, 0, ok, s0s[0], xs, nthreads=1)))
+    return {"metric": "benches/dcf.rs latency: one gen / one single-point eval per call (us)", "value": eval_us,
+            "unit": "us per single-point eval (host path)", "n_gpus": 1, "steps": iters, "warmup": iters // 10,
+            "ms_per_step": eval_us / 1e3, "higher_is_better": False, "scaling": "none", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "LAT: benches/dcf.rs bench_gen / bench_eval, N=16, lambda=16, Aes256HirosePrg "
+                                   "(2 AES keys), one key, one point, host buffers", "n_bytes": nb, "lambda": lam},
+            "gen_us": gen_us, "eval_us": eval_us, "python_api_gen_us": py_gen_us, "python_api_eval_us": py_eval_us,
+            "gen_with_prg_new_us": gen_fresh_us, "eval_with_prg_new_us": eval_fresh_us,
+            "cpu_baseline": {"gen_us": cpu_gen_us, "eval_us": cpu_eval_us, "cores": 1, "kind": "port",
+                             "sample": f"{iters} calls each, the C restatement with AES-NI, 1 thread",
+                             "matches_gpu": match},
+            "note": "latency-bound: a call is a kernel launch plus PCIe copies and a stream sync on the "
+                    "prg's streams; batch the points (C1) for throughput"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5", "fd"])
+    ap.add_argument("--workload", default="c3", choices=["c1", "c2", "c3", "c4", "c5", "fd", "lat"])
     ap.add_argument("--points", type=int, default=None)
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--n-bytes", type=int, default=None)
@@ -763,13 +849,15 @@ def main():
         args.n_bytes = args.n_bytes or 16
         args.points = args.points or (1 << 28)
     world, rank, _ = dist_setup(args.gpus, args.dist_backend)
-    if args.workload == "c5":
+    if args.workload == "lat":
+        out = run_latency(args, world, rank)
+    elif args.workload == "c5":
         out = run_c5(args, world, rank)
     elif args.workload == "fd":
         out = run_fd(args, world, rank)
     else:
         out = run_eval(args, world, rank)
-    if args.workload != "fd" and (args.workload != "c3" or args.prg != "hirose"):
+    if args.workload not in ("fd", "lat") and (args.workload != "c3" or args.prg != "hirose"):
         out["metric"] = (f"DCF evals/sec, workload {args.workload.upper()}, {args.prg} PRG "
                          "(not the BASELINE.json headline config)")
     if rank == 0:
