@@ -450,7 +450,7 @@ int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, con
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 #ifndef DCF_TAIL2_PTS
-#define DCF_TAIL2_PTS 32768  // points per workgroup (one table build each; C4 A/B: 4096 37.8-38.0 ms, 8192 37.0-37.4, 16384 36.9-37.0, 32768 36.7-37.0, 65536 36.4-36.8)
+#define DCF_TAIL2_PTS 32768  // at least this many points per workgroup (one table build each; C4 A/B: 4096 37.8-38.0 ms, 8192 37.0-37.4, 16384 36.9-37.0, 32768 36.7-37.0, 65536 36.4-36.8)
 #endif
   const uint64_t tiles = (lam + 127) / 128;
   uint64_t per = DCF_TAIL2_PTS;
@@ -511,6 +511,8 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
   if (rc) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(p->d_ws);
   WidePrefix wpf{nullptr, 0u};
+  // the lockstep head counts no blocks: dcf_prg_last_eval_blocks then reads 0, not a stale count
+  if (p->eval_mode == DCF_EVAL_TTABLE && p->d_ctr) HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = (m - off < chunk) ? m - off : chunk;
     const dim3 grid((unsigned)grid_for(cnt, p->cus));
