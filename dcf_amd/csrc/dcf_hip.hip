@@ -2,7 +2,7 @@
 //
 // Replaces the hot path of the `dcf` crate (xymeng16/dcf v0.2.2):
 //   DcfImpl::eval  (lib.rs:163-204)   -> k_eval16 (one lane per (key, point))
-//   DcfImpl::gen   (lib.rs:86-161)    -> k_gen16  (one lane per key, batched)
+//   DcfImpl::gen   (lib.rs:86-161)    -> k_gen16  (batched; a lane quad or one lane per key)
 //   Aes256HirosePrg::gen (prg.rs:42-73) inlined into both (hirose16)
 // The C ABI is declared in include/dcf_hip.h.  No CPU fallback: every compute
 // entry point runs a kernel or returns an error.
@@ -895,17 +895,29 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
     }
     return DCF_OK;
   }
-  // Large batches: 64-key units from the work counter (waves drift apart, as in k_eval16).
+  // Large batches: 64-lane units from the work counter (waves drift apart, as in k_eval16).
+  // Lanes per key: a quad while the batch leaves lanes idle (a key's 8N levels take a quarter of
+  // the AES latency: single gen 826 -> 266 us), one lane per key for large batches (2^20 keys:
+  // 7.5-7.6 ms with one lane, 8.0 with quads — the four lanes repeat the level update).
+#ifndef DCF_GEN_QUAD_MAX
+#define DCF_GEN_QUAD_MAX ((uint64_t)p->cus * kBlock / 2)  // keys
+#endif
+  const bool quad = (uint64_t)num_keys <= DCF_GEN_QUAD_MAX;
+  const uint64_t items = (uint64_t)num_keys * (quad ? 4u : 1u);
   uint32_t* ctr = nullptr;
-  if (num_keys >= (uint64_t)p->cus * kBlock * 2 && (num_keys + 63) / 64 <= 0xFFFFFFFFull) {
+  if (items >= (uint64_t)p->cus * kBlock * 2 && (items + 63) / 64 <= 0xFFFFFFFFull) {
     if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
     HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, (hipStream_t)stream));
     ctr = p->d_ctr;
   }
-  hipLaunchKernelGGL(k_gen16, dim3((unsigned)grid_for(num_keys, p->cus)), dim3(kBlock), 0, (hipStream_t)stream,
-                     p->d_tab, p->rk[0], alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1,
-                     (uint32_t)bound, (uint32_t)n_bytes, (uint64_t)num_keys, (uint4*)cws, (uint4*)cwv, cwt,
-                     (uint4*)np1, ctr);
+#define DCF_GEN16(L)                                                                                             \
+  hipLaunchKernelGGL(k_gen16<L>, dim3((unsigned)grid_for(items, p->cus)), dim3(kBlock), 0, (hipStream_t)stream,   \
+                     p->d_tab, p->rk[0], alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1,       \
+                     (uint32_t)bound, (uint32_t)n_bytes, (uint64_t)num_keys, (uint4*)cws, (uint4*)cwv, cwt,      \
+                     (uint4*)np1, ctr)
+  if (quad) DCF_GEN16(4);
+  else DCF_GEN16(1);
+#undef DCF_GEN16
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }

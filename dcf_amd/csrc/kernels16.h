@@ -259,9 +259,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_pair(
 }
 
 // ------------------------------------------------------------------------
-// k_gen16: DcfImpl::gen (lib.rs:86-161) at LAMBDA = 16, one lane per key.
-// Four AES blocks per level (PRG on both parties' seeds, lib.rs:103-104).
+// k_gen16: DcfImpl::gen (lib.rs:86-161) at LAMBDA = 16.  Four AES blocks per level
+// (PRG on both parties' seeds, lib.rs:103-104): LANES = 1, one lane per key encrypts all
+// four; LANES = 4, a lane quad per key, lane q encrypts block q (A0, B0, A1, B1) and a DPP
+// broadcast per word hands every lane of the quad all four, which then run the same
+// level update (a key's 8N levels take a quarter of the AES latency: single-key gen).
 // ------------------------------------------------------------------------
+template <int LANES>
 __global__ __launch_bounds__(kBlock, 1) void k_gen16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ alpha,
     const uint4* __restrict__ beta, const uint4* __restrict__ s0_0, const uint4* __restrict__ s0_1,
@@ -274,11 +278,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16(
   const uint32_t nchunk = (nbytes + 3u) >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t first = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
-  for (uint64_t base = ctr ? next_wave_base(ctr, 0, 0) : first; base < num_keys;
+  const uint64_t items = num_keys * LANES;
+  for (uint64_t base = ctr ? next_wave_base(ctr, 0, 0) : first; base < items;
        base = next_wave_base(ctr, base, stride)) {
     const uint64_t g = base + (threadIdx.x & 63u);
-    const bool live = g < num_keys;
-    const uint64_t k = live ? g : num_keys - 1;
+    const bool live = g < items;
+    const uint64_t k = (live ? g : items - 1) / LANES;
+    const uint32_t q = (uint32_t)(g % LANES);  // LANES = 4: this lane's block (0 A0, 1 B0, 2 A1, 3 B1)
     uint32_t s[2][4], va[4] = {0u, 0u, 0u, 0u}, be[4];
     {
       const uint4 a0 = s0_0[k], a1 = s0_1[k], bb = beta[k];
@@ -294,14 +300,29 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16(
       const uint32_t lend = min(32u, nlev - 32u * c);
       for (uint32_t b = 0; b < lend; ++b, ++lev) {
         uint32_t st[4][4];
+        if (LANES == 1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          st[0][j] = s[0][j];
-          st[1][j] = ~s[0][j];
-          st[2][j] = s[1][j];
-          st[3][j] = ~s[1][j];
+          for (int j = 0; j < 4; ++j) {
+            st[0][j] = s[0][j];
+            st[1][j] = ~s[0][j];
+            st[2][j] = s[1][j];
+            st[3][j] = ~s[1][j];
+          }
+          aes256_tt<4>(st, rk, lds, lc);  // A0, B0, A1, B1
+        } else {
+          uint32_t one[1][4];
+          const uint32_t inv = 0u - (q & 1u);  // B blocks encrypt ~s
+#pragma unroll
+          for (int j = 0; j < 4; ++j) one[0][j] = ((q >> 1) ? s[1][j] : s[0][j]) ^ inv;
+          aes256_tt<1>(one, rk, lds, lc);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // quad_perm broadcasts of lane b's block (b, b, b, b)
+            st[0][j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)one[0][j], 0x00, 0xF, 0xF, true);
+            st[1][j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)one[0][j], 0x55, 0xF, 0xF, true);
+            st[2][j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)one[0][j], 0xAA, 0xF, 0xF, true);
+            st[3][j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)one[0][j], 0xFF, 0xF, 0xF, true);
+          }
         }
-        aes256_tt<4>(st, rk, lds, lc);  // A0, B0, A1, B1
         const uint32_t a = cur >> 31;   // alpha_i, Msb0 (lib.rs:106)
         cur <<= 1;
         const uint32_t am = 0u - a;     // all ones when keep = R, lose = L
@@ -341,15 +362,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16(
         const uint32_t nt1 = (a ? tr1 : tl1) ^ (t1 & tkcw);
         t0 = nt0;
         t1 = nt1;
-        if (live) {
+        if (live) {  // LANES = 4: the quad's lanes 0, 1, 2 store one output each
           const uint64_t ci = (uint64_t)lev * num_keys + k;
-          cw_s[ci] = make_uint4(scw[0], scw[1], scw[2], scw[3]);
-          cw_v[ci] = make_uint4(vcw[0], vcw[1], vcw[2], vcw[3]);
-          cw_t[ci] = (uint8_t)(tlcw | (trcw << 1));
+          if (LANES == 1 || q == 0) cw_s[ci] = make_uint4(scw[0], scw[1], scw[2], scw[3]);
+          if (LANES == 1 || q == 1) cw_v[ci] = make_uint4(vcw[0], vcw[1], vcw[2], vcw[3]);
+          if (LANES == 1 || q == 2) cw_t[ci] = (uint8_t)(tlcw | (trcw << 1));
         }
       }
     }
-    if (live)  // lib.rs:155
+    if (live && (LANES == 1 || q == 0))  // lib.rs:155
       cw_np1[k] = make_uint4(s[0][0] ^ s[1][0] ^ va[0], s[0][1] ^ s[1][1] ^ va[1], s[0][2] ^ s[1][2] ^ va[2],
                              s[0][3] ^ s[1][3] ^ va[3]);
   }
