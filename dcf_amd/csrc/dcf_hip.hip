@@ -1106,6 +1106,30 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
       sct = p->d_kdig + (size_t)num_keys * n * 32;
     }
     PrefixTable pf{nullptr, 0u};
+    if (multi && DCF_MK_PFX && p->prefix_levels != 0 && n > kMkPfxLevels && ppk >= 32 &&
+        num_keys <= (1ull << (31 - kMkPfxLevels))) {
+      const size_t need = (size_t)num_keys * (32u << kMkPfxLevels);
+      if (p->pfx_bytes < need) {
+        if (p->d_pfx) {
+          HIP_TRY(hipStreamSynchronize(st));
+          HIP_TRY(hipFree(p->d_pfx));
+          p->d_pfx = nullptr;
+          p->pfx_bytes = 0;
+        }
+        if (hipMalloc(&p->d_pfx, need) != hipSuccess) {
+          (void)hipGetLastError();  // no room: walk from the root (same output bytes)
+        } else {
+          p->pfx_bytes = need;
+        }
+      }
+      if (p->pfx_bytes >= need) {
+        hipLaunchKernelGGL(k_mk_prefix16<true>, dim3((unsigned)((num_keys * 8 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           st, p->d_tab, p->rk[0], cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party,
+                           (uint64_t)num_keys, (uint4*)p->d_pfx, p->d_rk0, p->d_ctr);
+        HIP_TRY(hipGetLastError());
+        pf = PrefixTable{(const uint4*)p->d_pfx, kMkPfxLevels};
+      }
+    }
     if (!multi) {
       const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
       if (d) {

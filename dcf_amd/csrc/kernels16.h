@@ -629,6 +629,78 @@ __device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, co
   tr = ((st[1][0] ^ ~s[0]) & 1u) ^ (t & (ct >> 1) & 1u);
 }
 
+// Multi-key top trees: for each of K keys, its PrefixTable rows of depth 6 (64 rows per
+// key, row k * 64 + the point's top 6 x bits), so a key's points start on level 6 instead of
+// each walking levels 0..5 (C5: 64 points per key share the top of the tree).  Thread
+// (key k, node j of level 3) walks root -> j (3 PRG calls), then expands j's subtree
+// depth-first to its 8 leaves (7 calls): 80 PRG calls per key instead of 64 x 6 walks.
+// Same node values as the lockstep / stream walks (fd_children: lib.rs:176-189).
+#ifndef DCF_MK_PFX
+#define DCF_MK_PFX 1  // multi-key stream eval: per-key top trees (dcf_hip.hip, >= 32 points per key)
+#endif
+constexpr uint32_t kMkPfxLevels = 6;
+template <bool GKB = true>
+__global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
+    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ s0s,
+    const uint32_t party, const uint64_t num_keys, uint4* __restrict__ table, const uint4* __restrict__ rkg,
+    uint32_t* __restrict__ ctr) {
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t k = g >> 3;
+  // the eval's AES block count (dcf_prg_last_eval_blocks) includes the trees: 10 PRG calls
+  // of 2 blocks per thread
+  const uint64_t live = __ballot(k < num_keys);
+  if ((threadIdx.x & 63u) == 0 && live)
+    atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, 20ull * (unsigned long long)__popcll(live));
+  if (k >= num_keys) return;  // after the only barrier (lds_fill_tables)
+  const uint32_t j = (uint32_t)g & 7u;
+  auto cw = [&](uint32_t lev, uint32_t (&csw)[4], uint32_t (&cvw)[4]) {
+    const uint4 cs = cw_s[(uint64_t)lev * num_keys + k], cv = cw_v[(uint64_t)lev * num_keys + k];
+    csw[0] = cs.x; csw[1] = cs.y; csw[2] = cs.z; csw[3] = cs.w;
+    cvw[0] = cv.x; cvw[1] = cv.y; cvw[2] = cv.z; cvw[3] = cv.w;
+    return (uint32_t)cw_t[(uint64_t)lev * num_keys + k];
+  };
+  const uint4 sv = s0s[k];
+  uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w}, v[4] = {0u, 0u, 0u, 0u}, t = party;
+  for (uint32_t lev = 0; lev < 3; ++lev) {
+    uint32_t csw[4], cvw[4];
+    const uint32_t ct = cw(lev, csw, cvw);
+    uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
+    fd_children<GKB>(lds, lc, rk, csw, cvw, ct, s, v, t, sl, vl, tl, sr, vr, tr, rkg);
+    const bool right = (j >> (2u - lev)) & 1u;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      s[w] = right ? sr[w] : sl[w];
+      v[w] = right ? vr[w] : vl[w];
+    }
+    t = right ? tr : tl;
+  }
+  uint32_t c3s[4], c3v[4], c4s[4], c4v[4], c5s[4], c5v[4];
+  const uint32_t c3t = cw(3, c3s, c3v), c4t = cw(4, c4s, c4v), c5t = cw(5, c5s, c5v);
+  uint4* out = table + 2u * ((k << kMkPfxLevels) + 8u * j);
+  auto put = [&](uint32_t leaf, const uint32_t (&ls)[4], const uint32_t (&lv)[4], uint32_t lt) {
+    out[2u * leaf] = make_uint4(ls[0], ls[1], ls[2], (ls[3] & kMaskLast) | ((lt & 1u) << 24));
+    out[2u * leaf + 1u] = make_uint4(lv[0], lv[1], lv[2], lv[3]);
+  };
+  uint32_t as[2][4], av[2][4], at[2];  // level 4
+  fd_children<GKB>(lds, lc, rk, c3s, c3v, c3t, s, v, t, as[0], av[0], at[0], as[1], av[1], at[1], rkg);
+#pragma unroll
+  for (uint32_t b4 = 0; b4 < 2; ++b4) {
+    uint32_t bs[2][4], bv[2][4], bt[2];  // level 5
+    fd_children<GKB>(lds, lc, rk, c4s, c4v, c4t, as[b4], av[b4], at[b4], bs[0], bv[0], bt[0], bs[1], bv[1], bt[1], rkg);
+#pragma unroll
+    for (uint32_t b5 = 0; b5 < 2; ++b5) {
+      uint32_t ls[4], lv[4], lt, rs[4], rv[4], rt;  // level 6
+      fd_children<GKB>(lds, lc, rk, c5s, c5v, c5t, bs[b5], bv[b5], bt[b5], ls, lv, lt, rs, rv, rt, rkg);
+      put(4u * b4 + 2u * b5, ls, lv, lt);
+      put(4u * b4 + 2u * b5 + 1u, rs, rv, rt);
+    }
+  }
+}
+
 // Shared-prefix table (PrefixTable rows) of depth D in ONE launch, Hirose PRG.
 // The level-by-level build (k_fd_level16, one launch per level) spends most of its time
 // on the narrow upper levels (C2: 23 launches, ~1 ms of a 5 ms step).  Here workgroup w

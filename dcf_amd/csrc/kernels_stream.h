@@ -144,10 +144,11 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
     w0 = load_bits32(row, 0, nbytes);
   }
   uint32_t lev0 = 0u;
-  if (!MULTI && (PFX || pf.levels)) {  // start below the shared prefix: its row of the top-tree table
-    lev0 = pf.levels;
+  if ((!MULTI || DCF_MK_PFX) && (PFX || pf.levels)) {  // start below the shared prefix: its row of the top-tree table
+    lev0 = pf.levels;      // (MULTI: the key's own top tree, k_mk_prefix16, rows k * 2^levels + ...)
     uint4 sv, vv;
-    prefix_row(pf, w0 >> (32u - lev0), sv, vv, L.t[i]);
+    const uint32_t top = w0 >> (32u - lev0);
+    prefix_row(pf, MULTI ? (uint32_t)((k << lev0) + top) : top, sv, vv, L.t[i]);
     L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
     L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
   } else {

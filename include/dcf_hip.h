@@ -132,7 +132,10 @@ int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
  *                22), none below 8 or (LAMBDA = 16) for small batches;
  *   levels =  0: off;  levels > 0: that depth (capped at 28 (LAMBDA >= 32: 30) and
  *                at 8N - 1).
- * The table lives on the prg (its size follows the largest D used). */
+ * The table lives on the prg (its size follows the largest D used).
+ * Multi-key stream eval (LAMBDA = 16, >= 32 points per key, 8N > 6 levels):
+ * each key's own top tree of depth 6 (64 rows of 32 B per key, 80 PRG calls per key)
+ * unless levels = 0; if its buffer cannot be allocated the points walk from the root. */
 int dcf_prg_set_prefix_levels(dcf_prg* prg, int levels);
 /* The prefix depth D a dcf_eval* call of this shape would use (0 = none). */
 int dcf_eval_prefix_levels(const dcf_prg* prg, size_t n_bytes, size_t num_keys, size_t points_per_key);
@@ -160,7 +163,8 @@ int dcf_prg_set_stream_hybrid(dcf_prg* prg, unsigned ttable_wave_mask, int prior
 
 /* AES blocks the last stream-engine eval on this prg encrypted for live points (LAMBDA = 16:
  * DCF_EVAL_STREAM / _STREAM_HYBRID's stream waves; LAMBDA >= 32: the stream head over all of
- * the call's passes; not counting a shared-prefix table build), counted on the device.
+ * the call's passes; not counting a shared-prefix table build, except the multi-key
+ * per-key top trees, whose blocks are included), counted on the device.
  * Measurement hook for the bench; call after the eval's stream has been synchronized.  0
  * before any such eval. */
 int dcf_prg_last_eval_blocks(dcf_prg* prg, uint64_t* blocks);
