@@ -1123,7 +1123,8 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
         }
       }
       if (p->pfx_bytes >= need) {
-        hipLaunchKernelGGL(k_mk_prefix16<true>, dim3((unsigned)((num_keys * 8 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+        hipLaunchKernelGGL(k_mk_prefix16<true>,
+                           dim3((unsigned)(((num_keys << kMkPfxRoot) + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            st, p->d_tab, p->rk[0], cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party,
                            (uint64_t)num_keys, (uint4*)p->d_pfx, p->d_rk0, p->d_ctr);
         HIP_TRY(hipGetLastError());

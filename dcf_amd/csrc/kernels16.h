@@ -638,7 +638,11 @@ __device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, co
 #ifndef DCF_MK_PFX
 #define DCF_MK_PFX 1  // multi-key stream eval: per-key top trees (dcf_hip.hip, >= 32 points per key)
 #endif
-constexpr uint32_t kMkPfxLevels = 6;
+#ifndef DCF_MK_PFX_LEVELS
+#define DCF_MK_PFX_LEVELS 6
+#endif
+constexpr uint32_t kMkPfxLevels = DCF_MK_PFX_LEVELS;  // 4..6
+constexpr uint32_t kMkPfxRoot = kMkPfxLevels - 3u;     // levels walked from the root per thread
 template <bool GKB = true>
 __global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
@@ -649,14 +653,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t k = g >> 3;
-  // the eval's AES block count (dcf_prg_last_eval_blocks) includes the trees: 10 PRG calls
-  // of 2 blocks per thread
+  const uint64_t k = g >> kMkPfxRoot;
+  // the eval's AES block count (dcf_prg_last_eval_blocks) includes the trees: kMkPfxRoot + 7
+  // PRG calls of 2 blocks per thread
   const uint64_t live = __ballot(k < num_keys);
   if ((threadIdx.x & 63u) == 0 && live)
-    atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, 20ull * (unsigned long long)__popcll(live));
+    atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1,
+              2ull * (kMkPfxRoot + 7u) * (unsigned long long)__popcll(live));
   if (k >= num_keys) return;  // after the only barrier (lds_fill_tables)
-  const uint32_t j = (uint32_t)g & 7u;
+  const uint32_t j = (uint32_t)g & ((1u << kMkPfxRoot) - 1u);
   auto cw = [&](uint32_t lev, uint32_t (&csw)[4], uint32_t (&cvw)[4]) {
     const uint4 cs = cw_s[(uint64_t)lev * num_keys + k], cv = cw_v[(uint64_t)lev * num_keys + k];
     csw[0] = cs.x; csw[1] = cs.y; csw[2] = cs.z; csw[3] = cs.w;
@@ -665,12 +670,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
   };
   const uint4 sv = s0s[k];
   uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w}, v[4] = {0u, 0u, 0u, 0u}, t = party;
-  for (uint32_t lev = 0; lev < 3; ++lev) {
+  for (uint32_t lev = 0; lev < kMkPfxRoot; ++lev) {
     uint32_t csw[4], cvw[4];
     const uint32_t ct = cw(lev, csw, cvw);
     uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
     fd_children<GKB>(lds, lc, rk, csw, cvw, ct, s, v, t, sl, vl, tl, sr, vr, tr, rkg);
-    const bool right = (j >> (2u - lev)) & 1u;
+    const bool right = (j >> (kMkPfxRoot - 1u - lev)) & 1u;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       s[w] = right ? sr[w] : sl[w];
@@ -679,7 +684,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
     t = right ? tr : tl;
   }
   uint32_t c3s[4], c3v[4], c4s[4], c4v[4], c5s[4], c5v[4];
-  const uint32_t c3t = cw(3, c3s, c3v), c4t = cw(4, c4s, c4v), c5t = cw(5, c5s, c5v);
+  constexpr uint32_t A = kMkPfxRoot;
+  const uint32_t c3t = cw(A, c3s, c3v), c4t = cw(A + 1, c4s, c4v), c5t = cw(A + 2, c5s, c5v);
   uint4* out = table + 2u * ((k << kMkPfxLevels) + 8u * j);
   auto put = [&](uint32_t leaf, const uint32_t (&ls)[4], const uint32_t (&lv)[4], uint32_t lt) {
     out[2u * leaf] = make_uint4(ls[0], ls[1], ls[2], (ls[3] & kMaskLast) | ((lt & 1u) << 24));
