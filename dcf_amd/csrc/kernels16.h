@@ -629,17 +629,17 @@ __device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, co
   tr = ((st[1][0] ^ ~s[0]) & 1u) ^ (t & (ct >> 1) & 1u);
 }
 
-// Multi-key top trees: for each of K keys, its PrefixTable rows of depth 6 (64 rows per
-// key, row k * 64 + the point's top 6 x bits), so a key's points start on level 6 instead of
-// each walking levels 0..5 (C5: 64 points per key share the top of the tree).  Thread
-// (key k, node j of level 3) walks root -> j (3 PRG calls), then expands j's subtree
-// depth-first to its 8 leaves (7 calls): 80 PRG calls per key instead of 64 x 6 walks.
+// Multi-key top trees: for each of K keys, its PrefixTable rows of depth D (2^D rows per
+// key, row k * 2^D + the point's top D x bits), so a key's points start on level D instead of
+// each walking levels 0..D-1 (C5: 64 points per key share the top of the tree).  Thread
+// (key k, node j of level D - 3) walks root -> j (D - 3 PRG calls), then expands j's subtree
+// depth-first to its 8 leaves (7 calls): D = 5: 36 PRG calls per key instead of 64 x 5 walks.
 // Same node values as the lockstep / stream walks (fd_children: lib.rs:176-189).
 #ifndef DCF_MK_PFX
 #define DCF_MK_PFX 1  // multi-key stream eval: per-key top trees (dcf_hip.hip, >= 32 points per key)
 #endif
 #ifndef DCF_MK_PFX_LEVELS
-#define DCF_MK_PFX_LEVELS 6
+#define DCF_MK_PFX_LEVELS 5  // C5 A/B (same box, M evals/s): 6 400.5-400.8, 5 402.0-402.6, 4 401.2-401.7
 #endif
 constexpr uint32_t kMkPfxLevels = DCF_MK_PFX_LEVELS;  // 4..6
 constexpr uint32_t kMkPfxRoot = kMkPfxLevels - 3u;     // levels walked from the root per thread

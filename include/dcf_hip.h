@@ -134,7 +134,7 @@ int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
  *                at 8N - 1).
  * The table lives on the prg (its size follows the largest D used).
  * Multi-key stream eval (LAMBDA = 16, >= 32 points per key, 8N > 6 levels):
- * each key's own top tree of depth 6 (64 rows of 32 B per key, 80 PRG calls per key)
+ * each key's own top tree of depth 5 (32 rows of 32 B per key, 36 PRG calls per key)
  * unless levels = 0; if its buffer cannot be allocated the points walk from the root. */
 int dcf_prg_set_prefix_levels(dcf_prg* prg, int levels);
 /* The prefix depth D a dcf_eval* call of this shape would use (0 = none). */
