@@ -557,7 +557,7 @@ def run_c5(args, world, rank):
     peak = PEAK_TT_BLOCKS
     achieved = (gen_blocks + eval_blocks) / step_s
     eval_s = phase[1] + phase[2]
-    traffic, traffic_src = traffic_fields("k_gen16+2*k_cw_keymajor+2*k_eval16_stream", K * P, nb, lam, 0, alg_bytes)
+    traffic, traffic_src = traffic_fields("k_gen16+2*k_mk_prefix16+2*k_cw_keymajor+2*k_eval16_stream", K * P, nb, lam, 0, alg_bytes)
     out = {"metric": "C5 batched gen + eval (both parties)", "value": evals / wall, "unit": "evals/s",
            "keys_per_s": global_keys * args.steps / wall, "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
@@ -570,7 +570,7 @@ def run_c5(args, world, rank):
                          "note": "HIP events on the launch stream; each eval includes its key-major CW digest "
                                  "(k_cw_keymajor) — profiles/ has the per-kernel split"},
            "key_traffic_GBps": key_bytes / step_s / 1e9,
-           "roofline": {"bound": "lds", "kernel": "k_gen16 + k_cw_keymajor + k_eval16_stream<MULTI> (whole step)",
+           "roofline": {"bound": "lds", "kernel": "k_gen16 + k_mk_prefix16 + k_cw_keymajor + k_eval16_stream<MULTI> (whole step)",
                         "engine": "stream (multi-key)", "achieved": achieved / 1e9, "peak": peak / 1e9,
                         "unit": "G AES-256 blocks/s", "frac": achieved / peak,
                         "eval_only": {"achieved": eval_blocks / eval_s / 1e9, "frac": eval_blocks / eval_s / peak,
