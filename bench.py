@@ -174,8 +174,9 @@ def dist_setup(n_gpus: int, backend: str = "nccl"):
     return world, rank, local
 
 
-def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int):
-    """Rank 0 runs gen on its GPU; the CWB and both seeds go to every rank by RCCL broadcast."""
+def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int, timing: dict = None):
+    """Rank 0 runs gen on its GPU; the CWB and both seeds go to every rank by RCCL broadcast
+    (its time, between two barriers and outside any timed region, goes into timing['key_broadcast_ms'])."""
     dev = torch.device("cuda", torch.cuda.current_device())
     rng = np.random.default_rng(seed)
     alpha, beta, s0, s1 = rng.bytes(n_bytes), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
@@ -185,7 +186,15 @@ def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int):
         k = d.gen(dcf_amd.CmpFn(alpha, beta), [s0, s1], dcf_amd.BoundState.LtBeta)
         cwb.copy_(torch.from_numpy(np.frombuffer(dcf_amd.share_to_cwb(k, n_bytes, lam), np.uint8).copy()))
         seeds.copy_(torch.from_numpy(np.frombuffer(s0 + s1, np.uint8).reshape(2, lam).copy()))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
     broadcast_key([cwb, seeds], src=0)
+    torch.cuda.synchronize()
+    if timing is not None:
+        timing["key_broadcast_ms"] = (time.perf_counter() - t0) * 1e3
+        timing["key_bytes"] = cwb.numel() + seeds.numel()
     return cwb, seeds, alpha, beta
 
 
@@ -252,9 +261,10 @@ def cpu_baseline(keys, n_bytes, lam, cwb_h: bytes, seeds, xs_sample: np.ndarray,
     }
 
 
-def timed_loop(step, steps: int, warmup: int, world: int, stream=None):
+def timed_loop(step, steps: int, warmup: int, world: int, stream=None, local: dict = None):
     """Run `warmup` untimed steps, then time `steps` steps bracketed by barrier + sync.
-    Returns (wall seconds, max over ranks; seconds per step on `stream` by HIP events)."""
+    Returns (wall seconds, max over ranks; seconds per step on `stream` by HIP events).
+    local (optional) receives this rank's own wall seconds and event seconds per step."""
     stream = stream or torch.cuda.current_stream()
     for _ in range(warmup):
         step()
@@ -273,10 +283,36 @@ def timed_loop(step, steps: int, warmup: int, world: int, stream=None):
         dist.barrier()
     torch.cuda.synchronize()
     w = time.perf_counter() - t0
+    k = ev0.elapsed_time(ev1) / 1e3 / steps
+    if local is not None:
+        local.update(wall_s=w, event_s_per_step=k)
     t = torch.tensor([w], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item()), ev0.elapsed_time(ev1) / 1e3 / steps
+    return float(t.item()), k
+
+
+def gather_per_rank(world: int, rec: dict):
+    """Every rank's measurement record on rank 0 (all_gather_object: small host objects, outside
+    the timed region); [rec] at N = 1."""
+    if world == 1:
+        return [rec]
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return out
+
+
+def per_rank_summary(recs, steps: int):
+    """The N > 1 line's per-rank block: kernel / wall time per rank and the imbalance that a
+    scaling curve would hide (max over min of the ranks' step times)."""
+    walls = [r["wall_s"] / steps * 1e3 for r in recs]
+    kern = [r["kernel_ms"] for r in recs]
+    return {"ranks": recs, "wall_ms_per_step_min": min(walls), "wall_ms_per_step_max": max(walls),
+            "kernel_ms_min": min(kern), "kernel_ms_max": max(kern),
+            "imbalance": max(walls) / min(walls) if min(walls) > 0 else None,
+            "note": "per rank: its own wall and HIP-event time per step (the line's value uses the max over "
+                    "ranks), one extra untimed eval with phase events (table_ms = shared-prefix table / digest "
+                    "build, walk_ms = walk kernels) and the prefix depth its slice used"}
 
 
 def host_path(d, k_share_fn, xs_dev, lam, parties: int, steps: int):
@@ -323,7 +359,8 @@ def run_eval(args, world, rank):
     prg.set_prefix_levels(args.prefix)
     pfx = prg.eval_prefix_levels(nb, 1, m)  # shared-prefix depth this eval uses (0 = none)
     d = dcf_amd.DcfImpl(nb, lam, prg)
-    cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002)
+    ktime = {}
+    cwb, seeds, alpha, beta = make_key(d, nb, lam, world, 0xDCF0002, ktime)
     s0 = seeds[0].contiguous()
     s1 = seeds[1].contiguous()
     xs = gen_points(m, nb, start, 0xDCF0003)
@@ -337,9 +374,20 @@ def run_eval(args, world, rank):
         if parties == 2:
             d.eval_device(True, cwb, s1, xs, ys1)
 
-    wall, kern_s = timed_loop(step, args.steps, args.warmup, world)
+    mine = {}
+    wall, kern_s = timed_loop(step, args.steps, args.warmup, world, local=mine)
     kern_s /= parties
     dev_blocks = prg.last_eval_blocks()  # stream engine: AES blocks of the last launch, counted on the device
+    # one more (untimed) eval with phase events: this rank's table build vs walk split
+    prg.set_phase_timing(True)
+    d.eval_device(False, cwb, s0, xs, ys)
+    torch.cuda.synchronize()
+    table_ms, walk_ms, depth = prg.last_eval_phases()
+    prg.set_phase_timing(False)
+    rank_rec = {"rank": rank, "device": torch.cuda.current_device(), "points": m, "start": start,
+                "wall_s": mine["wall_s"], "kernel_ms": kern_s * 1e3, "table_ms": table_ms, "walk_ms": walk_ms,
+                "prefix_levels": depth, "key_broadcast_ms": ktime.get("key_broadcast_ms")}
+    per_rank = gather_per_rank(world, rank_rec)
     no_prefix = None
     if pfx and not args.no_compare:
         # the same batch without the shared-prefix table (each point walks all 8N levels)
@@ -415,7 +463,8 @@ def run_eval(args, world, rank):
                    "n_bytes": nb, "lambda": lam, "points_per_gpu": m, "global_points": global_points,
                    "parallelism": f"points sharded over {world} GPU(s) in contiguous slices, "
                                   "no collective in timed region"},
-        "aes_blocks_per_s": value * bpe,
+        "aes_blocks_per_s_reference_count": value * bpe,
+        "aes_blocks_per_s_executed": value * exec_bpe,
         "roofline": wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine) if (lam > 16 and engine != "mmo-wide") else {
             "bound": "lds" if engine in ("ttable", "ttable-small", "stream", "mmo", "mmo-wide") else ("valu" if engine == "bitsliced" else "lds+valu"),
             "kernel": kernel, "engine": engine,
@@ -431,7 +480,9 @@ def run_eval(args, world, rank):
                     "level + A on left levels, minus B blocks reused after a right step at t = 0, counted on the device; mmo: 2 AES-128 per level; both below a shared-prefix table "
                     "of prefix_levels levels built inside the timed call and counted; other engines: the "
                     "reference count, 2 per level); "
-                    "aes_blocks_per_s above uses the reference count.  Peak per GPU at 2.4 GHz: T-table "
+                    "aes_blocks_per_s_reference_count above uses the reference count (2 per level; the kernels skip "
+                    "unused A blocks, reused B blocks and the shared prefix, so it exceeds the LDS peak), "
+                    "aes_blocks_per_s_executed the blocks actually encrypted.  Peak per GPU at 2.4 GHz: T-table "
                     "engines LDS-bound (32 ds_read_b32 lookups/clk/CU, 224 per block), bitsliced VALU-bound "
                     "(128 lane-ops/clk/CU, ~800 per block); hybrid = LDS-saturating T-table + bitsliced on "
                     "the VALU left over (DESIGN.md section 4)",
@@ -443,6 +494,12 @@ def run_eval(args, world, rank):
             kernel, m, nb, lam, pfx, m * (nb + lam))
     if check is not None:
         out["slice_check"] = check
+    out["phases"] = {"table_ms": table_ms, "walk_ms": walk_ms, "prefix_levels": depth,
+                     "note": "rank 0, one untimed eval with phase events (dcf_prg_set_phase_timing)"}
+    if world > 1:
+        out["per_rank"] = per_rank_summary(per_rank, args.steps)
+        out["key_broadcast"] = {"ms": ktime.get("key_broadcast_ms"), "bytes": ktime.get("key_bytes"),
+                                "backend": args.dist_backend, "note": "once, before timing (outside the timed region)"}
     host_ys = None
     if args.host_path or args.workload == "c1":
         share = dcf_amd.cwb_to_share(cwb.cpu().numpy().tobytes(), nb, lam, [])
@@ -537,7 +594,8 @@ def run_c5(args, world, rank):
     d.eval_multikey_device(False, cwb, s0, xs, P, y0)
     torch.cuda.synchronize()
     b0 = prg.last_eval_blocks()
-    wall, step_s = timed_loop(step, args.steps, args.warmup, world)
+    mine = {}
+    wall, step_s = timed_loop(step, args.steps, args.warmup, world, local=mine)
     b1 = prg.last_eval_blocks()
     # per-phase HIP-event times over the same number of steps (separate loop: events between phases)
     for _ in range(args.steps):
@@ -562,7 +620,8 @@ def run_c5(args, world, rank):
            "keys_per_s": global_keys * args.steps / wall, "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
            "scaling": args.scaling, "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-           "aes_blocks_per_s": evals / wall * blocks_per_eval(nb, lam) + global_keys * args.steps / wall * 4 * n,
+           "aes_blocks_per_s_reference_count": evals / wall * blocks_per_eval(nb, lam) + global_keys * args.steps / wall * 4 * n,
+           "aes_blocks_per_s_executed_per_gpu": (gen_blocks + eval_blocks) / step_s,
            "config": {"workload": f"C5: {global_keys} keys x {P} points ({K} keys on this GPU), N={nb}, "
                                   f"lambda={lam}, batched gen + multi-key eval of both parties per step",
                       "n_bytes": nb, "lambda": lam, "keys_per_gpu": K, "points_per_key": P},
@@ -583,6 +642,11 @@ def run_c5(args, world, rank):
                         "note": "gen: 4 AES-256 blocks per level per key (k_gen16); eval: blocks the multi-key "
                                 "stream engine encrypts, counted on the device (B every level, A on left levels, "
                                 "minus reused B); peak = T-table LDS bound 87.8 G blocks/s"}}
+    if world > 1:
+        recs = gather_per_rank(world, {"rank": rank, "keys": K, "key_start": kstart, "wall_s": mine["wall_s"],
+                                       "kernel_ms": step_s * 1e3, "gen_ms": phase[0] * 1e3,
+                                       "eval_ms": (phase[1] + phase[2]) * 1e3})
+        out["per_rank"] = per_rank_summary(recs, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu:  # cpu_baseline: rank 0 at N=1 only
         out["cpu_baseline"] = c5_cpu_baseline(keys, nb, lam, alpha, beta, s0, s1, xs, cwb, y0, y1, K, P,
                                               args.cpu_seconds)

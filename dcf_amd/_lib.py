@@ -33,7 +33,8 @@ EXPORTS = [
     "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device", "dcf_eval_full_domain_device",
     "dcf_share_bincode_bytes", "dcf_share_to_bincode", "dcf_share_from_bincode",
     "dcf_point_slice", "dcf_eval_multi_gpu", "dcf_eval_multi_gpu_device", "dcf_prg_set_prefix_max_bytes",
-    "dcf_prg_device_bytes",
+    "dcf_prg_device_bytes", "dcf_prg_host_pinned_bytes", "dcf_prg_workspaces", "dcf_prg_set_phase_timing",
+    "dcf_prg_last_eval_phases",
 ]
 
 
@@ -92,6 +93,11 @@ def load(path: str = LIB_PATH):
         "dcf_point_slice": ([sz, sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)], None),
         "dcf_prg_set_prefix_max_bytes": ([vp, sz], i),
         "dcf_prg_device_bytes": ([vp], sz),
+        "dcf_prg_host_pinned_bytes": ([vp], sz),
+        "dcf_prg_workspaces": ([vp], i),
+        "dcf_prg_set_phase_timing": ([vp, i], i),
+        "dcf_prg_last_eval_phases": ([vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                      ctypes.POINTER(i)], i),
         "dcf_eval_multi_gpu": ([ctypes.POINTER(vp), sz, sz, i, u8p, sz, u8p, u8p, sz, u8p, sz], i),
         "dcf_eval_multi_gpu_device": ([ctypes.POINTER(vp), sz, sz, i, u8p, sz, u8p, ctypes.POINTER(vp),
                                        ctypes.POINTER(sz), ctypes.POINTER(vp), ctypes.POINTER(vp), u8p], i),

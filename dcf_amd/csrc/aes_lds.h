@@ -143,6 +143,12 @@ __device__ __forceinline__ uint32_t lk(const uint32_t* lds, uint32_t w, uint32_t
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + addr);
 }
 
+// DPP quad_perm encodings: lane c reads lane sel[c]; ctrl = sel0 | sel1<<2 | sel2<<4 | sel3<<6
+constexpr int kQpRot1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // c <- c+1
+constexpr int kQpRot2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // c <- c+2
+constexpr int kQpRot3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // c <- c+3
+constexpr int kQpBcast0 = 0;                                   // c <- 0
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
@@ -694,6 +700,28 @@ __device__ __forceinline__ void aes256_tt2(uint32_t (&st)[NB][4], const RoundKey
 #pragma unroll
     for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
 }
+
+// In-kernel clock probe (diagnostic builds only, -DDCF_CLOCK_STAMPS; MI355X_MICROARCH.md "DVFS
+// give-back" item 6): lane 0 of workgroup w stamps the shader-clock counter (s_memtime) and the
+// 100 MHz real-time counter (s_memrealtime) when its work starts and ends; the engine clock is
+// the ratio of the deltas x 100 MHz.  The stamps go to a buffer of their own by plain vector
+// stores (dcf_debug_clock_stamps reads them back); no output is computed from them.
+#ifdef DCF_CLOCK_STAMPS
+constexpr uint32_t kClkSlots = 4, kClkGroups = 4096;
+__device__ unsigned long long g_clk_stamps[kClkSlots * kClkGroups * 4];
+__device__ __forceinline__ void clk_stamp(uint32_t slot, uint32_t phase) {
+  const uint32_t wg = blockIdx.x + gridDim.x * blockIdx.y;
+  if (threadIdx.x == 0 && wg < kClkGroups) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime(), r = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o = g_clk_stamps + ((size_t)slot * kClkGroups + wg) * 4 + 2 * phase;
+    __hip_atomic_store(o, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(o + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+#define DCF_CLK(slot, phase) clk_stamp(slot, phase)
+#else
+#define DCF_CLK(slot, phase)
+#endif
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }
 

@@ -34,6 +34,7 @@
 
 #include "aes_lds.h"
 #include "kernels16.h"
+#include "kernels_lat.h"
 #include "kernels_wide.h"
 #include "kernels_bs.h"
 #include "kernels_stream.h"
@@ -97,6 +98,51 @@ struct DevBuf {
 
 constexpr size_t kCtrBytes = 16;  // d_ctr: work counter (u32), then the stream engine's block count (u64)
 
+// Per-call mutable state of a dcf_prg (the reference's `Dcf::eval(&self, ...)` is reentrant and
+// its PRG is `Sync`, lib.rs:34,52: one DcfImpl may be shared by many threads).  Every compute
+// entry point leases one workspace from the prg's pool for its duration, so concurrent calls
+// on one prg — from several host threads, or device calls queued on different streams — never
+// share a buffer.  The pool is LIFO, so a single caller keeps reusing one workspace whose
+// buffers have already grown.  Device calls return before their kernels finish: the lease
+// records `done` on the caller's stream, and the next lease of this workspace on another
+// stream waits for that event on the device (hipStreamWaitEvent) before touching a buffer.
+struct Workspace {
+  uint32_t* d_ctr = nullptr;  // work counter / device-counted AES blocks (dcf_prg_last_eval_blocks)
+  uint8_t* d_ws = nullptr;    // stream-ordered scratch (LAMBDA >= 32 paths, full domain)
+  size_t ws_bytes = 0;
+  uint8_t* d_dig = nullptr;   // LAMBDA >= 32 stream head: compact CW digest of the current key
+  uint32_t dig_levels = 0;
+  uint8_t* d_kdig = nullptr;  // LAMBDA = 16 multi-key stream eval: key-major CW digest
+  size_t kdig_bytes = 0;
+  void* d_slabs = nullptr;    // per-wave s/v slabs of the hybrid kernels (MEM variant)
+  size_t slab_bytes = 0;
+  uint8_t* d_pfx = nullptr;   // shared-prefix table + its build buffers / per-key top trees
+  size_t pfx_bytes = 0;
+  uint8_t* d_rows = nullptr;  // single-key stream eval: 48-byte CW rows (k_cw_rows48)
+  size_t rows_bytes = 0;
+  uint8_t* d_mkey = nullptr;  // dcf_eval_multi_gpu_device: this device's copy of the key (CWB + s0)
+  size_t mkey_bytes = 0;
+  // Host-pointer entry points: three non-blocking streams (copy-in, compute, copy-out), their
+  // events and staging (pinned host + device), grown on demand and kept.
+  hipStream_t hs[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t hev[6] = {};     // in[2], kernel[2], out[2] (double-buffered chunks)
+  uint8_t* h_stage = nullptr; // pinned
+  size_t h_stage_bytes = 0;
+  uint8_t* d_stage = nullptr;
+  size_t d_stage_bytes = 0;
+  uint8_t* h_tiny = nullptr;  // small host calls: pinned, device-mapped, coherent (read/written by the kernel)
+  size_t tiny_bytes = 0;
+  // Ordering of the device work of successive leases (see above).
+  hipEvent_t done = nullptr;
+  hipStream_t done_stream = nullptr;
+  bool pending = false;
+  uint32_t host_streams = 0;  // hs[] the current host call queued work on (bit i = hs[i])
+  // dcf_prg_set_phase_timing: events around the last eval's preparation and walk kernels.
+  hipEvent_t tev[3] = {};
+  bool timed = false;
+  uint32_t last_prefix = 0;
+};
+
 struct dcf_prg {
   int kind = 0;               // 0: Aes256HirosePrg (prg.rs), 1: Aes128MatyasMeyerOseasPrg (kernels_mmo.h)
   int device = 0;
@@ -104,63 +150,124 @@ struct dcf_prg {
   size_t lambda = 0;
   size_t cipher_n = 0;
   std::vector<RoundKeys> rk;  // Aes256::new per key (prg.rs:28-31)
-  uint4* d_rk128 = nullptr;   // MMO: AES-128 schedules of ciphers 0..3 (4 x 11 round keys)
+  uint4* d_rk128 = nullptr;   // MMO: AES-128 schedules (4 * LAMBDA/16 x 11 round keys)
+  size_t rk128_count = 0;     // ... how many
   uint4* d_rk2 = nullptr;     // LAMBDA >= 32 stream head: AES-256 schedules of ciphers 0 and 17
   uint4* d_rk0 = nullptr;     // LAMBDA = 16 stream eval: AES-256 schedule of cipher 0 (15 x 16 B)
-  uint8_t* d_dig = nullptr;   // LAMBDA >= 32 stream head: compact CW digest of the current key
-  uint8_t* d_kdig = nullptr;  // LAMBDA = 16 multi-key stream eval: key-major CW digest
-  size_t kdig_bytes = 0;
-  uint32_t dig_levels = 0;
   uint32_t* d_tab = nullptr;  // T0..T3 (4 KiB) on the device
   uint4* d_km = nullptr;      // bitsliced round-key masks of cipher 0 (15 x 4 x 8 uint4)
-  uint8_t* d_ws = nullptr;    // stream-ordered scratch (LAMBDA >= 32 paths)
-  size_t ws_bytes = 0;
-  uint32_t* d_ctr = nullptr;  // work counter of the hybrid eval kernel
-  void* d_slabs = nullptr;    // per-wave s/v slabs of the hybrid kernel (MEM variant)
-  size_t slab_bytes = 0;
-  int eval_mode = DCF_EVAL_AUTO;
-  int prefix_levels = -1;     // shared-prefix table depth for single-key stream eval: -1 auto, 0 off
-  uint8_t* d_pfx = nullptr;   // its two node buffers (s, v, t per node) + work counters
-  size_t pfx_bytes = 0;
-  int hybrid_tt_waves = 13;   // T-table waves per hybrid workgroup (r01 sweep: 13 of 16 best)
-  int hybrid_mem = 1;         // 1: 16-wave workgroups with s/v slabs; 0: 12 waves, s/v in registers
-  uint32_t shy_mask = 0x7777; // stream-hybrid: stream waves (bit w = wave w); 0x7777 = one SIMD bitsliced
-  int shy_prio = 0;           // stream-hybrid: raise the stream waves' issue priority
   std::vector<uint8_t> key_blob;  // the PRG keys as given (multi-GPU calls check every prg holds the same)
-  // Host-pointer entry points (dcf_gen / dcf_eval / dcf_prg_gen / dcf_eval_multi_gpu): three
-  // prg-owned non-blocking streams (copy-in, compute, copy-out), their events, and staging
-  // pooled across calls (pinned host + device), so a call never synchronizes the device.
-  hipStream_t hs[3] = {nullptr, nullptr, nullptr};
-  hipEvent_t hev[6] = {};     // in[2], kernel[2], out[2] (double-buffered chunks)
-  uint8_t* h_stage = nullptr; // pinned
-  size_t h_stage_bytes = 0;
-  uint8_t* d_stage = nullptr;
-  size_t d_stage_bytes = 0;
-  uint8_t* d_mkey = nullptr;  // dcf_eval_multi_gpu_device: this device's copy of the key (CWB + s0)
-  size_t mkey_bytes = 0;
-  size_t prefix_cap = 0;      // dcf_prg_set_prefix_max_bytes: cap on the auto table's buffers (0 = none)
-  uint8_t* d_rows = nullptr;  // single-key stream eval: 48-byte CW rows (k_cw_rows48)
-  size_t rows_bytes = 0;
+  // Settings (read once per call; atomics so a setter racing a call is not a data race).
+  std::atomic<int> eval_mode{DCF_EVAL_AUTO};
+  std::atomic<int> prefix_levels{-1};     // shared-prefix table depth: -1 auto, 0 off
+  std::atomic<int> hybrid_tt_waves{13};   // T-table waves per hybrid workgroup (r01 sweep: 13 of 16 best)
+  std::atomic<int> hybrid_mem{1};         // 1: 16-wave workgroups with s/v slabs; 0: 12 waves, s/v in registers
+  std::atomic<uint32_t> shy_mask{0x7777}; // stream-hybrid: stream waves (bit w = wave w)
+  std::atomic<int> shy_prio{0};           // stream-hybrid: raise the stream waves' issue priority
+  std::atomic<size_t> prefix_cap{0};      // dcf_prg_set_prefix_max_bytes (0 = none)
+  std::atomic<int> timing{0};             // dcf_prg_set_phase_timing
+  // Workspace pool (see Workspace).
+  std::mutex pool_mu;
+  std::vector<Workspace*> all_ws, free_ws;
+  std::atomic<Workspace*> last_ws{nullptr};  // the workspace of the last eval call to return
 };
 
 namespace {
+
+// A workspace leased for one call.  `st` is the stream the call's device work is queued on
+// (for host entry points: the workspace's own compute stream, set by host_lease()).
+struct Lease {
+  dcf_prg* p;
+  Workspace* w = nullptr;
+  hipStream_t st = nullptr;
+  bool ordered = false;
+  bool drained = false;  // a host call synchronized its streams: nothing left to order after
+  Lease(dcf_prg* prg) : p(prg) {
+    {
+      std::lock_guard<std::mutex> g(p->pool_mu);
+      if (!p->free_ws.empty()) {
+        w = p->free_ws.back();
+        p->free_ws.pop_back();
+      }
+    }
+    if (!w) {
+      w = new Workspace();
+      std::lock_guard<std::mutex> g(p->pool_mu);
+      p->all_ws.push_back(w);
+    }
+  }
+  // Queue the call's device work on `stream`, after this workspace's previous device work.
+  int order(hipStream_t stream) {
+    st = stream;
+    ordered = true;
+    if (w->pending && w->done_stream != st) {
+      const hipError_t e = hipStreamWaitEvent(st, w->done, 0);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(DCF_ERR_HIP, std::string("hipStreamWaitEvent: ") + hipGetErrorString(e));
+      }
+    }
+    return DCF_OK;
+  }
+  ~Lease() {
+    if (drained) {
+      w->pending = false;
+    } else if (ordered) {
+      if (!w->done) (void)hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
+      if (w->done && hipEventRecord(w->done, st) == hipSuccess) {
+        w->done_stream = st;
+        w->pending = true;
+      } else {
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(st);  // cannot order the next user: drain instead
+        w->pending = false;
+      }
+    }
+    std::lock_guard<std::mutex> g(p->pool_mu);
+    p->free_ws.push_back(w);
+  }
+  Lease(const Lease&) = delete;
+  Lease& operator=(const Lease&) = delete;
+};
 
 constexpr int kPrefixNoMem = -100;            // build_prefix: table allocation failed (internal)
 constexpr uint64_t kWideChunk = 1ull << 22;   // points per head/tail pass (t-vector scratch 256 MiB)
 constexpr uint64_t kGenChunk = 4096;          // keys per wide-gen launch (scratch 3*LAMBDA per key)
 constexpr uint32_t kTailPts = 4096;          // points per tail workgroup (one table build each)
 
-int ensure_ws(dcf_prg* p, size_t bytes, hipStream_t st) {
-  if (p->ws_bytes >= bytes) return DCF_OK;
-  if (p->d_ws) {
+// Grow a workspace buffer to `need` bytes (contents not kept).  The old buffer may still be
+// read by this workspace's earlier work on `st`, so that drains first.
+int grow(uint8_t** buf, size_t* have, size_t need, hipStream_t st) {
+  if (*have >= need) return DCF_OK;
+  if (*buf) {
     HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(hipFree(p->d_ws));
-    p->d_ws = nullptr;
-    p->ws_bytes = 0;
+    HIP_TRY(hipFree(*buf));
+    *buf = nullptr;
+    *have = 0;
   }
-  HIP_TRY(hipMalloc(&p->d_ws, bytes));
-  p->ws_bytes = bytes;
+  HIP_TRY(hipMalloc(buf, need));
+  *have = need;
   return DCF_OK;
+}
+
+int ensure_ws(Workspace* w, size_t bytes, hipStream_t st) { return grow(&w->d_ws, &w->ws_bytes, bytes, st); }
+
+int ensure_ctr(Workspace* w) {
+  if (!w->d_ctr) HIP_TRY(hipMalloc(&w->d_ctr, kCtrBytes));
+  return DCF_OK;
+}
+
+// Phase timing (dcf_prg_set_phase_timing): event i of the lease's workspace on its stream.
+void phase_mark(dcf_prg* p, Lease& L, int i) {
+  if (!p->timing.load(std::memory_order_relaxed)) return;
+  Workspace* w = L.w;
+  if (!w->tev[i] && hipEventCreate(&w->tev[i]) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  if (hipEventRecord(w->tev[i], L.st) != hipSuccess) (void)hipGetLastError();
+  if (i == 0) w->timed = false;
+  if (i == 2) w->timed = true;
 }
 
 // Workgroups of the single-launch table builds (k_prefix_build16, k_wpfx_build): 2^S
@@ -276,54 +383,39 @@ uint32_t wide_prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t m) {
 }
 
 // Expand the top `levels` levels of one key's tree for the wide stream head (the CW
-// digest p->d_dig must hold this key) into WidePrefix rows in p->d_pfx, in one launch
+// digest w->d_dig must hold this key) into WidePrefix rows in w->d_pfx, in one launch
 // (k_wpfx_build): [table 2^D x 80 B | 2 x 2^S regions of 2^(D-1-S) nodes].
-int build_wide_prefix(dcf_prg* p, uint32_t nlev, int party, const uint8_t* s0, uint32_t levels, WidePrefix* out,
-                      hipStream_t st) {
+int build_wide_prefix(dcf_prg* p, Workspace* w, uint32_t nlev, int party, const uint8_t* s0, uint32_t levels,
+                      WidePrefix* out, hipStream_t st) {
   const uint32_t S = prefix_split(levels);
   const uint32_t R = 1u << (levels - 1u - S);
   const size_t tab_bytes = (((size_t)80 << levels) + 255) & ~(size_t)255;
   const size_t region = (size_t)80 * R;
   const size_t need = tab_bytes + 2 * ((size_t)1 << S) * region;
-  if (p->pfx_bytes < need) {
-    if (p->d_pfx) {
-      HIP_TRY(hipStreamSynchronize(st));
-      HIP_TRY(hipFree(p->d_pfx));
-      p->d_pfx = nullptr;
-      p->pfx_bytes = 0;
-    }
-    HIP_TRY(hipMalloc(&p->d_pfx, need));
-    p->pfx_bytes = need;
-  }
-  uint4* table = (uint4*)p->d_pfx;
-  uint4* ba = (uint4*)(p->d_pfx + tab_bytes);
-  uint4* bb = (uint4*)(p->d_pfx + tab_bytes + ((size_t)1 << S) * region);
+  if (int rc = grow(&w->d_pfx, &w->pfx_bytes, need, st)) return rc;
+  uint4* table = (uint4*)w->d_pfx;
+  uint4* ba = (uint4*)(w->d_pfx + tab_bytes);
+  uint4* bb = (uint4*)(w->d_pfx + tab_bytes + ((size_t)1 << S) * region);
   if (p->lambda == 32)
     hipLaunchKernelGGL(k_wpfx_build<true>, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->d_rk2,
-                       (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, s0, (uint32_t)party, S, levels, ba, bb, R,
+                       (const uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64, s0, (uint32_t)party, S, levels, ba, bb, R,
                        table);
   else
     hipLaunchKernelGGL(k_wpfx_build<false>, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->d_rk2,
-                       (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, s0, (uint32_t)party, S, levels, ba, bb, R,
+                       (const uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64, s0, (uint32_t)party, S, levels, ba, bb, R,
                        table);
   HIP_TRY(hipGetLastError());
   *out = WidePrefix{table, levels};
   return DCF_OK;
 }
 
-// Device copy of cipher 0's AES-256 schedule (read per round by aes256_tt_gk).
-int ensure_rk0(dcf_prg* p) {
-  if (p->d_rk0) return DCF_OK;
-  HIP_TRY(hipMalloc(&p->d_rk0, sizeof(RoundKeys)));
-  HIP_TRY(hipMemcpy(p->d_rk0, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice));
-  return DCF_OK;
-}
 
 // Expand the top `levels` levels of the key's tree (s = s0, v = 0, t = party at the
-// root; k_fd_level16 per level, as the full-domain eval does) into p->d_pfx.
+// root; k_fd_level16 per level, as the full-domain eval does) into w->d_pfx.
 
-int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const uint4* cwv, const uint8_t* cwt,
-                 const uint4* np1, const uint8_t* s0, uint32_t levels, PrefixTable* out, hipStream_t st) {
+int build_prefix(dcf_prg* p, Workspace* w, size_t n_bytes, int party, const uint4* cws, const uint4* cwv,
+                 const uint8_t* cwt, const uint4* np1, const uint8_t* s0, uint32_t levels, PrefixTable* out,
+                 hipStream_t st) {
   const uint64_t maxnodes = 1ull << levels;
   const size_t nodeb = 33, half = (maxnodes * nodeb + 255) & ~(size_t)255;
   // Hirose: [table 2^D x 32 B | 2 x 2^S regions of 2^(D-1-S) nodes]; MMO: two level buffers + counters
@@ -332,40 +424,38 @@ int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const 
   const size_t region = ((size_t)R * nodeb + 255) & ~(size_t)255;
   const size_t tab_bytes = (maxnodes * 32 + 255) & ~(size_t)255;
   const size_t need = p->kind == 0 ? tab_bytes + 2 * ((size_t)1 << S) * region : 2 * half + 64 * sizeof(uint32_t);
-  if (p->pfx_bytes < need) {
-    if (p->d_pfx) {
+  if (w->pfx_bytes < need) {
+    if (w->d_pfx) {
       HIP_TRY(hipStreamSynchronize(st));
-      HIP_TRY(hipFree(p->d_pfx));
-      p->d_pfx = nullptr;
-      p->pfx_bytes = 0;
+      HIP_TRY(hipFree(w->d_pfx));
+      w->d_pfx = nullptr;
+      w->pfx_bytes = 0;
     }
-    const hipError_t e = hipMalloc(&p->d_pfx, need);
+    const hipError_t e = hipMalloc(&w->d_pfx, need);
     if (e != hipSuccess) {
       (void)hipGetLastError();
-      p->d_pfx = nullptr;
+      w->d_pfx = nullptr;
       return fail(kPrefixNoMem, std::string("prefix table: hipMalloc: ") + hipGetErrorString(e));
     }
-    p->pfx_bytes = need;
+    w->pfx_bytes = need;
   }
   if (p->kind == 0) {  // one launch: k_prefix_build16
-    uint8_t* ba = p->d_pfx + tab_bytes;
+    uint8_t* ba = w->d_pfx + tab_bytes;
     const uint32_t H = prefix_dfs_levels(levels, S);
-    if (DCF_PFX_GK)
-      if (int rc = ensure_rk0(p)) return rc;
     hipLaunchKernelGGL(k_prefix_build16, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->rk[0], cws, cwv, cwt,
                        (const uint4*)s0, (uint32_t)party, S, levels, H, ba, ba + ((size_t)1 << S) * region,
-                       (uint64_t)region, R, (uint4*)p->d_pfx, DCF_PFX_GK ? p->d_rk0 : nullptr);
+                       (uint64_t)region, R, (uint4*)w->d_pfx, DCF_PFX_GK ? p->d_rk0 : nullptr);
     HIP_TRY(hipGetLastError());
-    *out = PrefixTable{(const uint4*)p->d_pfx, levels};
+    *out = PrefixTable{(const uint4*)w->d_pfx, levels};
     return DCF_OK;
   }
-  uint4* s_a = (uint4*)p->d_pfx;
+  uint4* s_a = (uint4*)w->d_pfx;
   uint4* v_a = s_a + maxnodes;
   uint8_t* t_a = (uint8_t*)(v_a + maxnodes);
-  uint4* s_b = (uint4*)(p->d_pfx + half);
+  uint4* s_b = (uint4*)(w->d_pfx + half);
   uint4* v_b = s_b + maxnodes;
   uint8_t* t_b = (uint8_t*)(v_b + maxnodes);
-  uint32_t* ctrs = (uint32_t*)(p->d_pfx + 2 * half);
+  uint32_t* ctrs = (uint32_t*)(w->d_pfx + 2 * half);
   HIP_TRY(hipMemsetAsync(ctrs, 0, 64 * sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_fd_root16, dim3(1), dim3(64), 0, st, (const uint4*)s0, (uint32_t)party, s_a, v_a, t_a);
   HIP_TRY(hipGetLastError());
@@ -395,11 +485,11 @@ int build_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const 
 
 // build_prefix at depth d; in auto mode (prefix_levels < 0) an allocation failure retries
 // two levels shallower, down to 8, and then evaluates without a table (same output bytes).
-int try_prefix(dcf_prg* p, size_t n_bytes, int party, const uint4* cws, const uint4* cwv, const uint8_t* cwt,
-               const uint4* np1, const uint8_t* s0, uint32_t d, PrefixTable* out, hipStream_t st) {
+int try_prefix(dcf_prg* p, Workspace* w, size_t n_bytes, int party, const uint4* cws, const uint4* cwv,
+               const uint8_t* cwt, const uint4* np1, const uint8_t* s0, uint32_t d, PrefixTable* out, hipStream_t st) {
   *out = PrefixTable{nullptr, 0u};
   while (d) {
-    const int rc = build_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0, d, out, st);
+    const int rc = build_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0, d, out, st);
     if (rc != kPrefixNoMem) return rc;
     if (p->prefix_levels >= 0) return fail(DCF_ERR_HIP, t_err);  // a forced depth must fit
     d = d >= 10u ? d - 2u : 0u;
@@ -497,8 +587,9 @@ int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const u
 }
 
 // Dcf::eval at LAMBDA >= 32 for key `key` of a K-key CWB (see kernels_wide.h).
-int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb, const uint8_t* s0,
-              const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
+// The caller (eval_launch) has zeroed the workspace's block count once for the whole call.
+int eval_wide(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
+              const uint8_t* s0, const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nlev = (uint32_t)(8 * n_bytes);
   if (n_bytes > 31) return fail(DCF_ERR_UNSUPPORTED, "LAMBDA >= 32 eval supports N <= 31");
   const size_t n = 8 * n_bytes;
@@ -507,41 +598,31 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
   const uint8_t* cwt = cwb + 2 * n * K * lam;
   const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
   const uint64_t chunk = m < kWideChunk ? m : kWideChunk;
-  int rc = ensure_ws(p, chunk * kTWords * 4, st);
+  int rc = ensure_ws(w, chunk * kTWords * 4, st);
   if (rc) return rc;
-  uint32_t* tvec = reinterpret_cast<uint32_t*>(p->d_ws);
+  uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
   WidePrefix wpf{nullptr, 0u};
-  // the lockstep head counts no blocks: dcf_prg_last_eval_blocks then reads 0, not a stale count
-  if (p->eval_mode == DCF_EVAL_TTABLE && p->d_ctr) HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
+  const int mode = p->eval_mode;
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = (m - off < chunk) ? m - off : chunk;
     const dim3 grid((unsigned)grid_for(cnt, p->cus));
-    if (p->eval_mode != DCF_EVAL_TTABLE) {  // stream head: 2.5 AES blocks per level instead of 4
-      if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
-      // the work counter every pass, the block count (dcf_prg_last_eval_blocks) once per call
-      HIP_TRY(hipMemsetAsync(p->d_ctr, 0, off == 0 ? kCtrBytes : 8, st));
-      if (!p->d_rk2) {  // round keys of ciphers 0 and 17 (2 x 15 x 16 B), read into LDS by the kernel
-        HIP_TRY(hipMalloc(&p->d_rk2, 2 * sizeof(RoundKeys)));
-        HIP_TRY(hipMemcpy(p->d_rk2, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(p->d_rk2 + 15, &p->rk[17], sizeof(RoundKeys), hipMemcpyHostToDevice));
-      }
+    if (mode != DCF_EVAL_TTABLE) {  // stream head: 2.5 AES blocks per level instead of 4
+      HIP_TRY(hipMemsetAsync(w->d_ctr, 0, 8, st));  // the pass's work counter (the block count stays)
       if (off == 0) {  // CW digest of this key (bytes [0,32) of each level's cw_s / cw_v, and cw_t)
-        if (p->dig_levels < nlev) {
-          if (p->d_dig) {
-            HIP_TRY(hipStreamSynchronize(st));
-            HIP_TRY(hipFree(p->d_dig));
-          }
-          HIP_TRY(hipMalloc(&p->d_dig, (size_t)nlev * 65));
-          p->dig_levels = nlev;
+        if (w->dig_levels < nlev) {
+          size_t have = (size_t)w->dig_levels * 65;
+          if (int rc2 = grow(&w->d_dig, &have, (size_t)nlev * 65, st)) return rc2;
+          w->dig_levels = nlev;
         }
         hipLaunchKernelGGL(k_cw_digest, dim3((4 * nlev + 255) / 256), dim3(256), 0, st, cws, cwv, cwt, nlev, lam, K,
-                           key, (uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64);
+                           key, (uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64);
         HIP_TRY(hipGetLastError());
         const uint32_t d = wide_prefix_depth(p, n_bytes, m);
         if (d) {
-          rc = build_wide_prefix(p, nlev, party, s0, d, &wpf, st);
+          rc = build_wide_prefix(p, w, nlev, party, s0, d, &wpf, st);
           if (rc) return rc;
         }
+        w->last_prefix = d;
       }
       const uint64_t units = (cnt + kWideUnit - 1) / kWideUnit;
       uint64_t blocks = (units + 15) / 16;
@@ -554,8 +635,8 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
 #endif
 #define DCF_WHS(MH, XR)                                                                                        \
   hipLaunchKernelGGL((k_eval_wide_head_stream<DCF_WHS_NS, MH, XR, DCF_WHS_WG>), dim3((unsigned)blocks), dim3(DCF_WHS_WG), 0, st, p->d_tab,     \
-                     p->d_rk2, (const uint4*)p->d_dig, p->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
-                     lam, K, key, cnt, p->d_ctr, ys + off * lam, tvec, wpf)
+                     p->d_rk2, (const uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
+                     lam, K, key, cnt, w->d_ctr, ys + off * lam, tvec, wpf)
       const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16;
       if (lam == 32 && xreg) DCF_WHS(true, true);
       else if (lam == 32) DCF_WHS(true, false);
@@ -582,7 +663,7 @@ int eval_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, c
 // Dcf::eval with the MMO PRG at LAMBDA >= 32 for key `key` (kernels_mmo_wide.h): per pass
 // of up to kWideChunk points, the head walks block 0 (y[0:16), t-vector), then the tail
 // walks blocks 1..nb-1 given the t-vectors.
-int eval_mmo_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
+int eval_mmo_wide(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
                   const uint8_t* s0, const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nb = lam / 16u;
   if (n_bytes > 31) return fail(DCF_ERR_UNSUPPORTED, "MMO eval at LAMBDA >= 32 supports N <= 31");
@@ -592,8 +673,8 @@ int eval_mmo_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int part
   const uint8_t* cwt = cwb + 2 * n * K * lam;
   const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
   const uint64_t chunk = m < kWideChunk ? m : kWideChunk;
-  if (int rc = ensure_ws(p, chunk * kMmoTWords * 4, st)) return rc;
-  uint32_t* tvec = reinterpret_cast<uint32_t*>(p->d_ws);
+  if (int rc = ensure_ws(w, chunk * kMmoTWords * 4, st)) return rc;
+  uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = std::min<uint64_t>(chunk, m - off);
     const uint64_t groups = (cnt + 63) / 64;
@@ -615,12 +696,12 @@ int eval_mmo_wide(dcf_prg* p, size_t n_bytes, uint64_t K, uint64_t key, int part
 
 // Batched Dcf::gen with the MMO PRG at LAMBDA >= 32 (kernels_mmo_wide.h): per pass of keys,
 // the head over block 0 of both parties (t-CWs, per-level t bits), then the tail.
-int gen_mmo_wide(dcf_prg* p, size_t n_bytes, uint64_t K, const uint8_t* alpha, const uint8_t* beta,
+int gen_mmo_wide(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, const uint8_t* alpha, const uint8_t* beta,
                  const uint8_t* s0_0, const uint8_t* s0_1, int bound, uint8_t* cws, uint8_t* cwv, uint8_t* cwt,
                  uint8_t* np1, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nb = lam / 16u, nlev = (uint32_t)(8 * n_bytes);
-  if (int rc = ensure_ws(p, (size_t)K * nlev * 4, st)) return rc;
-  uint32_t* tinfo = reinterpret_cast<uint32_t*>(p->d_ws);
+  if (int rc = ensure_ws(w, (size_t)K * nlev * 4, st)) return rc;
+  uint32_t* tinfo = reinterpret_cast<uint32_t*>(w->d_ws);
   const uint64_t groups = (K + 63) / 64;
   const dim3 gh((unsigned)std::min<uint64_t>((groups + 15) / 16, (uint64_t)p->cus));
   hipLaunchKernelGGL(k_mmo_wide_gen<true>, gh, dim3(kBlock), 0, st, p->d_tab, p->d_rk128, alpha, beta, s0_0, s0_1,
@@ -685,10 +766,17 @@ int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int 
   if (e == hipSuccess) e = hipMemcpy(p->d_tab, g_tab, sizeof(g_tab), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&p->d_km, km.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(p->d_km, km.data(), km.size() * 4, hipMemcpyHostToDevice);
+  // device copies of the schedules the kernels read per round: cipher 0 (LAMBDA = 16 stream /
+  // pair / table-build kernels) and, at LAMBDA >= 32, ciphers 0 and 17 (the wide stream head)
+  if (e == hipSuccess) e = hipMalloc(&p->d_rk0, sizeof(RoundKeys));
+  if (e == hipSuccess) e = hipMemcpy(p->d_rk0, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice);
+  if (e == hipSuccess && lambda > 16) {
+    e = hipMalloc(&p->d_rk2, 2 * sizeof(RoundKeys));
+    if (e == hipSuccess) e = hipMemcpy(p->d_rk2, &p->rk[0], sizeof(RoundKeys), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_rk2 + 15, &p->rk[17], sizeof(RoundKeys), hipMemcpyHostToDevice);
+  }
   if (e != hipSuccess) {
-    if (p->d_tab) (void)hipFree(p->d_tab);
-    if (p->d_km) (void)hipFree(p->d_km);
-    delete p;
+    dcf_prg_free(p);
     return fail(DCF_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e));
   }
   *out = p;
@@ -724,6 +812,7 @@ int dcf_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int dev
   if (e == hipSuccess) e = hipMemcpy(p->d_tab, g_tab, sizeof(g_tab), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&p->d_rk128, w.size() * 4);
   if (e == hipSuccess) e = hipMemcpy(p->d_rk128, w.data(), w.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) p->rk128_count = nsched;
   if (e != hipSuccess) {
     dcf_prg_free(p);
     return fail(DCF_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e));
@@ -734,31 +823,32 @@ int dcf_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int dev
 
 int dcf_prg_kind(const dcf_prg* p) { return p ? p->kind : -1; }
 
+static void free_workspace(Workspace* w) {
+  for (hipStream_t s : w->hs)  // host-path work still queued (an error return drains these too)
+    if (s) (void)hipStreamSynchronize(s);
+  if (w->pending) (void)hipEventSynchronize(w->done);  // the last device call's kernels
+  for (void* b : {(void*)w->d_ctr, (void*)w->d_ws, (void*)w->d_dig, (void*)w->d_kdig, w->d_slabs, (void*)w->d_pfx,
+                  (void*)w->d_rows, (void*)w->d_mkey, (void*)w->d_stage})
+    if (b) (void)hipFree(b);
+  if (w->h_stage) (void)hipHostFree(w->h_stage);
+  if (w->h_tiny) (void)hipHostFree(w->h_tiny);
+  for (hipStream_t s : w->hs)
+    if (s) (void)hipStreamDestroy(s);
+  for (hipEvent_t e : w->hev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : w->tev)
+    if (e) (void)hipEventDestroy(e);
+  if (w->done) (void)hipEventDestroy(w->done);
+  delete w;
+}
+
 void dcf_prg_free(dcf_prg* p) {
   if (!p) return;
   {
     DeviceGuard dg(p->device);
-    for (hipStream_t s : p->hs)  // host-path work still queued (an error return drains these too)
-      if (s) (void)hipStreamSynchronize(s);
-    if (p->d_tab) (void)hipFree(p->d_tab);
-    if (p->d_km) (void)hipFree(p->d_km);
-    if (p->d_rk128) (void)hipFree(p->d_rk128);
-    if (p->d_rk2) (void)hipFree(p->d_rk2);
-    if (p->d_rk0) (void)hipFree(p->d_rk0);
-    if (p->d_dig) (void)hipFree(p->d_dig);
-    if (p->d_kdig) (void)hipFree(p->d_kdig);
-    if (p->d_ws) (void)hipFree(p->d_ws);
-    if (p->d_ctr) (void)hipFree(p->d_ctr);
-    if (p->d_pfx) (void)hipFree(p->d_pfx);
-    if (p->d_slabs) (void)hipFree(p->d_slabs);
-    for (hipStream_t s : p->hs)
-      if (s) (void)hipStreamDestroy(s);
-    for (hipEvent_t e : p->hev)
-      if (e) (void)hipEventDestroy(e);
-    if (p->h_stage) (void)hipHostFree(p->h_stage);
-    if (p->d_stage) (void)hipFree(p->d_stage);
-    if (p->d_mkey) (void)hipFree(p->d_mkey);
-    if (p->d_rows) (void)hipFree(p->d_rows);
+    for (Workspace* w : p->all_ws) free_workspace(w);
+    for (void* b : {(void*)p->d_tab, (void*)p->d_km, (void*)p->d_rk128, (void*)p->d_rk2, (void*)p->d_rk0})
+      if (b) (void)hipFree(b);
   }
   delete p;
 }
@@ -815,21 +905,59 @@ size_t dcf_prg_device_bytes(const dcf_prg* p) {
   size_t b = 0;
   if (p->d_tab) b += sizeof(g_tab);
   if (p->d_km) b += 15 * 4 * 8 * 16;
-  if (p->d_rk128) b += 4 * 44 * 4;
+  if (p->d_rk128) b += p->rk128_count * 44 * 4;
   if (p->d_rk2) b += 2 * sizeof(RoundKeys);
   if (p->d_rk0) b += sizeof(RoundKeys);
-  if (p->d_dig) b += (size_t)p->dig_levels * 65;
-  if (p->d_ctr) b += kCtrBytes;
-  return b + p->kdig_bytes + p->ws_bytes + p->pfx_bytes + p->slab_bytes + p->d_stage_bytes + p->mkey_bytes +
-         p->rows_bytes;
+  std::lock_guard<std::mutex> g(const_cast<dcf_prg*>(p)->pool_mu);
+  for (const Workspace* w : p->all_ws) {
+    if (w->d_ctr) b += kCtrBytes;
+    b += (size_t)w->dig_levels * 65 + w->kdig_bytes + w->ws_bytes + w->pfx_bytes + w->slab_bytes +
+         w->d_stage_bytes + w->mkey_bytes + w->rows_bytes;
+  }
+  return b;
+}
+
+size_t dcf_prg_host_pinned_bytes(const dcf_prg* p) {
+  if (!p) return 0;
+  size_t b = 0;
+  std::lock_guard<std::mutex> g(const_cast<dcf_prg*>(p)->pool_mu);
+  for (const Workspace* w : p->all_ws) b += w->h_stage_bytes + w->tiny_bytes;
+  return b;
+}
+
+int dcf_prg_workspaces(const dcf_prg* p) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  std::lock_guard<std::mutex> g(const_cast<dcf_prg*>(p)->pool_mu);
+  return (int)p->all_ws.size();
 }
 
 int dcf_prg_last_eval_blocks(dcf_prg* p, uint64_t* blocks) {
   if (!p || !blocks) return fail(DCF_ERR_ARG, "null argument");
   *blocks = 0;
-  if (!p->d_ctr) return DCF_OK;
+  Workspace* w = p->last_ws.load();
+  if (!w || !w->d_ctr) return DCF_OK;
   DeviceGuard dg(p->device);
-  HIP_TRY(hipMemcpy(blocks, p->d_ctr + 2, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(blocks, w->d_ctr + 2, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return DCF_OK;
+}
+
+int dcf_prg_set_phase_timing(dcf_prg* p, int on) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  if (on != 0 && on != 1) return fail(DCF_ERR_ARG, "on must be 0 or 1");
+  p->timing = on;
+  return DCF_OK;
+}
+
+int dcf_prg_last_eval_phases(dcf_prg* p, float* prep_ms, float* walk_ms, int* prefix_levels) {
+  if (!p || !prep_ms || !walk_ms) return fail(DCF_ERR_ARG, "null argument");
+  *prep_ms = *walk_ms = 0.f;
+  if (prefix_levels) *prefix_levels = 0;
+  Workspace* w = p->last_ws.load();
+  if (!w || !w->timed) return fail(DCF_ERR_ARG, "no timed eval yet (dcf_prg_set_phase_timing)");
+  DeviceGuard dg(p->device);
+  HIP_TRY(hipEventElapsedTime(prep_ms, w->tev[0], w->tev[1]));
+  HIP_TRY(hipEventElapsedTime(walk_ms, w->tev[1], w->tev[2]));
+  if (prefix_levels) *prefix_levels = (int)w->last_prefix;
   return DCF_OK;
 }
 
@@ -843,56 +971,78 @@ int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priorit
   return DCF_OK;
 }
 
-// Per-wave scratch slabs (bitsliced v) for every 16-wave workgroup of the hybrid kernels.
-static int ensure_slabs(dcf_prg* p, hipStream_t st) {
-  const size_t need = (size_t)p->cus * 16 * kSlabUint4 * sizeof(uint4);
-  if (p->slab_bytes >= need) return DCF_OK;
-  if (p->d_slabs) {
-    HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(hipFree(p->d_slabs));
-    p->d_slabs = nullptr;
-    p->slab_bytes = 0;
-  }
-  HIP_TRY(hipMalloc(&p->d_slabs, need));
-  p->slab_bytes = need;
-  return DCF_OK;
+// Tiny batches run the latency kernels of kernels_lat.h (one AES column per lane).  Thresholds:
+// scripts/lat_sweep.sh (DESIGN.md §4 "Latency kernels").
+#ifndef DCF_EVAL_OCT_MAX
+#define DCF_EVAL_OCT_MAX 32768  // points (one key) up to which auto-mode eval runs k_eval16_oct
+#endif                          // (r03a sweep, us per device call: 32768 oct 187 vs pair 273; 100k 623 vs 485)
+#ifndef DCF_GEN_COL_MAX
+#define DCF_GEN_COL_MAX 16384   // keys up to which gen runs k_gen16_col (r03a: 4096 keys 232 vs 562 us quads)
+#endif
+// Items per workgroup of the latency kernels: a small batch spread over the CUs (one wave per
+// CU while it lasts), at most `cap` (a full 1024-thread workgroup).
+static uint32_t per_wg(uint64_t items, int cus, uint32_t cap) {
+  const uint64_t per = (items + (uint64_t)cus - 1) / (uint64_t)cus;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, per));
+}
+static bool oct_eval(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
+  return p->kind == 0 && p->lambda == 16 && num_keys == 1 && total <= (uint64_t)DCF_EVAL_OCT_MAX &&
+         8 * n_bytes <= kColMaxLevels && p->prefix_levels <= 0 && p->eval_mode == DCF_EVAL_AUTO;
+}
+static bool col_gen(const dcf_prg* p, size_t n_bytes, uint64_t num_keys) {
+  return p->kind == 0 && p->lambda == 16 && num_keys <= (uint64_t)DCF_GEN_COL_MAX && 8 * n_bytes <= kColMaxLevels;
 }
 
-int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint8_t* alpha, const uint8_t* beta,
-                         const uint8_t* s0_0, const uint8_t* s0_1, int bound, uint8_t* cwb_out, void* stream) {
-  if (!p) return fail(DCF_ERR_ARG, "null prg");
-  if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
-  if (bound != DCF_BOUND_LT_BETA && bound != DCF_BOUND_GT_BETA) return fail(DCF_ERR_ARG, "bad bound");
-  if (num_keys == 0) return DCF_OK;
-  if (!alpha || !beta || !s0_0 || !s0_1 || !cwb_out) return fail(DCF_ERR_ARG, "null buffer");
-  DeviceGuard dg(p->device);
+// Per-wave scratch slabs (bitsliced v) for every 16-wave workgroup of the hybrid kernels.
+static int ensure_slabs(dcf_prg* p, Workspace* w, hipStream_t st) {
+  const size_t need = (size_t)p->cus * 16 * kSlabUint4 * sizeof(uint4);
+  size_t have = w->slab_bytes;
+  uint8_t* b = (uint8_t*)w->d_slabs;
+  const int rc = grow(&b, &have, need, st);
+  w->d_slabs = b;
+  w->slab_bytes = have;
+  return rc;
+}
+
+static int gen_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, const uint8_t* alpha,
+                      const uint8_t* beta, const uint8_t* s0_0, const uint8_t* s0_1, int bound, uint8_t* cwb_out) {
+  Workspace* w = L.w;
+  hipStream_t st = L.st;
   const size_t n = 8 * n_bytes, lam = p->lambda;
   uint8_t* cws = cwb_out;
   uint8_t* cwv = cwb_out + n * num_keys * lam;
   uint8_t* cwt = cwb_out + 2 * n * num_keys * lam;
   uint8_t* np1 = cwb_out + dcf_cwb_np1_offset(n_bytes, lam, num_keys);
-  if (p->kind == 1 && lam > 16) return gen_mmo_wide(p, n_bytes, num_keys, alpha, beta, s0_0, s0_1, bound, cws, cwv,
-                                                    cwt, np1, (hipStream_t)stream);
+  if (p->kind == 1 && lam > 16) return gen_mmo_wide(p, w, n_bytes, num_keys, alpha, beta, s0_0, s0_1, bound, cws, cwv,
+                                                    cwt, np1, st);
   if (p->kind == 1) {  // Aes128MatyasMeyerOseasPrg (LAMBDA = 16)
-    hipLaunchKernelGGL(k_gen16_mmo, dim3((unsigned)grid_for(num_keys, p->cus)), dim3(kBlock), 0, (hipStream_t)stream,
-                       p->d_tab, p->d_rk128, alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1,
-                       (uint32_t)bound, (uint32_t)n_bytes, (uint64_t)num_keys, (uint4*)cws, (uint4*)cwv, cwt,
-                       (uint4*)np1);
+    hipLaunchKernelGGL(k_gen16_mmo, dim3((unsigned)grid_for(num_keys, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                       p->d_rk128, alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1, (uint32_t)bound,
+                       (uint32_t)n_bytes, (uint64_t)num_keys, (uint4*)cws, (uint4*)cwv, cwt, (uint4*)np1);
     HIP_TRY(hipGetLastError());
     return DCF_OK;
   }
   if (lam > 16) {  // one workgroup per key, keys in chunks (scratch 3*LAMBDA per key)
-    hipStream_t st = (hipStream_t)stream;
     const uint64_t chunk = num_keys < kGenChunk ? num_keys : kGenChunk;
-    int rc = ensure_ws(p, chunk * 3 * lam, st);
+    int rc = ensure_ws(w, chunk * 3 * lam, st);
     if (rc) return rc;
     for (uint64_t k0 = 0; k0 < num_keys; k0 += chunk) {
       const uint64_t cnt = (num_keys - k0 < chunk) ? num_keys - k0 : chunk;
       hipLaunchKernelGGL(k_gen_wide, dim3((unsigned)cnt), dim3(kBlock), 0, st, p->d_tab, p->rk[0], p->rk[17], alpha,
                          beta, s0_0, s0_1, (uint32_t)bound, (uint32_t)n_bytes, (uint64_t)num_keys, k0, (uint32_t)lam,
-                         cws, cwv, cwt, np1, p->d_ws);
+                         cws, cwv, cwt, np1, w->d_ws);
       HIP_TRY(hipGetLastError());
     }
+    return DCF_OK;
+  }
+  if (col_gen(p, n_bytes, num_keys)) {
+    // Small batches (a single key through the C ABI: benches/dcf.rs bench_gen) are latency-
+    // bound: 16 lanes per key, one AES column each (k_gen16_col).
+    const uint32_t kpw = per_wg(num_keys, p->cus, kBlock / 16);
+    hipLaunchKernelGGL(k_gen16_col, dim3((unsigned)((num_keys + kpw - 1) / kpw)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], alpha, beta, s0_0, s0_1, (uint32_t)bound, (uint32_t)n_bytes, kpw,
+                       (uint64_t)num_keys, cws, cwv, cwt, np1);
+    HIP_TRY(hipGetLastError());
     return DCF_OK;
   }
   // Large batches: 64-lane units from the work counter (waves drift apart, as in k_eval16).
@@ -906,15 +1056,14 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
   const uint64_t items = (uint64_t)num_keys * (quad ? 4u : 1u);
   uint32_t* ctr = nullptr;
   if (items >= (uint64_t)p->cus * kBlock * 2 && (items + 63) / 64 <= 0xFFFFFFFFull) {
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, (hipStream_t)stream));
-    ctr = p->d_ctr;
+    if (int rc = ensure_ctr(w)) return rc;
+    HIP_TRY(hipMemsetAsync(w->d_ctr, 0, kCtrBytes, st));
+    ctr = w->d_ctr;
   }
-#define DCF_GEN16(L)                                                                                             \
-  hipLaunchKernelGGL(k_gen16<L>, dim3((unsigned)grid_for(items, p->cus)), dim3(kBlock), 0, (hipStream_t)stream,   \
-                     p->d_tab, p->rk[0], alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1,       \
-                     (uint32_t)bound, (uint32_t)n_bytes, (uint64_t)num_keys, (uint4*)cws, (uint4*)cwv, cwt,      \
-                     (uint4*)np1, ctr)
+#define DCF_GEN16(LN)                                                                                           \
+  hipLaunchKernelGGL(k_gen16<LN>, dim3((unsigned)grid_for(items, p->cus)), dim3(kBlock), 0, st, p->d_tab, p->rk[0], \
+                     alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1, (uint32_t)bound,          \
+                     (uint32_t)n_bytes, (uint64_t)num_keys, (uint4*)cws, (uint4*)cwv, cwt, (uint4*)np1, ctr)
   if (quad) DCF_GEN16(4);
   else DCF_GEN16(1);
 #undef DCF_GEN16
@@ -922,22 +1071,53 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
   return DCF_OK;
 }
 
-static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, int party, const uint8_t* cwb,
-                       const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, void* stream) {
+int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint8_t* alpha, const uint8_t* beta,
+                         const uint8_t* s0_0, const uint8_t* s0_1, int bound, uint8_t* cwb_out, void* stream) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");
   if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
-  if (party != 0 && party != 1) return fail(DCF_ERR_ARG, "party must be 0 or 1");
-  const uint64_t total = (uint64_t)num_keys * ppk;
-  if (total == 0) return DCF_OK;
-  if (!cwb || !s0s || !xs || !ys) return fail(DCF_ERR_ARG, "null buffer");
+  if (bound != DCF_BOUND_LT_BETA && bound != DCF_BOUND_GT_BETA) return fail(DCF_ERR_ARG, "bad bound");
+  if (num_keys == 0) return DCF_OK;
+  if (!alpha || !beta || !s0_0 || !s0_1 || !cwb_out) return fail(DCF_ERR_ARG, "null buffer");
   DeviceGuard dg(p->device);
+  Lease L(p);
+  if (int rc = L.order((hipStream_t)stream)) return rc;
+  return gen_launch(p, L, n_bytes, num_keys, alpha, beta, s0_0, s0_1, bound, cwb_out);
+}
+
+// Dcf::eval of K keys x ppk points on the lease's stream (arguments checked by the caller).
+// Phase marks (dcf_prg_set_phase_timing): 0 at entry, 1 before the walk kernel (after any
+// table / digest preparation), 2 at the end.
+static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party, const uint8_t* cwb,
+                     const uint8_t* s0s, const uint8_t* xs, uint8_t* ys);
+
+static int eval_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party,
+                       const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys) {
+  if (int rc = ensure_ctr(L.w)) return rc;
+  // the block count (dcf_prg_last_eval_blocks) covers the whole call: zeroed once here (the
+  // latency kernel zeroes it itself: one command less on a ~100 us call)
+  if (!(p->eval_mode == DCF_EVAL_AUTO && oct_eval(p, n_bytes, num_keys, (uint64_t)num_keys * ppk)))
+    HIP_TRY(hipMemsetAsync(L.w->d_ctr, 0, kCtrBytes, L.st));
+  L.w->last_prefix = 0;
+  phase_mark(p, L, 0);
+  const int rc = eval_body(p, L, n_bytes, num_keys, ppk, party, cwb, s0s, xs, ys);
+  phase_mark(p, L, 2);
+  p->last_ws.store(L.w);
+  return rc;
+}
+
+static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party, const uint8_t* cwb,
+                     const uint8_t* s0s, const uint8_t* xs, uint8_t* ys) {
+  Workspace* w = L.w;
+  hipStream_t st = L.st;
+  const uint64_t total = (uint64_t)num_keys * ppk;
   const size_t n = 8 * n_bytes, lam = p->lambda;
   if (lam > 16) {  // head/tail pipeline per key
+    phase_mark(p, L, 1);
     for (uint64_t k = 0; k < num_keys; ++k) {
-      int rc = p->kind == 1 ? eval_mmo_wide(p, n_bytes, num_keys, k, party, cwb, s0s + k * lam,
-                                            xs + k * ppk * n_bytes, ppk, ys + k * ppk * lam, (hipStream_t)stream)
-                            : eval_wide(p, n_bytes, num_keys, k, party, cwb, s0s + k * lam, xs + k * ppk * n_bytes,
-                                        ppk, ys + k * ppk * lam, (hipStream_t)stream);
+      int rc = p->kind == 1 ? eval_mmo_wide(p, w, n_bytes, num_keys, k, party, cwb, s0s + k * lam,
+                                            xs + k * ppk * n_bytes, ppk, ys + k * ppk * lam, st)
+                            : eval_wide(p, w, n_bytes, num_keys, k, party, cwb, s0s + k * lam, xs + k * ppk * n_bytes,
+                                        ppk, ys + k * ppk * lam, st);
       if (rc) return rc;
     }
     return DCF_OK;
@@ -947,7 +1127,6 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   const uint8_t* cwt = cwb + 2 * n * num_keys * lam;
   const uint4* np1 = (const uint4*)(cwb + dcf_cwb_np1_offset(n_bytes, lam, num_keys));
   const dim3 grid((unsigned)grid_for(total, p->cus)), block(kBlock);
-  hipStream_t st = (hipStream_t)stream;
   if (p->kind == 1) {  // MMO: lockstep, two blocks per level (the side's s and v), any engine setting
 #define DCF_MMO(MODE)                                                                                          \
   hipLaunchKernelGGL(k_eval16_mmo<MODE>, grid, block, 0, st, p->d_tab, p->d_rk128, cws, cwv, cwt, np1,            \
@@ -958,10 +1137,12 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     if (num_keys == 1 && (p->prefix_levels > 0 || total >= (uint64_t)p->cus * kBlock * 2)) {
       const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
       if (d) {
-        int rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+        int rc = try_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
         if (rc) return rc;
+        w->last_prefix = pf.levels;
       }
     }
+    phase_mark(p, L, 1);
     if (num_keys == 1) DCF_MMO(0);
     else if (ppk % 64 == 0) DCF_MMO(1);
     else DCF_MMO(2);
@@ -971,6 +1152,16 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   }
   const bool bs_ok = (num_keys == 1 && n_bytes <= 16);
   int mode = p->eval_mode;
+  if (mode == DCF_EVAL_AUTO && oct_eval(p, n_bytes, num_keys, total)) {
+    // Tiny batches (a single point through the C ABI: benches/dcf.rs bench_eval) are latency-
+    // bound: 8 lanes per point, one AES column each, A and B side by side (k_eval16_oct).
+    phase_mark(p, L, 1);
+    const uint32_t ppw = per_wg(total, p->cus, kBlock / 8);
+    hipLaunchKernelGGL(k_eval16_oct, dim3((unsigned)((total + ppw - 1) / ppw)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], cwb, s0s, (uint32_t)party, xs, (uint32_t)n_bytes, ppw, (uint64_t)total, ys, w->d_ctr);
+    HIP_TRY(hipGetLastError());
+    return DCF_OK;
+  }
   // Auto: one key -> the stream engine (T-table, right steps encrypt B only; C3: 407 M
   // evals/s vs 353 M hybrid, 332 M T-table).  Many keys -> lockstep T-table, whose waves
   // share one key's CWs through scalar loads (C5: 264 M vs 206 M evals/s with streams,
@@ -984,15 +1175,16 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
 #ifndef DCF_SMALL_PAIR
 #define DCF_SMALL_PAIR 1
 #endif
-    if (int rc = ensure_rk0(p)) return rc;
     PrefixTable spf{nullptr, 0u};
     if (DCF_SMALL_PAIR && num_keys == 1) {
       const uint32_t d = small_prefix_depth(p, n_bytes, total);
       if (d) {
-        int rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &spf, st);
+        int rc = try_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &spf, st);
         if (rc) return rc;
+        w->last_prefix = spf.levels;
       }
     }
+    phase_mark(p, L, 1);
     const uint64_t lanes_per_point = DCF_SMALL_PAIR ? 2 : 1;
     uint64_t threads = (total * lanes_per_point + p->cus - 1) / p->cus;
     threads = ((threads + 63) / 64) * 64;
@@ -1027,25 +1219,24 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "hybrid eval: single key, N <= 16");
     const bool mem = tt_single || p->hybrid_mem != 0;
     const int waves = mem ? 16 : kHybridWaves;
-    int ntt = tt_single ? 16 : p->hybrid_tt_waves;
+    int ntt = tt_single ? 16 : p->hybrid_tt_waves.load();
     if (mem && ntt < 1) ntt = 1;  // 15 LDS x-slots for bitsliced waves
     if (ntt > waves) ntt = waves;
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
     const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
     uint64_t blocks = (units + waves - 1) / waves;
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
     uint4* slabs = nullptr;
     if (mem) {
-      int rc = ensure_slabs(p, st);
+      int rc = ensure_slabs(p, w, st);
       if (rc) return rc;
-      slabs = reinterpret_cast<uint4*>(p->d_slabs);
+      slabs = reinterpret_cast<uint4*>(w->d_slabs);
     }
+    phase_mark(p, L, 1);
     const dim3 g((unsigned)blocks), b((unsigned)(waves * 64));
 #define DCF_HYB(XA, MEM)                                                                                   \
   hipLaunchKernelGGL((k_eval16_hybrid<XA, MEM>), g, b, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,       \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint32_t)ntt, \
-                     p->d_ctr, slabs, p->d_km, (uint4*)ys)
+                     w->d_ctr, slabs, p->d_km, (uint4*)ys)
     const bool xa = n_bytes % 4 == 0;
     if (xa && mem) DCF_HYB(true, true);
     else if (xa) DCF_HYB(true, false);
@@ -1056,109 +1247,107 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
     if (!(num_keys == 1 && n_bytes % 4 == 0 && n_bytes <= 16))
       return fail(DCF_ERR_UNSUPPORTED, "stream-hybrid eval: single key, N % 4 == 0, N <= 16");
     const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
-    if (units > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "stream-hybrid eval: more than 2^32 work units");
-    int rc = ensure_slabs(p, st);
+    if (total >= (1ull << 31)) return fail(DCF_ERR_UNSUPPORTED, "stream-hybrid eval: 2^31 points or more");
+    int rc = ensure_slabs(p, w, st);
     if (rc) return rc;
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
     PrefixTable pf{nullptr, 0u};
     const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
     if (d) {
-      rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+      rc = try_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
       if (rc) return rc;
+      w->last_prefix = pf.levels;
     }
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
+    phase_mark(p, L, 1);
     uint64_t blocks = (units + 15) / 16;
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
     hipLaunchKernelGGL(k_eval16_shybrid, dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
-                       (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, p->d_ctr,
-                       (uint4*)ys, pf, p->shy_mask, (uint32_t)p->shy_prio, reinterpret_cast<uint4*>(p->d_slabs),
+                       (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, w->d_ctr,
+                       (uint4*)ys, pf, (uint32_t)p->shy_mask, (uint32_t)p->shy_prio, reinterpret_cast<uint4*>(w->d_slabs),
                        p->d_km);
   } else if (mode == DCF_EVAL_STREAM) {
 #ifndef DCF_STREAM_NS
 #define DCF_STREAM_NS 2  // streams per lane
 #endif
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
-    if (int rc = ensure_rk0(p)) return rc;
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
-    const uint64_t units = (total + kStreamUnit - 1) / kStreamUnit;
-    if (units > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "stream eval: more than 2^32 work units");
-    uint64_t blocks = (units + 15) / 16;
-    if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
     const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16, multi = num_keys > 1;
+    if (multi && ppk >= (1ull << 31)) return fail(DCF_ERR_UNSUPPORTED, "multi-key stream eval: 2^31 points per key or more");
     const uint4* scs = cws;
     const uint8_t* sct = cwt;
     if (multi) {  // key-major digest of the K keys (kernels_stream.h)
-      const size_t need = (size_t)num_keys * n * 33;
-      if (p->kdig_bytes < need) {
-        if (p->d_kdig) {
-          HIP_TRY(hipStreamSynchronize(st));
-          HIP_TRY(hipFree(p->d_kdig));
-          p->d_kdig = nullptr;
-          p->kdig_bytes = 0;
-        }
-        HIP_TRY(hipMalloc(&p->d_kdig, need));
-        p->kdig_bytes = need;
-      }
+      if (int rc = grow(&w->d_kdig, &w->kdig_bytes, (size_t)num_keys * n * 33, st)) return rc;
       hipLaunchKernelGGL(k_cw_keymajor, dim3((unsigned)((num_keys + 15) / 16)), dim3(256), 0, st, cws, cwv, cwt,
-                         (uint32_t)n, (uint64_t)num_keys, (uint4*)p->d_kdig, p->d_kdig + (size_t)num_keys * n * 32);
+                         (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig, w->d_kdig + (size_t)num_keys * n * 32);
       HIP_TRY(hipGetLastError());
-      scs = (const uint4*)p->d_kdig;
-      sct = p->d_kdig + (size_t)num_keys * n * 32;
+      scs = (const uint4*)w->d_kdig;
+      sct = w->d_kdig + (size_t)num_keys * n * 32;
     }
     PrefixTable pf{nullptr, 0u};
     if (multi && DCF_MK_PFX && p->prefix_levels != 0 && n > kMkPfxLevels && ppk >= 32 &&
         num_keys <= (1ull << (31 - kMkPfxLevels))) {
       const size_t need = (size_t)num_keys * (32u << kMkPfxLevels);
-      if (p->pfx_bytes < need) {
-        if (p->d_pfx) {
+      if (w->pfx_bytes < need) {
+        if (w->d_pfx) {
           HIP_TRY(hipStreamSynchronize(st));
-          HIP_TRY(hipFree(p->d_pfx));
-          p->d_pfx = nullptr;
-          p->pfx_bytes = 0;
+          HIP_TRY(hipFree(w->d_pfx));
+          w->d_pfx = nullptr;
+          w->pfx_bytes = 0;
         }
-        if (hipMalloc(&p->d_pfx, need) != hipSuccess) {
+        if (hipMalloc(&w->d_pfx, need) != hipSuccess) {
           (void)hipGetLastError();  // no room: walk from the root (same output bytes)
         } else {
-          p->pfx_bytes = need;
+          w->pfx_bytes = need;
         }
       }
-      if (p->pfx_bytes >= need) {
+      if (w->pfx_bytes >= need) {
         hipLaunchKernelGGL(k_mk_prefix16<true>,
                            dim3((unsigned)(((num_keys << kMkPfxRoot) + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            st, p->d_tab, p->rk[0], cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party,
-                           (uint64_t)num_keys, (uint4*)p->d_pfx, p->d_rk0, p->d_ctr);
+                           (uint64_t)num_keys, (uint4*)w->d_pfx, p->d_rk0, w->d_ctr);
         HIP_TRY(hipGetLastError());
-        pf = PrefixTable{(const uint4*)p->d_pfx, kMkPfxLevels};
+        pf = PrefixTable{(const uint4*)w->d_pfx, kMkPfxLevels};
+        w->last_prefix = kMkPfxLevels;
       }
     }
     if (!multi) {
       const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
       if (d) {
-        int rc = try_prefix(p, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+        int rc = try_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
         if (rc) return rc;
+        w->last_prefix = pf.levels;
       }
       if (DCF_STREAM_D48) {  // single key: 48-byte CW rows + a zero row (kernels_stream.h k_cw_rows48)
-        const size_t need = (n + 1) * 48;
-        if (p->rows_bytes < need) {
-          if (p->d_rows) {
-            HIP_TRY(hipStreamSynchronize(st));
-            HIP_TRY(hipFree(p->d_rows));
-            p->d_rows = nullptr;
-            p->rows_bytes = 0;
-          }
-          HIP_TRY(hipMalloc(&p->d_rows, need));
-          p->rows_bytes = need;
-        }
-        hipLaunchKernelGGL(k_cw_rows48, dim3(1), dim3(256), 0, st, cws, cwv, cwt, (uint32_t)n, (uint4*)p->d_rows);
+        if (int rc = grow(&w->d_rows, &w->rows_bytes, (n + 1) * 48, st)) return rc;
+        hipLaunchKernelGGL(k_cw_rows48, dim3(1), dim3(256), 0, st, cws, cwv, cwt, (uint32_t)n, (uint4*)w->d_rows);
         HIP_TRY(hipGetLastError());
-        scs = (const uint4*)p->d_rows;
+        scs = (const uint4*)w->d_rows;
       }
     }
+    phase_mark(p, L, 1);
     const bool pfx = DCF_STREAM_PFXT && pf.levels != 0;
+    // One launch covers < 2^31 points and (multi-key) < 2^24 keys: the kernel's work
+    // distribution, point and digest-row indices are 32-bit (kernels_stream.h StreamLane).
+    // Larger batches run as several launches over consecutive points / whole keys, sharing
+    // the table, digest and CW rows built above.
+    const uint64_t kpl = multi ? std::max<uint64_t>(1, std::min<uint64_t>(1ull << 24, (1ull << 31) / ppk)) : 1;
+    const uint64_t ppl = multi ? kpl * ppk : (1ull << 31);  // points per launch
+    for (uint64_t c0 = 0; c0 < total; c0 += ppl) {
+    const uint64_t cnt = std::min<uint64_t>(ppl, total - c0), k0 = multi ? c0 / ppk : 0, kc = multi ? cnt / ppk : 1;
+    // the table build counted its work units on the counter: each walk's counter starts at 0
+    // (the block count beside it keeps the per-key top trees' blocks)
+    HIP_TRY(hipMemsetAsync(w->d_ctr, 0, 8, st));
+    const uint64_t units = (cnt + kStreamUnit - 1) / kStreamUnit;
+    uint64_t blocks = (units + 15) / 16;
+    if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
+    const uint4* lcs = multi ? scs + k0 * 2 * n : scs;
+    const uint8_t* lct = multi ? sct + k0 * n : sct;
+    const uint4* lnp1 = np1 + k0;
+    const uint8_t* lxs = xs + c0 * n_bytes;
+    uint8_t* lys = ys + c0 * lam;
+    const uint8_t* ls0 = s0s + k0 * lam;
+    const PrefixTable lpf = (multi && pf.levels) ? PrefixTable{pf.sv + 2 * (k0 << pf.levels), pf.levels} : pf;
 #define DCF_STREAM_KN(XR, MK, PF, D4, NBC)                                                                    \
   hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK, kBlock, false, PF, D4, NBC>), dim3((unsigned)blocks), block, 0, st, \
-                     p->d_tab, p->rk[0], scs, cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, \
-                     (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf, p->d_rk0)
+                     p->d_tab, p->rk[0], lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes, \
+                     (uint64_t)kc, (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0)
 #define DCF_STREAM_K(XR, MK, PF, D4) DCF_STREAM_KN(XR, MK, PF, D4, 0)
     // single key, x in registers: N = 16 (C1 / C3) and N = 4 (C2) with the x width fixed at
     // compile time (a point's start loads x without width branches: C2 starts a point every
@@ -1176,19 +1365,22 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
       uint64_t b2 = (units + 9) / 10;
       if (b2 > 2 * (uint64_t)p->cus) b2 = 2 * (uint64_t)p->cus;
       hipLaunchKernelGGL((k_eval16_stream<2, true, false, 640, true>), dim3((unsigned)b2), dim3(640), 0, st, p->d_tab,
-                         p->rk[0], scs, cwv, sct, np1, (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes,
-                         (uint64_t)num_keys, (uint64_t)ppk, (uint64_t)total, p->d_ctr, (uint4*)ys, pf, p->d_rk0);
+                         p->rk[0], lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes,
+                         (uint64_t)kc, (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0);
     } else
 #endif
     if (xreg && multi) DCF_STREAM(true, true);
     else if (xreg) DCF_STREAM(true, false);
     else if (multi) DCF_STREAM(false, true);
     else DCF_STREAM(false, false);
+    HIP_TRY(hipGetLastError());
+    }  // launches
 #undef DCF_STREAM
 #undef DCF_STREAM_K
 #undef DCF_STREAM_KN
   } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
+    phase_mark(p, L, 1);
     const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;
     uint64_t blocks = (waves + 3) / 4;
     const uint64_t cap = (uint64_t)p->cus * 8;
@@ -1200,13 +1392,12 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
       hipLaunchKernelGGL(k_eval16_bs<false>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
                          (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
   } else {  // lockstep T-table, 64-point units from the work counter
-    if (!p->d_ctr) HIP_TRY(hipMalloc(&p->d_ctr, kCtrBytes));
-    HIP_TRY(hipMemsetAsync(p->d_ctr, 0, kCtrBytes, st));
     if ((total + 63) / 64 > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "more than 2^32 64-point units");
+    phase_mark(p, L, 1);
 #define DCF_TT(MODE)                                                                                         \
   hipLaunchKernelGGL(k_eval16<MODE>, grid, block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,               \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk, \
-                     (uint4*)ys, p->d_ctr)
+                     (uint4*)ys, w->d_ctr)
     if (num_keys == 1) DCF_TT(0);
     else if (ppk % 64 == 0) DCF_TT(1);
     else DCF_TT(2);
@@ -1216,92 +1407,155 @@ static int eval_launch(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t ppk, 
   return DCF_OK;
 }
 
+static int check_eval_args(dcf_prg* p, size_t n_bytes, int party, uint64_t total, const void* cwb, const void* s0s,
+                           const void* xs, const void* ys) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  if (n_bytes == 0) return fail(DCF_ERR_N, "n_bytes must be > 0");
+  if (party != 0 && party != 1) return fail(DCF_ERR_ARG, "party must be 0 or 1");
+  if (total && (!cwb || !s0s || !xs || !ys)) return fail(DCF_ERR_ARG, "null buffer");
+  return DCF_OK;
+}
+
 int dcf_eval_device(dcf_prg* p, size_t n_bytes, int party, const uint8_t* cwb, const uint8_t* s0,
                     const uint8_t* xs, size_t m, uint8_t* ys, void* stream) {
-  return eval_launch(p, n_bytes, 1, m, party, cwb, s0, xs, ys, stream);
+  if (int rc = check_eval_args(p, n_bytes, party, m, cwb, s0, xs, ys)) return rc;
+  if (m == 0) return DCF_OK;
+  DeviceGuard dg(p->device);
+  Lease L(p);
+  if (int rc = L.order((hipStream_t)stream)) return rc;
+  return eval_launch(p, L, n_bytes, 1, m, party, cwb, s0, xs, ys);
 }
 
 int dcf_eval_multikey_device(dcf_prg* p, size_t n_bytes, size_t num_keys, size_t points_per_key, int party,
                              const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys,
                              void* stream) {
-  return eval_launch(p, n_bytes, num_keys, points_per_key, party, cwb, s0s, xs, ys, stream);
+  const uint64_t total = (uint64_t)num_keys * points_per_key;
+  if (int rc = check_eval_args(p, n_bytes, party, total, cwb, s0s, xs, ys)) return rc;
+  if (total == 0) return DCF_OK;
+  DeviceGuard dg(p->device);
+  Lease L(p);
+  if (int rc = L.order((hipStream_t)stream)) return rc;
+  return eval_launch(p, L, n_bytes, num_keys, points_per_key, party, cwb, s0s, xs, ys);
 }
 
-// ---- host-pointer path: prg-owned streams, pooled staging, chunked pipeline ----
+// ---- host-pointer path: per-workspace streams and staging, chunked pipeline ----
 
 static size_t align256(size_t n) { return (n + 255) & ~(size_t)255; }
 
 // Points per chunk of the host eval pipeline: ~128 MiB of x + y per buffer (C3 shape: 4 Mi
 // points, an 8 ms kernel against ~3 ms of PCIe each way, so the copies hide behind it).
 constexpr size_t kHostChunkBytes = 128ull << 20;
+// Tiny host calls (the latency kernels' batch sizes): inputs and outputs through one pinned,
+// device-mapped buffer that the kernel reads and writes itself — one launch, no copy commands.
+constexpr size_t kTinyBytes = 1ull << 20;
 
-static int ensure_host_path(dcf_prg* p) {
-  if (p->hs[0]) return DCF_OK;
+static int ensure_host_path(Workspace* w) {
+  if (w->hs[0]) return DCF_OK;
   hipStream_t hs[3] = {nullptr, nullptr, nullptr};
   for (auto& s : hs) HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  for (auto& e : p->hev)
+  for (auto& e : w->hev)
     if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  for (int i = 0; i < 3; ++i) p->hs[i] = hs[i];
+  for (int i = 0; i < 3; ++i) w->hs[i] = hs[i];
   return DCF_OK;
 }
 
-static int ensure_stage(dcf_prg* p, size_t hbytes, size_t dbytes) {
-  if (p->h_stage_bytes < hbytes) {
-    if (p->h_stage) HIP_TRY(hipHostFree(p->h_stage));
-    p->h_stage = nullptr;
-    p->h_stage_bytes = 0;
-    HIP_TRY(hipHostMalloc((void**)&p->h_stage, hbytes, hipHostMallocDefault));
-    p->h_stage_bytes = hbytes;
+static int ensure_stage(Workspace* w, size_t hbytes, size_t dbytes) {
+  if (w->h_stage_bytes < hbytes) {
+    if (w->h_stage) HIP_TRY(hipHostFree(w->h_stage));
+    w->h_stage = nullptr;
+    w->h_stage_bytes = 0;
+    HIP_TRY(hipHostMalloc((void**)&w->h_stage, hbytes, hipHostMallocDefault));
+    w->h_stage_bytes = hbytes;
   }
-  if (p->d_stage_bytes < dbytes) {
-    if (p->d_stage) HIP_TRY(hipFree(p->d_stage));
-    p->d_stage = nullptr;
-    p->d_stage_bytes = 0;
-    HIP_TRY(hipMalloc(&p->d_stage, dbytes));
-    p->d_stage_bytes = dbytes;
+  if (w->d_stage_bytes < dbytes) {
+    if (w->d_stage) HIP_TRY(hipFree(w->d_stage));
+    w->d_stage = nullptr;
+    w->d_stage_bytes = 0;
+    HIP_TRY(hipMalloc(&w->d_stage, dbytes));
+    w->d_stage_bytes = dbytes;
   }
   return DCF_OK;
 }
 
-// Every host entry point ends here: wait for the prg's own streams only (never the whole
-// device), also after an error, so no queued copy still targets the staging buffers.
-static int host_finish(dcf_prg* p, int rc) {
-  for (hipStream_t s : p->hs) {
-    if (!s) continue;
-    const hipError_t e = hipStreamSynchronize(s);
-    if (e != hipSuccess && rc == DCF_OK) {
+// The tiny-call buffer: coherent (the kernel's stores are visible once the stream has passed
+// it) and mapped into the device's address space.  Returns its device address.
+static int ensure_tiny(Workspace* w, uint8_t** dptr) {
+  if (!w->h_tiny) {
+    HIP_TRY(hipHostMalloc((void**)&w->h_tiny, kTinyBytes, hipHostMallocMapped | hipHostMallocCoherent));
+    w->tiny_bytes = kTinyBytes;
+  }
+  HIP_TRY(hipHostGetDevicePointer((void**)dptr, w->h_tiny, 0));
+  return DCF_OK;
+}
+
+// Every host entry point ends here: wait for the workspace's own streams only (never the
+// whole device), also after an error, so no queued copy still targets the staging buffers.
+static int host_finish(Lease& L, int rc) {
+  Workspace* w = L.w;
+  bool ok = true;
+  for (int i = 0; i < 3; ++i) {
+    if (!w->hs[i] || !((w->host_streams >> i) & 1u)) continue;
+    const hipError_t e = hipStreamSynchronize(w->hs[i]);
+    if (e != hipSuccess) {
+      ok = false;
       (void)hipGetLastError();
-      rc = fail(DCF_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+      if (rc == DCF_OK) rc = fail(DCF_ERR_HIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
     }
   }
+  w->host_streams = 0;
+  L.drained = ok;
   return rc;
 }
 
-// Dcf::eval over host buffers (caller: DeviceGuard held, arguments checked, m > 0).  Chunks
-// of `chunk` points flow through two staging slots on three streams: copy-in (pinned ->
-// device), compute (eval_launch), copy-out (device -> pinned); the host copies chunk c's x
-// into pinned memory and chunk c-1's y out of it while the GPU works on chunk c, so PCIe
-// transfers overlap the kernels of neighbouring chunks.  The GPU never touches caller memory.
-static int host_eval(dcf_prg* p, size_t nb, int party, const uint8_t* cwb, size_t cwb_len, const uint8_t* s0,
-                     const uint8_t* xs, uint64_t m, uint8_t* ys) {
+// A lease for a host entry point: its workspace's streams exist and the compute stream is
+// ordered after the workspace's earlier device work (a *_device call on any stream).
+static int host_lease(Lease& L) {
+  if (int rc = ensure_host_path(L.w)) return rc;
+  L.w->host_streams = 2u;  // the compute stream; the chunked eval pipeline adds copy-in / copy-out
+  return L.order(L.w->hs[1]);
+}
+
+// Dcf::eval over host buffers (caller: DeviceGuard held, arguments checked, m > 0).
+// Tiny batches: one launch of k_eval16_oct that reads the key and points from, and writes
+// the outputs to, the workspace's mapped pinned buffer.  Otherwise chunks of `chunk` points
+// flow through two staging slots on three streams: copy-in (pinned -> device), compute
+// (eval_launch), copy-out (device -> pinned); the host copies chunk c's x into pinned memory
+// and chunk c-1's y out of it while the GPU works on chunk c, so PCIe transfers overlap the
+// kernels of neighbouring chunks.  The GPU never touches caller memory.
+static int host_eval(dcf_prg* p, Lease& L, size_t nb, int party, const uint8_t* cwb, size_t cwb_len,
+                     const uint8_t* s0, const uint8_t* xs, uint64_t m, uint8_t* ys) {
+  Workspace* w = L.w;
   const size_t lam = p->lambda;
-  if (int rc = ensure_host_path(p)) return rc;
+  const size_t ko = 0, so0 = align256(cwb_len), xo = so0 + 256, yo = xo + align256(m * nb);
+  if (oct_eval(p, nb, 1, m) && yo + m * lam <= kTinyBytes) {
+    uint8_t* d = nullptr;
+    if (int rc = ensure_tiny(w, &d)) return rc;
+    uint8_t* h = w->h_tiny;
+    memcpy(h + ko, cwb, cwb_len);
+    memcpy(h + so0, s0, lam);
+    memcpy(h + xo, xs, m * nb);
+    if (int rc = eval_launch(p, L, nb, 1, m, party, d + ko, d + so0, d + xo, d + yo)) return rc;
+    HIP_TRY(hipStreamSynchronize(L.st));
+    memcpy(ys, h + yo, m * lam);
+    return DCF_OK;
+  }
+  w->host_streams = 7u;
   const uint64_t chunk = std::min<uint64_t>(m, std::max<uint64_t>(256, kHostChunkBytes / (nb + lam)));
   const int nbuf = m > chunk ? 2 : 1;
   const size_t kb = align256(cwb_len) + align256(lam);
   const size_t xb = align256(chunk * nb), yb = align256(chunk * lam);
-  if (int rc = ensure_stage(p, nbuf * (xb + yb), kb + nbuf * (xb + yb))) return rc;
-  uint8_t* dk = p->d_stage;
+  if (int rc = ensure_stage(w, nbuf * (xb + yb), kb + nbuf * (xb + yb))) return rc;
+  uint8_t* dk = w->d_stage;
   uint8_t* ds0 = dk + align256(cwb_len);
   uint8_t *dx[2], *dy[2], *hx[2], *hy[2];
   for (int b = 0; b < nbuf; ++b) {
     dx[b] = dk + kb + b * xb;
     dy[b] = dk + kb + nbuf * xb + b * yb;
-    hx[b] = p->h_stage + b * xb;
-    hy[b] = p->h_stage + nbuf * xb + b * yb;
+    hx[b] = w->h_stage + b * xb;
+    hy[b] = w->h_stage + nbuf * xb + b * yb;
   }
-  hipStream_t si = p->hs[0], sc = p->hs[1], so = p->hs[2];
-  hipEvent_t *ev_in = p->hev, *ev_k = p->hev + 2, *ev_out = p->hev + 4;
+  hipStream_t si = w->hs[0], sc = w->hs[1], so = w->hs[2];
+  hipEvent_t *ev_in = w->hev, *ev_k = w->hev + 2, *ev_out = w->hev + 4;
   HIP_TRY(hipMemcpyAsync(dk, cwb, cwb_len, hipMemcpyHostToDevice, sc));
   HIP_TRY(hipMemcpyAsync(ds0, s0, lam, hipMemcpyHostToDevice, sc));
   const uint64_t nch = (m + chunk - 1) / chunk;
@@ -1316,7 +1570,7 @@ static int host_eval(dcf_prg* p, size_t nb, int party, const uint8_t* cwb, size_
       HIP_TRY(hipEventRecord(ev_in[b], si));
       HIP_TRY(hipStreamWaitEvent(sc, ev_in[b], 0));
       if (c >= 2) HIP_TRY(hipStreamWaitEvent(sc, ev_out[b], 0));  // chunk c-2's D2H is done with dy[b]
-      if (int rc = eval_launch(p, nb, 1, cnt, party, dk, ds0, dx[b], dy[b], sc)) return rc;
+      if (int rc = eval_launch(p, L, nb, 1, cnt, party, dk, ds0, dx[b], dy[b])) return rc;
       HIP_TRY(hipEventRecord(ev_k[b], sc));
       HIP_TRY(hipStreamWaitEvent(so, ev_k[b], 0));
       HIP_TRY(hipMemcpyAsync(hy[b], dy[b], cnt * lam, hipMemcpyDeviceToHost, so));
@@ -1333,38 +1587,49 @@ static int host_eval(dcf_prg* p, size_t nb, int party, const uint8_t* cwb, size_
   return DCF_OK;
 }
 
-// Dcf::gen for one key over host buffers, on the prg's compute stream.
-static int host_gen(dcf_prg* p, size_t nb, const uint8_t* alpha, const uint8_t* beta, const uint8_t* s0_0,
+// Dcf::gen for one key over host buffers, on the workspace's compute stream.  Tiny path (the
+// column kernel): inputs and the CWB through the mapped pinned buffer, one launch.
+static int host_gen(dcf_prg* p, Lease& L, size_t nb, const uint8_t* alpha, const uint8_t* beta, const uint8_t* s0_0,
                     const uint8_t* s0_1, int bound, uint8_t* cwb_out) {
+  Workspace* w = L.w;
   const size_t lam = p->lambda, cwb_len = dcf_cwb_bytes(nb, lam, 1);
-  if (int rc = ensure_host_path(p)) return rc;
   const size_t oa = 0, ob = align256(nb), o0 = ob + align256(lam), o1 = o0 + align256(lam), ok = o1 + align256(lam);
   const size_t total = ok + align256(cwb_len);
-  if (int rc = ensure_stage(p, total, total)) return rc;
-  uint8_t *h = p->h_stage, *d = p->d_stage;
+  const bool tiny = col_gen(p, nb, 1) && total <= kTinyBytes;
+  uint8_t *h = nullptr, *d = nullptr;
+  if (tiny) {
+    if (int rc = ensure_tiny(w, &d)) return rc;
+    h = w->h_tiny;
+  } else {
+    if (int rc = ensure_stage(w, total, total)) return rc;
+    h = w->h_stage;
+    d = w->d_stage;
+  }
   memcpy(h + oa, alpha, nb);
   memcpy(h + ob, beta, lam);
   memcpy(h + o0, s0_0, lam);
   memcpy(h + o1, s0_1, lam);
-  hipStream_t sc = p->hs[1];
-  HIP_TRY(hipMemcpyAsync(d, h, ok, hipMemcpyHostToDevice, sc));
-  HIP_TRY(hipMemsetAsync(d + ok, 0, cwb_len, sc));
-  int rc = dcf_gen_batch_device(p, nb, 1, d + oa, d + ob, d + o0, d + o1, bound, d + ok, sc);
+  hipStream_t sc = L.st;
+  if (!tiny) HIP_TRY(hipMemcpyAsync(d, h, ok, hipMemcpyHostToDevice, sc));
+  if (!tiny) HIP_TRY(hipMemsetAsync(d + ok, 0, cwb_len, sc));  // the CWB's padding bytes read 0
+  int rc = gen_launch(p, L, nb, 1, d + oa, d + ob, d + o0, d + o1, bound, d + ok);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(h + ok, d + ok, cwb_len, hipMemcpyDeviceToHost, sc));
+  if (!tiny) HIP_TRY(hipMemcpyAsync(h + ok, d + ok, cwb_len, hipMemcpyDeviceToHost, sc));
   HIP_TRY(hipStreamSynchronize(sc));
   memcpy(cwb_out, h + ok, cwb_len);
+  if (tiny)  // the CWB's padding bytes (between cw_t and cw_np1) read 0, as on the staged path
+    memset(cwb_out + 2 * 8 * nb * lam + 8 * nb, 0, dcf_cwb_np1_offset(nb, lam, 1) - (2 * 8 * nb * lam + 8 * nb));
   return DCF_OK;
 }
 
-// Prg::gen for m seeds over host buffers (test hook), on the prg's compute stream.
-static int host_prg_gen(dcf_prg* p, const uint8_t* seeds, size_t m, uint8_t* out) {
+// Prg::gen for m seeds over host buffers (test hook), on the workspace's compute stream.
+static int host_prg_gen(dcf_prg* p, Lease& L, const uint8_t* seeds, size_t m, uint8_t* out) {
+  Workspace* w = L.w;
   const size_t lam = p->lambda, row = 4 * lam + 2;
-  if (int rc = ensure_host_path(p)) return rc;
   const size_t so = align256(m * lam), total = so + align256(m * row);
-  if (int rc = ensure_stage(p, total, total)) return rc;
-  uint8_t *h = p->h_stage, *d = p->d_stage;
-  hipStream_t sc = p->hs[1];
+  if (int rc = ensure_stage(w, total, total)) return rc;
+  uint8_t *h = w->h_stage, *d = w->d_stage;
+  hipStream_t sc = L.st;
   memcpy(h, seeds, m * lam);
   HIP_TRY(hipMemcpyAsync(d, h, m * lam, hipMemcpyHostToDevice, sc));
   if (p->kind == 1 && lam > 16)
@@ -1481,7 +1746,9 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   if (party != 0 && party != 1) return fail(DCF_ERR_ARG, "party must be 0 or 1");
   if (!cwb || !s0 || !ys) return fail(DCF_ERR_ARG, "null buffer");
   DeviceGuard dg(p->device);
-  hipStream_t st = (hipStream_t)stream;
+  Lease L(p);
+  if (int rc = L.order((hipStream_t)stream)) return rc;
+  hipStream_t st = L.st;
   const uint32_t nlev = (uint32_t)(8 * n_bytes);
   const uint64_t npts = 1ull << nlev;
   const size_t lam = p->lambda;
@@ -1490,7 +1757,7 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
     HIP_TRY(xs.alloc(npts * n_bytes));
     hipLaunchKernelGGL(k_domain_points, dim3(1024), dim3(256), 0, st, (uint32_t)n_bytes, npts, (uint8_t*)xs.p);
     HIP_TRY(hipGetLastError());
-    int rc = eval_launch(p, n_bytes, 1, npts, party, cwb, s0, (const uint8_t*)xs.p, ys, st);
+    int rc = eval_launch(p, L, n_bytes, 1, npts, party, cwb, s0, (const uint8_t*)xs.p, ys);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(st));  // xs is freed on return
     return DCF_OK;
@@ -1504,10 +1771,9 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   const size_t nodeb = 33;
   // + one work counter per launch (64-node units, see next_wave_base) after the nodes
   const size_t ctr_off = (2 * maxnodes * nodeb + 64 + 255) & ~(size_t)255;
-  int rc = ensure_ws(p, ctr_off + 64 * sizeof(uint32_t), st);
+  int rc = ensure_ws(L.w, ctr_off + 64 * sizeof(uint32_t), st);
   if (rc) return rc;
-  if (DCF_FD_GK && fused && (rc = ensure_rk0(p))) return rc;  // the tail reads it only with DCF_FD_GK
-  uint8_t* w = p->d_ws;
+  uint8_t* w = L.w->d_ws;
   uint32_t* ctrs = (uint32_t*)(w + ctr_off);
   HIP_TRY(hipMemsetAsync(ctrs, 0, 64 * sizeof(uint32_t), st));
   uint4* s_a = (uint4*)w;
@@ -1560,8 +1826,10 @@ int dcf_gen(dcf_prg* p, size_t n_bytes, const uint8_t* alpha, const uint8_t* bet
   if (bound != DCF_BOUND_LT_BETA && bound != DCF_BOUND_GT_BETA) return fail(DCF_ERR_ARG, "bad bound");
   DeviceGuard dg(p->device);
   if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
-  int rc = host_gen(p, n_bytes, alpha, beta, s0_0, s0_1, bound, cwb_out);
-  return host_finish(p, rc);
+  Lease L(p);
+  int rc = host_lease(L);
+  if (rc == DCF_OK) rc = host_gen(p, L, n_bytes, alpha, beta, s0_0, s0_1, bound, cwb_out);
+  return host_finish(L, rc);
 }
 
 int dcf_eval(dcf_prg* p, size_t n_bytes, int party, const uint8_t* cwb, size_t cwb_len, const uint8_t* s0,
@@ -1577,8 +1845,10 @@ int dcf_eval(dcf_prg* p, size_t n_bytes, int party, const uint8_t* cwb, size_t c
   if (!xs || !ys) return fail(DCF_ERR_ARG, "null buffer");
   DeviceGuard dg(p->device);
   if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
-  int rc = host_eval(p, n_bytes, party, cwb, cwb_len, s0, xs, m, ys);
-  return host_finish(p, rc);
+  Lease L(p);
+  int rc = host_lease(L);
+  if (rc == DCF_OK) rc = host_eval(p, L, n_bytes, party, cwb, cwb_len, s0, xs, m, ys);
+  return host_finish(L, rc);
 }
 
 int dcf_prg_gen(dcf_prg* p, const uint8_t* seeds, size_t m, uint8_t* out) {
@@ -1587,8 +1857,10 @@ int dcf_prg_gen(dcf_prg* p, const uint8_t* seeds, size_t m, uint8_t* out) {
   if (!seeds || !out) return fail(DCF_ERR_ARG, "null buffer");
   DeviceGuard dg(p->device);
   if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
-  int rc = host_prg_gen(p, seeds, m, out);
-  return host_finish(p, rc);
+  Lease L(p);
+  int rc = host_lease(L);
+  if (rc == DCF_OK) rc = host_prg_gen(p, L, seeds, m, out);
+  return host_finish(L, rc);
 }
 
 // ---- multi-GPU (SURVEY §8(b) dcf_eval_multi_gpu; the reference spreads Dcf::eval over
@@ -1629,8 +1901,11 @@ int dcf_eval_multi_gpu(dcf_prg* const* prgs, size_t G, size_t n_bytes, int party
     if (!dg.ok) {
       rcs[g] = fail(DCF_ERR_HIP, "hipSetDevice failed");
     } else {
-      rcs[g] = host_finish(prgs[g], host_eval(prgs[g], n_bytes, party, cwb, cwb_len, s0, xs + start * n_bytes, cnt,
-                                              ys + start * lam));
+      Lease L(prgs[g]);
+      int rc = host_lease(L);
+      if (rc == DCF_OK)
+        rc = host_eval(prgs[g], L, n_bytes, party, cwb, cwb_len, s0, xs + start * n_bytes, cnt, ys + start * lam);
+      rcs[g] = host_finish(L, rc);
     }
     if (rcs[g]) errs[g] = t_err;
   };
@@ -1657,33 +1932,27 @@ int dcf_eval_multi_gpu_device(dcf_prg* const* prgs, size_t G, size_t n_bytes, in
   size_t off = 0;
   for (size_t g = 0; g < G; ++g) {
     dcf_prg* p = prgs[g];
-    hipStream_t st = streams ? (hipStream_t)streams[g] : nullptr;
     DeviceGuard dg(p->device);
     if (!dg.ok) return fail(DCF_ERR_HIP, "hipSetDevice failed");
+    Lease L(p);
+    if (int rc = L.order(streams ? (hipStream_t)streams[g] : nullptr)) return rc;
+    hipStream_t st = L.st;
+    Workspace* w = L.w;
     // the key to this device, once per call (4.2 KB at N = LAMBDA = 16): the "broadcast"
     const size_t kb = align256(cwb_len) + align256(lam);
-    if (p->mkey_bytes < kb) {
-      if (p->d_mkey) {
-        HIP_TRY(hipStreamSynchronize(st));
-        HIP_TRY(hipFree(p->d_mkey));
-        p->d_mkey = nullptr;
-        p->mkey_bytes = 0;
-      }
-      HIP_TRY(hipMalloc(&p->d_mkey, kb));
-      p->mkey_bytes = kb;
-    }
-    HIP_TRY(hipMemcpyAsync(p->d_mkey, cwb, cwb_len, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(p->d_mkey + align256(cwb_len), s0, lam, hipMemcpyHostToDevice, st));
+    if (int rc = grow(&w->d_mkey, &w->mkey_bytes, kb, st)) return rc;
+    HIP_TRY(hipMemcpyAsync(w->d_mkey, cwb, cwb_len, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(w->d_mkey + align256(cwb_len), s0, lam, hipMemcpyHostToDevice, st));
     if (ms[g]) {
       if (!xs[g] || !ys[g]) return fail(DCF_ERR_ARG, "null slice buffer");
-      int rc = eval_launch(p, n_bytes, 1, ms[g], party, p->d_mkey, p->d_mkey + align256(cwb_len), xs[g], ys[g], st);
+      int rc = eval_launch(p, L, n_bytes, 1, ms[g], party, w->d_mkey, w->d_mkey + align256(cwb_len), xs[g], ys[g]);
       if (rc) return rc;
       if (gather_ys) {  // slice g -> its rows of the gather buffer on prgs[0]'s device, over xGMI
         if (p->device != dev0) {
+          // direct peer writes when the devices can map each other; hipMemcpyPeerAsync stages the
+          // copy itself when they cannot, so a refused peer mapping is not an error
           const hipError_t e = hipDeviceEnablePeerAccess(dev0, 0);
-          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-            return fail(DCF_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
-          (void)hipGetLastError();
+          if (e != hipSuccess) (void)hipGetLastError();
           HIP_TRY(hipMemcpyPeerAsync(gather_ys + off * lam, dev0, ys[g], p->device, ms[g] * lam, st));
         } else {
           HIP_TRY(hipMemcpyAsync(gather_ys + off * lam, ys[g], ms[g] * lam, hipMemcpyDeviceToDevice, st));
@@ -1694,6 +1963,25 @@ int dcf_eval_multi_gpu_device(dcf_prg* const* prgs, size_t G, size_t n_bytes, in
   }
   return DCF_OK;
 }
+
+#ifdef DCF_CLOCK_STAMPS
+// Diagnostic builds only (not in include/dcf_hip.h): the in-kernel clock stamps of slot `slot`
+// (0 = k_eval_wide_tail2, 1 = k_eval_wide_head_stream, 2 = k_eval16_stream) of the last launch:
+// per workgroup {memtime, realtime} at start and end, kClkGroups x 4 u64.
+int dcf_debug_clock_stamps(int device, int slot, unsigned long long* out, size_t n) {
+  if (!out || slot < 0 || slot >= (int)kClkSlots || n < (size_t)kClkGroups * 4) return fail(DCF_ERR_ARG, "bad argument");
+  DeviceGuard dg(device);
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk_stamps), (size_t)kClkGroups * 4 * 8,
+                              (size_t)slot * kClkGroups * 4 * 8, hipMemcpyDeviceToHost));
+  return DCF_OK;
+}
+int dcf_debug_clock_reset(int device) {
+  DeviceGuard dg(device);
+  static std::vector<unsigned long long> z((size_t)kClkSlots * kClkGroups * 4, 0);
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_clk_stamps), z.data(), z.size() * 8, 0, hipMemcpyHostToDevice));
+  return DCF_OK;
+}
+#endif
 
 void dcf_point_slice(size_t total, size_t G, size_t g, size_t* start, size_t* count) {
   if (!start || !count) return;

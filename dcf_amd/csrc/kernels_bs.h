@@ -25,11 +25,6 @@ __device__ __forceinline__ uint32_t qperm(uint32_t v) {
   // v_mov of a fallback value is needed before each DPP move.
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
-// DPP quad_perm encodings: lane c reads lane sel[c]; ctrl = sel0 | sel1<<2 | sel2<<4 | sel3<<6
-constexpr int kQpRot1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // c <- c+1
-constexpr int kQpRot2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // c <- c+2
-constexpr int kQpRot3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // c <- c+3
-constexpr int kQpBcast0 = 0;                                   // c <- 0
 
 // 32 x 32 bit transpose (LSB convention): afterwards a[j] bit i = old a[i] bit j.
 __device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {

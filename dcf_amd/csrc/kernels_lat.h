@@ -1,0 +1,232 @@
+// kernels_lat.h — latency kernels for tiny batches at LAMBDA = 16 (Hirose PRG):
+// one AES-256 column per lane.  Included by dcf_hip.hip only (after kernels16.h).
+//
+// The crate's own benches time ONE gen and ONE single-point eval per call
+// (benches/dcf.rs:7-43).  A lone point walks its 8N levels back to back, so what
+// bounds the call is the latency of one level, not throughput: with a whole block
+// per lane (k_eval16_pair) a round is 16 table lookups + 16 address VALUs + 8 XORs
+// issued by one wave (~300 cycles per round).  Here the four columns of a block sit
+// in a lane quad: lane j builds column j of the next state from byte 0 of its own
+// column and bytes 1..3 of columns j+1..j+3, which DPP quad_perm rotations bring in
+// (T-table round of FIPS-197 §5.1 as in aes256_tt: out_j = T0[s_j.b0] ^ T1[s_{j+1}.b1]
+// ^ T2[s_{j+2}.b2] ^ T3[s_{j+3}.b3] ^ rk_j) — 4 lookups, 4 address VALUs, 3 DPP moves
+// and 2 XORs per lane and round, a quarter of the dependent chain.
+//   eval  (k_eval16_oct): 8 lanes per point, quad 0 = A = AES(s), quad 1 = B = AES(~s);
+//         a DPP row rotation swaps the two quads' column, and every lane then runs the
+//         level update (lib.rs:174-189) for its column; t comes from column 0's lanes.
+//   gen   (k_gen16_col):  16 lanes per key, quad q = block q of the level (A0, B0, A1,
+//         B1: prg.rs:42-73 on both parties' seeds, lib.rs:103-104); three DPP row
+//         rotations give every lane its column of all four blocks (lib.rs:105-152).
+// The key (eval) / alpha (gen) are staged in LDS beside the T-tables, so the kernels may
+// read their inputs from, and write outputs to, host-mapped pinned memory (the C ABI's
+// host entry points pass such buffers for tiny calls: no copy commands at all).
+#pragma once
+
+#include "aes_lds.h"
+
+namespace {
+
+constexpr uint32_t kColMaxLevels = 256;  // N <= 32 (the staged key / x rows)
+
+// DPP: quad_perm rotations (aes_lds.h kQpRot*) and row rotations (lane i <- i - n mod 16).
+constexpr int kRowRor4 = 0x124, kRowRor8 = 0x128, kRowRor12 = 0x12C;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+
+// Column j of AES-256(in) for the lane quad holding the block's four columns (lane j of the
+// quad holds column j); kw[r] = word j of round key r.
+__device__ __forceinline__ uint32_t aes256_col(uint32_t st, const uint32_t (&kw)[15], const uint32_t* lds,
+                                               uint32_t lc) {
+  st ^= kw[0];
+#pragma unroll
+  for (int r = 1; r < 14; ++r) {
+    const uint32_t w1 = dpp<kQpRot1>(st), w2 = dpp<kQpRot2>(st), w3 = dpp<kQpRot3>(st);
+    const uint32_t a = lk<0, 0>(lds, st, lc);
+    const uint32_t c = lk<1, 1>(lds, w1, lc);
+    const uint32_t d = lk<2, 2>(lds, w2, lc);
+    const uint32_t e = lk<3, 3>(lds, w3, lc);
+    st = xor3(xor3(a, c, d), e, kw[r]);
+  }
+  // final round: SubBytes + ShiftRows + AddRoundKey (S(x) sits in byte r of T_{(r+2)&3})
+  const uint32_t w1 = dpp<kQpRot1>(st), w2 = dpp<kQpRot2>(st), w3 = dpp<kQpRot3>(st);
+  const uint32_t a = lk<2, 0>(lds, st, lc);
+  const uint32_t c = lk<3, 1>(lds, w1, lc);
+  const uint32_t d = lk<0, 2>(lds, w2, lc);
+  const uint32_t e = lk<1, 3>(lds, w3, lc);
+  return xor3(__builtin_amdgcn_perm(c, a, 0x0c0c0500u), __builtin_amdgcn_perm(e, d, 0x07020c0cu), kw[14]);
+}
+
+// The 128 KiB replicated T-tables (lds_fill_tables' layout), every load of a thread issued
+// before its stores: a latency kernel cannot afford 32 dependent load/store round trips.
+__device__ __forceinline__ void lds_fill_tables_fast(uint32_t* lds, const uint32_t* __restrict__ tab) {
+  constexpr int kPer = kLdsWords / kBlock;
+  uint32_t v[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int idx = (int)threadIdx.x + i * kBlock;
+    const int half = idx >> 14, rem = idx & 16383;
+    v[i] = tab[(2 * half + ((rem & 63) >> 5)) * 256 + (rem >> 6)];
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) lds[(int)threadIdx.x + i * kBlock] = v[i];
+}
+
+__device__ __forceinline__ void col_round_keys(const RoundKeys& rk, uint32_t j, uint32_t (&kw)[15]) {
+#pragma unroll
+  for (int r = 0; r < 15; ++r) {
+    const uint32_t a = rk.w[4 * r], b = rk.w[4 * r + 1], c = rk.w[4 * r + 2], d = rk.w[4 * r + 3];
+    kw[r] = (j & 2u) ? ((j & 1u) ? d : c) : ((j & 1u) ? b : a);
+  }
+}
+
+// Dcf::eval (lib.rs:163-204) of one key at m points, 8 lanes per point: `ppw` points per
+// workgroup of kBlock threads (every thread fills the LDS tables; the octets past ppw leave
+// after that).  The host spreads a small batch over the CUs (ppw = ceil(m / CUs)): 16 active
+// waves on one CU make each round LDS-throughput bound instead of latency bound.  ctr: the
+// workspace counter, whose block count (dcf_prg_last_eval_blocks) this engine zeroes (it
+// counts none).  cwb / s0 / xs / ys may be host-mapped.
+__global__ __launch_bounds__(kBlock, 1) void k_eval16_oct(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ cwb,
+    const uint8_t* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint32_t ppw, const uint64_t m, uint8_t* __restrict__ ys, uint32_t* __restrict__ ctr) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint4 key[2 * kColMaxLevels + kColMaxLevels / 16 + 2];  // cw_s | cw_v | cw_t | cw_np1
+  __shared__ uint8_t xsh[(kBlock / 8) * (kColMaxLevels / 8)];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint4*>(ctr) = make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t n = 8u * nbytes;
+  const uint64_t p0 = (uint64_t)blockIdx.x * ppw;
+  const uint32_t np = (uint32_t)min<uint64_t>(ppw, m - p0);
+  // stage the key (single-key CWB, include/dcf_hip.h: 16-byte multiple) and this group's x rows
+  const uint32_t np1_off = (2u * n * 16u + n + 15u) & ~15u;
+  const uint32_t kq = np1_off / 16u + 1u;
+  for (uint32_t i = threadIdx.x; i < kq; i += blockDim.x) key[i] = reinterpret_cast<const uint4*>(cwb)[i];
+  for (uint32_t i = threadIdx.x; i < np * nbytes; i += blockDim.x) xsh[i] = xs[p0 * nbytes + i];
+  lds_fill_tables_fast(lds, tab);
+  __syncthreads();
+  const uint32_t lc = lane_const();
+  const uint32_t oct = threadIdx.x >> 3, b = (threadIdx.x >> 2) & 1u, j = threadIdx.x & 3u;
+  if (oct >= np) return;  // whole octets (and whole quads) leave together: after the only barrier
+  uint32_t kw[15];
+  col_round_keys(rk, j, kw);
+  const uint32_t* kcs = reinterpret_cast<const uint32_t*>(key);             // cw_s[l] word j: kcs[4l + j]
+  const uint32_t* kcv = kcs + 4u * n;                                        // cw_v
+  const uint8_t* kct = reinterpret_cast<const uint8_t*>(key) + 32u * n;     // cw_t[l]
+  const uint32_t np1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(key) + np1_off)[j];
+  const uint8_t* x = xsh + oct * nbytes;
+  const uint32_t inv = 0u - b;                                      // quad 1 encrypts ~s (B)
+  const uint32_t msk = (j == 3u) ? kMaskLast : 0xFFFFFFFFu;         // clear bit 0 of byte 15 (prg.rs:65-68)
+  uint32_t s = reinterpret_cast<const uint32_t*>(s0)[j];            // k.s0s[0] (lib.rs:168)
+  uint32_t v = 0u, t = party, cur = 0u;
+  for (uint32_t lev = 0; lev < n; ++lev) {
+    if ((lev & 31u) == 0u) {  // next 32 bits of x, Msb0 (lib.rs:181)
+      const uint32_t c = lev >> 5;
+      uint32_t wv = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wv = (wv << 8) | (4u * c + k < nbytes ? (uint32_t)x[4u * c + k] : 0u);
+      cur = wv;
+    }
+    const uint32_t cs = kcs[4u * lev + j], cv = kcv[4u * lev + j], ct = kct[lev];
+    const uint32_t mine = aes256_col(s ^ inv, kw, lds, lc);
+    // The other quad's column j.  Both rotations run on every lane, then a bitwise select: a
+    // DPP move reads its source lane through EXEC, so it must not sit under a per-lane branch
+    // (the compiler turned `b ? dpp(4) : dpp(12)` into one — each side then read 0 from the
+    // other quad's disabled lanes).
+    uint32_t r4 = dpp<kRowRor4>(mine), r12 = dpp<kRowRor12>(mine);
+    asm volatile("" : "+v"(r4), "+v"(r12));
+    const uint32_t other = (r4 & inv) | (r12 & ~inv);
+    const uint32_t A = (other & inv) | (mine & ~inv), B = (mine & inv) | (other & ~inv);
+    const uint32_t xb = cur >> 31;
+    cur <<= 1;
+    const uint32_t keepA = xb - 1u, tm = 0u - t;
+    // t' = lsb(side)[0] ^ t & cw.t(side): column 0 holds byte 0 (lib.rs:179-180, 183/187)
+    const uint32_t tl = (A ^ s) & 1u, tr = (B ^ ~s) & 1u;
+    const uint32_t tn = dpp<kQpBcast0>((xb ? tr : tl) ^ (t & (ct >> xb) & 1u));
+    v ^= ((~s ^ (B & keepA)) & msk) ^ (tm & cv);   // v ^= v_hat(side) ^ t*cw.v   (lib.rs:182/186)
+    s = ((s ^ (A & keepA)) & msk) ^ (tm & cs);      // s' = s(side) ^ t*cw.s      (lib.rs:177-178)
+    t = tn;
+  }
+  if (b == 0u)  // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), column j of point p0 + oct
+    reinterpret_cast<uint32_t*>(ys)[(p0 + oct) * 4u + j] = v ^ s ^ ((0u - t) & np1);
+}
+
+// Dcf::gen (lib.rs:86-161) of num_keys keys, 16 lanes per key: `kpw` keys per workgroup of
+// kBlock threads (spread over the CUs as k_eval16_oct spreads points).  Inputs and the CWB
+// output may be host-mapped.
+__global__ __launch_bounds__(kBlock, 1) void k_gen16_col(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ alpha,
+    const uint8_t* __restrict__ beta, const uint8_t* __restrict__ s0_0, const uint8_t* __restrict__ s0_1,
+    const uint32_t bound, const uint32_t nbytes, const uint32_t kpw, const uint64_t num_keys,
+    uint8_t* __restrict__ cw_s, uint8_t* __restrict__ cw_v, uint8_t* __restrict__ cw_t, uint8_t* __restrict__ cw_np1) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint8_t ash[(kBlock / 16) * (kColMaxLevels / 8)];
+  const uint32_t n = 8u * nbytes;
+  const uint64_t k0 = (uint64_t)blockIdx.x * kpw;
+  const uint32_t nk = (uint32_t)min<uint64_t>(kpw, num_keys - k0);
+  for (uint32_t i = threadIdx.x; i < nk * nbytes; i += blockDim.x) ash[i] = alpha[k0 * nbytes + i];
+  lds_fill_tables_fast(lds, tab);
+  __syncthreads();
+  const uint32_t lc = lane_const();
+  const uint32_t kk = threadIdx.x >> 4, q = (threadIdx.x >> 2) & 3u, j = threadIdx.x & 3u;
+  if (kk >= nk) return;  // whole keys (whole DPP rows) leave together, after the only barrier
+  const uint64_t k = k0 + kk;
+  uint32_t kw[15];
+  col_round_keys(rk, j, kw);
+  const uint32_t msk = (j == 3u) ? kMaskLast : 0xFFFFFFFFu;
+  uint32_t s0w = reinterpret_cast<const uint32_t*>(s0_0)[k * 4u + j];   // s0s[0] (lib.rs:98)
+  uint32_t s1w = reinterpret_cast<const uint32_t*>(s0_1)[k * 4u + j];   // s0s[1]
+  const uint32_t be = reinterpret_cast<const uint32_t*>(beta)[k * 4u + j];
+  uint32_t va = 0u, t0 = 0u, t1 = 1u, cur = 0u;  // lib.rs:99-100
+  const uint8_t* al = ash + kk * nbytes;
+  const uint32_t inv = 0u - (q & 1u);                  // blocks 1 and 3 encrypt ~s
+  const uint32_t rot = q;                               // block q's source lane offsets below
+  for (uint32_t lev = 0; lev < n; ++lev) {
+    if ((lev & 31u) == 0u) {  // next 32 bits of alpha, Msb0 (lib.rs:106)
+      const uint32_t c = lev >> 5;
+      uint32_t wv = 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wv = (wv << 8) | (4u * c + e < nbytes ? (uint32_t)al[4u * c + e] : 0u);
+      cur = wv;
+    }
+    const uint32_t mine = aes256_col(((q >> 1) ? s1w : s0w) ^ inv, kw, lds, lc);
+    // column j of every block: row_ror:4n brings block (q - n) & 3
+    const uint32_t r4 = dpp<kRowRor4>(mine), r8 = dpp<kRowRor8>(mine), r12 = dpp<kRowRor12>(mine);
+    uint32_t X[4];
+#pragma unroll
+    for (uint32_t tb = 0; tb < 4; ++tb) {
+      const uint32_t d = (rot - tb) & 3u;  // block tb sits in the value rotated by 4d lanes
+      X[tb] = (d & 2u) ? ((d & 1u) ? r12 : r8) : ((d & 1u) ? r4 : mine);
+    }
+    const uint32_t A0 = X[0], B0 = X[1], A1 = X[2], B1 = X[3];
+    const uint32_t a = cur >> 31;  // alpha_i (lib.rs:106)
+    cur <<= 1;
+    const uint32_t am = 0u - a;
+    const uint32_t bm = (bound == 0u) ? am : ~am;  // LtBeta: beta joins v_cw when alpha_i = 1 (lib.rs:114-125)
+    // PRG outputs per party: L = ((A^s)&M, (B^~s)&M), R = (s&M, ~s&M)
+    const uint32_t sl0 = (A0 ^ s0w) & msk, vl0 = (B0 ^ ~s0w) & msk, sr0 = s0w & msk, vr0 = ~s0w & msk;
+    const uint32_t sl1 = (A1 ^ s1w) & msk, vl1 = (B1 ^ ~s1w) & msk, sr1 = s1w & msk, vr1 = ~s1w & msk;
+    const uint32_t scw = (a ? sl0 : sr0) ^ (a ? sl1 : sr1);                       // lib.rs:112
+    const uint32_t vcw = (a ? vl0 : vr0) ^ (a ? vl1 : vr1) ^ va ^ (bm & be);      // lib.rs:113-125
+    va ^= (a ? vr0 : vl0) ^ (a ? vr1 : vl1) ^ vcw;                                 // lib.rs:126-129
+    // t bits from byte 0 (column 0 lanes), broadcast to the quad
+    const uint32_t tl0 = (A0 ^ s0w) & 1u, tr0 = (B0 ^ ~s0w) & 1u, tl1 = (A1 ^ s1w) & 1u, tr1 = (B1 ^ ~s1w) & 1u;
+    const uint32_t tlcw = tl0 ^ tl1 ^ a ^ 1u, trcw = tr0 ^ tr1 ^ a;  // lib.rs:130-131
+    const uint32_t tkcw = a ? trcw : tlcw;
+    const uint32_t nt0 = (a ? tr0 : tl0) ^ (t0 & tkcw), nt1 = (a ? tr1 : tl1) ^ (t1 & tkcw);  // lib.rs:149-152
+    const uint32_t tp = dpp<kQpBcast0>(tlcw | (trcw << 1) | (nt0 << 2) | (nt1 << 3));
+    const uint32_t m0 = 0u - t0, m1 = 0u - t1;
+    s0w = (a ? sr0 : sl0) ^ (m0 & scw);  // lib.rs:139-148
+    s1w = (a ? sr1 : sl1) ^ (m1 & scw);
+    t0 = (tp >> 2) & 1u;
+    t1 = (tp >> 3) & 1u;
+    const uint64_t ci = (uint64_t)lev * num_keys + k;
+    if (q == 0u) reinterpret_cast<uint32_t*>(cw_s)[ci * 4u + j] = scw;
+    if (q == 1u) reinterpret_cast<uint32_t*>(cw_v)[ci * 4u + j] = vcw;
+    if (q == 2u && j == 0u) cw_t[ci] = (uint8_t)(tp & 3u);
+  }
+  if (q == 0u) reinterpret_cast<uint32_t*>(cw_np1)[k * 4u + j] = s0w ^ s1w ^ va;  // lib.rs:155
+}
+
+}  // namespace

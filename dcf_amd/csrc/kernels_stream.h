@@ -109,7 +109,11 @@ struct StreamLane {
   uint32_t xw[NS][4];             // XREG: queue of the point's next x words, as loaded (byte-swapped on use)
   bool fresh[NS];                 // XREG: take cur from the queue head xw[0] before the next update
   const uint8_t* xp[NS];          // !XREG: the point's row in xs
-  uint64_t ci[NS], pt[NS], key[NS];
+  // MULTI: key-major digest row key * 8N + level (< 2^32: the host launches at most 2^24 keys
+  // at a time); pt: the point's index in this launch (< 2^32: the host cuts larger batches).
+  // The key itself is pt / points_per_key, needed once per point (its cw_np1), so it holds
+  // no registers during the walk (r03: the C5 multi-key instance spilled at 128 VGPRs).
+  uint32_t ci[NS], pt[NS];
   bool alive[NS];
 };
 
@@ -133,7 +137,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
                                              const uint8_t* __restrict__ xs, uint32_t nbytes_rt, uint64_t ppk,
                                              const PrefixTable& pf) {
   const uint32_t nbytes = NBC ? (uint32_t)NBC : nbytes_rt;  // NBC: x width fixed at compile time
-  const uint64_t k = MULTI ? p / ppk : 0;
+  const uint32_t k = MULTI ? (uint32_t)p / (uint32_t)ppk : 0u;
   const uint8_t* row = xs + p * nbytes;
   uint32_t w0;  // first 32 x bits, Msb0 (lib.rs:181)
   if (XREG) {
@@ -148,7 +152,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
     lev0 = pf.levels;      // (MULTI: the key's own top tree, k_mk_prefix16, rows k * 2^levels + ...)
     uint4 sv, vv;
     const uint32_t top = w0 >> (32u - lev0);
-    prefix_row(pf, MULTI ? (uint32_t)((k << lev0) + top) : top, sv, vv, L.t[i]);
+    prefix_row(pf, MULTI ? (k << lev0) + top : top, sv, vv, L.t[i]);
     L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
     L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
   } else {
@@ -160,9 +164,8 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
   }
   L.ph[i] = 0u;
   L.lev[i] = lev0;
-  L.ci[i] = k * (8u * nbytes) + lev0;  // key-major digest row (MULTI); the level of the single key otherwise
-  L.key[i] = k;
-  L.pt[i] = p;
+  L.ci[i] = (uint32_t)k * (8u * nbytes) + lev0;  // key-major digest row (MULTI); the level of the single key otherwise
+  L.pt[i] = (uint32_t)p;
   L.alive[i] = true;
   if (XREG) {
     if (PFX || lev0) {  // word 0 is consumed here, shifted past the prefix bits
@@ -180,9 +183,9 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
 // Give every lane whose stream i is free (`mine`) a new point, or retire the
 // stream when the counter is exhausted.  Called in wave-uniform control flow.
 template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit, bool PFX = false, int NBC = 0>
-__device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint64_t& unext,
-                                              uint64_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
-                                              uint64_t nunits, uint64_t total, const uint4* __restrict__ s0s,
+__device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint32_t& unext,
+                                              uint32_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
+                                              uint32_t nunits, uint32_t total, const uint4* __restrict__ s0s,
                                               const uint4 s0v, uint32_t party, const uint8_t* __restrict__ xs,
                                               uint32_t nbytes, uint64_t ppk, const PrefixTable& pf) {
   // The loop only hands out point indices; the stream state is written once after it
@@ -191,7 +194,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
   // (single key, x width fixed: the multi-key and runtime-width instances spill VGPRs with it)
   constexpr bool ONCE = DCF_REFILL_ONCE && !MULTI && NBC != 0;
   if (ONCE) {
-    uint64_t pnew = 0;
+    uint32_t pnew = 0;
     bool got = false;
     while (need) {
       if (unext >= uend && !exhausted) {
@@ -199,17 +202,17 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
         if (u >= nunits) {
           exhausted = true;
         } else {
-          unext = (uint64_t)u * UNIT;
-          uend = min(unext + (uint64_t)UNIT, total);
+          unext = u * UNIT;
+          uend = min(unext + UNIT, total);
         }
       }
       if (exhausted && unext >= uend) break;
       const uint32_t rank = lane_rank(need);
-      const bool take = mine && (uint64_t)rank < uend - unext;
+      const bool take = mine && rank < uend - unext;
       pnew = take ? unext + rank : pnew;
       got = got || take;
       const uint64_t taken = __ballot(take);
-      unext += (uint64_t)__popcll(taken);
+      unext += (uint32_t)__popcll(taken);
       need &= ~taken;
       mine = mine && !take;
     }
@@ -228,8 +231,8 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
       if (u >= nunits) {
         exhausted = true;
       } else {
-        unext = (uint64_t)u * UNIT;
-        uend = min(unext + (uint64_t)UNIT, total);
+        unext = u * UNIT;
+        uend = min(unext + UNIT, total);
       }
     }
     if (exhausted && unext >= uend) {
@@ -241,10 +244,10 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
       return;
     }
     const uint32_t rank = lane_rank(need);
-    const bool take = mine && (uint64_t)rank < uend - unext;
+    const bool take = mine && rank < uend - unext;
     if (take) stream_start<NS, XREG, MULTI, PFX, NBC>(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk, pf);
     const uint64_t taken = __ballot(take);
-    unext += (uint64_t)__popcll(taken);
+    unext += (uint32_t)__popcll(taken);
     need &= ~taken;
     mine = mine && !take;
   }
@@ -254,9 +257,9 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
 // retire the stream when the counter is exhausted.  Called in wave-uniform control flow;
 // issues no memory access but the work-counter atomic (the stream is started by the caller).
 template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit>
-__device__ __forceinline__ void stream_claim(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint64_t& unext,
-                                             uint64_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
-                                             uint64_t nunits, uint64_t total, uint64_t& pnew, bool& got) {
+__device__ __forceinline__ void stream_claim(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint32_t& unext,
+                                             uint32_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
+                                             uint32_t nunits, uint32_t total, uint32_t& pnew, bool& got) {
   uint64_t need = __ballot(mine);
   while (need) {
     if (unext >= uend && !exhausted) {
@@ -264,17 +267,17 @@ __device__ __forceinline__ void stream_claim(StreamLane<NS, XREG, MULTI>& L, int
       if (u >= nunits) {
         exhausted = true;
       } else {
-        unext = (uint64_t)u * UNIT;
-        uend = min(unext + (uint64_t)UNIT, total);
+        unext = u * UNIT;
+        uend = min(unext + UNIT, total);
       }
     }
     if (exhausted && unext >= uend) break;
     const uint32_t rank = lane_rank(need);
-    const bool take = mine && (uint64_t)rank < uend - unext;
+    const bool take = mine && rank < uend - unext;
     pnew = take ? unext + rank : pnew;
     got = got || take;
     const uint64_t taken = __ballot(take);
-    unext += (uint64_t)__popcll(taken);
+    unext += (uint32_t)__popcll(taken);
     need &= ~taken;
     mine = mine && !take;
   }
@@ -356,8 +359,10 @@ __device__ __forceinline__ void stream_run(
   const uint32_t nlev = 8u * nbytes;
   // batched refill (single key, x width fixed, x words queued in registers)
   constexpr bool BATCH = DCF_REFILL_BATCH && DCF_REFILL_ONCE && XREG && !MULTI && NBC != 0 && !DCF_STREAM_LATE_STORE;
-  const uint64_t nunits = (total + UNIT - 1) / UNIT;
-  uint64_t unext = 0, uend = 0;
+  // one launch covers < 2^32 points (the host cuts larger batches): 32-bit work distribution
+  const uint32_t total32 = (uint32_t)total;
+  const uint32_t nunits = (uint32_t)((total + UNIT - 1) / UNIT);
+  uint32_t unext = 0, uend = 0;
   bool exhausted = false;
   const uint4 s0v = s0s[0];
   StreamLane<NS, XREG, MULTI> L;
@@ -372,8 +377,8 @@ __device__ __forceinline__ void stream_run(
   const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, true, unext, uend, exhausted, ctr, nunits, total, s0s, s0v,
-                                              party, xs, nbytes, ppk, pf);
+    stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, true, unext, uend, exhausted, ctr, nunits, total32, s0s,
+                                                  s0v, party, xs, nbytes, ppk, pf);
 
   uint64_t nblk = 0;  // AES blocks this wave encrypts for live streams (wave-uniform)
   for (;;) {
@@ -394,7 +399,7 @@ __device__ __forceinline__ void stream_run(
     for (int i = 0; i < NS; ++i) {
       // CW row: the key-major digest row (MULTI); for one key the row is the level itself (a
       // 32-bit index: ci only mirrors lev there, and a retired stream's lev is reset to 0)
-      const uint64_t cwi = MULTI ? L.ci[i] : (uint64_t)L.lev[i];
+      const uint32_t cwi = MULTI ? L.ci[i] : L.lev[i];
       const uint4* row = cw_s + 3 * cwi;  // D48: level rows cs | cv | (ct, 0, 0, 0), plus a zero row 8N
       if (D48) {
         cs[i] = row[0];
@@ -418,7 +423,7 @@ __device__ __forceinline__ void stream_run(
 #endif
       // Loaded unconditionally (L1-resident): loads under a divergent branch made the
       // compiler wait for them before the AES.
-      const uint64_t c2 = cwi + (L.lev[i] + 1u < nlev ? 1u : 0u);
+      const uint32_t c2 = cwi + (L.lev[i] + 1u < nlev ? 1u : 0u);
       if (D48) {  // the next row (row 8N is zeros: no clamp needed)
         cs2[i] = row[3];
         cv2[i] = row[4];
@@ -600,9 +605,9 @@ __device__ __forceinline__ void stream_run(
         const bool dn = L.alive[i] && L.lev[i] == nlev;
         if (!__ballot(dn)) continue;
         bool got = false;
-        uint64_t pnew = 0;
-        stream_claim<NS, XREG, MULTI, UNIT>(L, i, dn, unext, uend, exhausted, ctr, nunits, total, pnew, got);
-        if (got) stream_load_x(L, i, xs + pnew * nbytes, nbytes);
+        uint32_t pnew = 0;
+        stream_claim<NS, XREG, MULTI, UNIT>(L, i, dn, unext, uend, exhausted, ctr, nunits, total32, pnew, got);
+        if (got) stream_load_x(L, i, xs + (uint64_t)pnew * nbytes, nbytes);
         DCF_BATCH_FENCE;
         if (dn) {
           const uint32_t tm = 0u - L.t[i];
@@ -620,9 +625,9 @@ __device__ __forceinline__ void stream_run(
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
       uint4 yv = make_uint4(0u, 0u, 0u, 0u);
-      uint64_t yp = 0;
+      uint32_t yp = 0;
       if (done) {
-        const uint4 np = MULTI ? cw_np1[L.key[i]] : np1v;
+        const uint4 np = MULTI ? cw_np1[L.pt[i] / (uint32_t)ppk] : np1v;
         const uint32_t tm = 0u - L.t[i];
         yv = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
                         L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
@@ -630,7 +635,7 @@ __device__ __forceinline__ void stream_run(
         if (!DCF_STREAM_LATE_STORE) ys[yp] = yv;
       }
       if (__ballot(done))
-        stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total, s0s,
+        stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total32, s0s,
                                                   s0v, party, xs, nbytes, ppk, pf);
       if (DCF_STREAM_LATE_STORE && done) {
         asm volatile("" ::: "memory");  // keep the store below the refill's loads
@@ -672,9 +677,11 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   constexpr int HK = (MULTI && !TT2) ? DCF_MK_HK : 0;
   constexpr int SL = (MULTI && !TT2) ? DCF_MK_SL : -1;
   constexpr int SK = (MULTI && !TT2) ? DCF_MK_SK : 0;
+  DCF_CLK(2, 0);
   stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC, SK>(
       lds, (GK || HK || SK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total,
       ctr, ys, pf);
+  DCF_CLK(2, 1);
 }
 
 }  // namespace

@@ -497,6 +497,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
     }
   }
   __syncthreads();
+  DCF_CLK(0, 0);
   const uint32_t q = threadIdx.x % LP;
   const uint32_t pi = (threadIdx.x >> 3) & 1u;   // the point's half of a 16-lane LDS pass
   const uint32_t off = byte0 + 16 * q;
@@ -596,6 +597,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
     load_t(ta, p + 4 * pstep);
     load_t(tb, p + 5 * pstep);
   }
+  DCF_CLK(0, 1);
 }
 
 // ------------------------------------------------------------------------

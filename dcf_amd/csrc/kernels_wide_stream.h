@@ -176,6 +176,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   __shared__ uint4 rks[23 + 15];
   if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
   lds_fill_tables(lds, tab);  // its barrier also publishes rks
+  DCF_CLK(1, 0);
   const uint32_t rks_a = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)rks;  // LDS byte address
   const __amdgpu_buffer_rsrc_t rkrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(rk2), (short)0, 480, 0x00020000);
   const uint32_t lc = lane_const();
@@ -379,6 +380,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks), accumulated over passes
   if ((threadIdx.x & 63u) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, (unsigned long long)nblk);
+  DCF_CLK(1, 1);
 }
 
 // One wide prefix node (80 B: s[0:32) | v[0:32) | {t, t-vector word 0, partial word, 0})

@@ -215,6 +215,24 @@ class Aes256HirosePrg:
         check(_lib.load().dcf_prg_last_eval_blocks(self._h, ctypes.byref(n)))
         return int(n.value)
 
+    def host_pinned_bytes(self) -> int:
+        """Pinned host memory this prg holds for the host-pointer entry points."""
+        return int(_lib.load().dcf_prg_host_pinned_bytes(self._h))
+
+    def workspaces(self) -> int:
+        """Workspaces in the prg's pool (the most calls that were in flight at once)."""
+        return int(_lib.load().dcf_prg_workspaces(self._h))
+
+    def set_phase_timing(self, on: bool) -> None:
+        """Record HIP events around every eval's preparation and walk (measurement hook)."""
+        check(_lib.load().dcf_prg_set_phase_timing(self._h, int(bool(on))))
+
+    def last_eval_phases(self):
+        """(prep_ms, walk_ms, prefix_levels) of the last timed eval; sync its stream first."""
+        a, b, d = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+        check(_lib.load().dcf_prg_last_eval_phases(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(d)))
+        return float(a.value), float(b.value), int(d.value)
+
     def gen(self, seed: bytes):
         """`Prg::gen` (lib.rs:52-54) for one seed — the GPU PRG kernel, not a CPU path."""
         return self.gen_many([seed])[0]

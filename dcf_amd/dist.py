@@ -8,11 +8,12 @@ data path.  The only exchanges are:
   * broadcast of the key material (correction-word block + seeds) from the rank
     that ran gen, once, before evaluation;
   * an optional gather of output shares onto one rank when the caller needs
-    them on one device.
+    them on one device (the reference writes every output into the caller's
+    `ys`, lib.rs:163,196-198).
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -48,12 +49,39 @@ def broadcast_key(tensors: List[torch.Tensor], src: int = 0) -> List[torch.Tenso
     return tensors
 
 
-def gather_shares(ys: torch.Tensor, dst: int = 0) -> Optional[torch.Tensor]:
-    """Gather every rank's equally-sized output slice onto `dst` (rank order =
-    global point order).  Returns the concatenation on dst, None elsewhere."""
+def _host_collectives(t: torch.Tensor) -> bool:
+    """gloo's gather / all_gather of row counts take host tensors only."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def gather_shares(ys: torch.Tensor, dst: int = 0, counts: Optional[Sequence[int]] = None) -> Optional[torch.Tensor]:
+    """Gather every rank's output slice onto `dst` in rank order (= global point order
+    for the contiguous slices of point_slice / weak_slice).  Slices may differ in length
+    (point_slice gives the first total % world ranks one extra point): the row counts are
+    all-gathered (or taken from `counts`), every slice is padded to the longest for the
+    collective, and dst trims the padding.  Returns the concatenation (on ys's device)
+    on dst, None elsewhere."""
     ws, rank = world()
     if ws == 1:
         return ys
-    parts = [torch.empty_like(ys) for _ in range(ws)] if rank == dst else None
-    dist.gather(ys, gather_list=parts, dst=dst)
-    return torch.cat(parts, 0) if rank == dst else None
+    dev = ys.device
+    host = _host_collectives(ys)
+    if counts is None:
+        n = torch.tensor([ys.shape[0]], dtype=torch.int64, device="cpu" if host else dev)
+        got = [torch.zeros_like(n) for _ in range(ws)]
+        dist.all_gather(got, n)
+        counts = [int(c.item()) for c in got]
+    counts = [int(c) for c in counts]
+    if len(counts) != ws or counts[rank] != ys.shape[0]:
+        raise ValueError(f"counts {counts} do not match this rank's {ys.shape[0]} rows")
+    rows = max(counts)
+    src = ys.cpu() if host else ys
+    if src.shape[0] < rows:  # pad to the longest slice (the collective needs equal shapes)
+        pad = torch.zeros((rows,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        pad[:src.shape[0]] = src
+        src = pad
+    parts = [torch.empty_like(src) for _ in range(ws)] if rank == dst else None
+    dist.gather(src.contiguous(), gather_list=parts, dst=dst)
+    if rank != dst:
+        return None
+    return torch.cat([p[:c] for p, c in zip(parts, counts)], 0).to(dev)

@@ -43,12 +43,20 @@
  * kernels of neighbouring chunks, and they wait for those streams only (never
  * the whole device).  The GPU never reads or writes caller host memory.
  *
- * Threading: one dcf_prg may be used by one host thread at a time, and its
- * device calls must not overlap on different streams (its work counter and
- * scratch buffers are per dcf_prg; calls queued on one stream are fine);
- * distinct dcf_prg objects are independent.  Multi-GPU: one dcf_prg per device
- * (all built from the same keys) and dcf_eval_multi_gpu / _device below, or one
- * process per device; the path shards by points/keys with no collective.
+ * Threading (the reference's `Dcf::eval(&self, ...)` over a `Prg: Sync`, lib.rs:34,52):
+ * every compute entry point may be called on ONE dcf_prg from any number of host
+ * threads at once, and its device calls may be queued on different streams at once.
+ * Each call leases a workspace (work counter, scratch, shared-prefix table, host
+ * streams and staging) from a pool on the prg, so concurrent calls share no mutable
+ * buffer; a workspace re-used on another stream first waits (on the device, with an
+ * event) for the device work of its previous call, so a host call queued after a
+ * *_device call on the same prg is ordered after it without any synchronization by the
+ * caller.  The pool grows to the number of calls in flight at once and is freed with
+ * the prg (dcf_prg_workspaces, dcf_prg_device_bytes, dcf_prg_host_pinned_bytes report
+ * it).  The setters (dcf_prg_set_*) may race calls: a call reads each setting once.
+ * Multi-GPU: one dcf_prg per device (all built from the same keys) and
+ * dcf_eval_multi_gpu / _device below, or one process per device; the path shards by
+ * points/keys with no collective.
  */
 #ifndef DCF_HIP_H
 #define DCF_HIP_H
@@ -144,8 +152,15 @@ int dcf_eval_prefix_levels(const dcf_prg* prg, size_t n_bytes, size_t num_keys, 
  * until they fit, and no table is built below depth 8.  0 = no cap (the default: up to
  * ~4.4 GB at depth 26, LAMBDA = 16).  Forced depths ignore it.  Output bytes never change. */
 int dcf_prg_set_prefix_max_bytes(dcf_prg* prg, size_t max_bytes);
-/* Device memory this dcf_prg currently holds (tables, prefix table, scratch, staging). */
+/* Device memory this dcf_prg currently holds (tables, prefix tables, scratch, staging, over
+ * all of its workspaces). */
 size_t dcf_prg_device_bytes(const dcf_prg* prg);
+/* Pinned host memory this dcf_prg holds for the host-pointer entry points (per workspace: up
+ * to two 128 MiB x + y chunks of the eval pipeline, sized to the largest call, plus a 1 MiB
+ * mapped buffer for tiny calls), kept until dcf_prg_free. */
+size_t dcf_prg_host_pinned_bytes(const dcf_prg* prg);
+/* Number of workspaces in the prg's pool (the most calls that were in flight at once). */
+int dcf_prg_workspaces(const dcf_prg* prg);
 
 /* Hybrid engine tuning (results are identical for every setting):
  *   slab_variant 1: 16-wave workgroups, bitsliced s/v state in a scratch slab;
@@ -161,13 +176,23 @@ int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves, int slab_variant);
  *   priority:         1 = stream waves issue at raised priority (s_setprio). */
 int dcf_prg_set_stream_hybrid(dcf_prg* prg, unsigned ttable_wave_mask, int priority);
 
-/* AES blocks the last stream-engine eval on this prg encrypted for live points (LAMBDA = 16:
- * DCF_EVAL_STREAM / _STREAM_HYBRID's stream waves; LAMBDA >= 32: the stream head over all of
- * the call's passes; not counting a shared-prefix table build, except the multi-key
- * per-key top trees, whose blocks are included), counted on the device.
+/* AES blocks the last eval call on this prg (the last one to return, from any thread)
+ * encrypted for live points (LAMBDA = 16: DCF_EVAL_STREAM / _STREAM_HYBRID's stream waves;
+ * LAMBDA >= 32: the stream head over all of the call's keys and passes; not counting a
+ * shared-prefix table build, except the multi-key per-key top trees, whose blocks are
+ * included), counted on the device; 0 for engines that do not count.
  * Measurement hook for the bench; call after the eval's stream has been synchronized.  0
- * before any such eval. */
+ * before any eval. */
 int dcf_prg_last_eval_blocks(dcf_prg* prg, uint64_t* blocks);
+
+/* Phase timing of eval calls (measurement hook, off by default).  When on, every eval call
+ * records HIP events on its stream at entry, before its walk kernel(s) (after any shared-
+ * prefix table, per-key top trees or CW digest/rows were built) and at the end.
+ * dcf_prg_last_eval_phases reads the last eval call's split (call after synchronizing its
+ * stream): prep_ms = table / digest preparation, walk_ms = the walk kernels, prefix_levels =
+ * the shared-prefix depth it used (0 = none).  DCF_ERR_ARG if no timed eval has run. */
+int dcf_prg_set_phase_timing(dcf_prg* prg, int on);
+int dcf_prg_last_eval_phases(dcf_prg* prg, float* prep_ms, float* walk_ms, int* prefix_levels);
 
 /* CWB layout helpers (see above). */
 size_t dcf_cwb_bytes(size_t n_bytes, size_t lambda, size_t num_keys);

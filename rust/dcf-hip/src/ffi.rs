@@ -33,9 +33,14 @@ extern "C" {
     pub fn dcf_eval_prefix_levels(prg: *const DcfPrg, n_bytes: usize, num_keys: usize, points_per_key: usize) -> c_int;
     pub fn dcf_prg_set_prefix_max_bytes(prg: *mut DcfPrg, max_bytes: usize) -> c_int;
     pub fn dcf_prg_device_bytes(prg: *const DcfPrg) -> usize;
+    pub fn dcf_prg_host_pinned_bytes(prg: *const DcfPrg) -> usize;
+    pub fn dcf_prg_workspaces(prg: *const DcfPrg) -> c_int;
     pub fn dcf_prg_set_hybrid_split(prg: *mut DcfPrg, ttable_waves: c_int, slab_variant: c_int) -> c_int;
     pub fn dcf_prg_set_stream_hybrid(prg: *mut DcfPrg, ttable_wave_mask: c_uint, priority: c_int) -> c_int;
     pub fn dcf_prg_last_eval_blocks(prg: *mut DcfPrg, blocks: *mut u64) -> c_int;
+    pub fn dcf_prg_set_phase_timing(prg: *mut DcfPrg, on: c_int) -> c_int;
+    pub fn dcf_prg_last_eval_phases(prg: *mut DcfPrg, prep_ms: *mut f32, walk_ms: *mut f32,
+                                    prefix_levels: *mut c_int) -> c_int;
     pub fn dcf_cwb_bytes(n_bytes: usize, lambda: usize, num_keys: usize) -> usize;
     pub fn dcf_cwb_np1_offset(n_bytes: usize, lambda: usize, num_keys: usize) -> usize;
     pub fn dcf_gen(prg: *mut DcfPrg, n_bytes: usize, alpha: *const u8, beta: *const u8, s0_0: *const u8,

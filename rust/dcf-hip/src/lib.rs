@@ -76,6 +76,10 @@ pub struct DcfHip<const N: usize, const LAMBDA: usize> {
 }
 
 unsafe impl<const N: usize, const LAMBDA: usize> Send for DcfHip<N, LAMBDA> {}
+// One dcf_prg may be driven from many threads at once (include/dcf_hip.h "Threading": every
+// call leases its own workspace from the prg's pool), as `DcfImpl` is with a `Sync` PRG
+// (lib.rs:34,52): an `Arc<DcfHip>` can be shared across rayon or std threads unchanged.
+unsafe impl<const N: usize, const LAMBDA: usize> Sync for DcfHip<N, LAMBDA> {}
 
 impl<const N: usize, const LAMBDA: usize> DcfHip<N, LAMBDA> {
     /// `Aes256HirosePrg::<LAMBDA, CIPHER_N>::new(keys)` (prg.rs:27-33) on `device`.
@@ -139,7 +143,9 @@ impl<const N: usize, const LAMBDA: usize> Dcf<N, LAMBDA> for DcfHip<N, LAMBDA> {
     }
 
     fn eval(&self, b: bool, k: &Share<LAMBDA>, xs: &[&[u8; N]], ys: &mut [&mut [u8; LAMBDA]]) {
-        self.try_eval(b, k, xs, ys).unwrap_or_else(|e| panic!("dcf_eval: {e:?}"))
+        // the crate zips xs with ys (lib.rs:196-198): min(len) points, extra ys rows untouched
+        let m = xs.len().min(ys.len());
+        self.try_eval(b, k, &xs[..m], &mut ys[..m]).unwrap_or_else(|e| panic!("dcf_eval: {e:?}"))
     }
 }
 
@@ -169,7 +175,9 @@ impl<const N: usize, const LAMBDA: usize> Dcf<N, LAMBDA> for DcfHipMulti<N, LAMB
     }
 
     fn eval(&self, b: bool, k: &Share<LAMBDA>, xs: &[&[u8; N]], ys: &mut [&mut [u8; LAMBDA]]) {
-        assert_eq!(xs.len(), ys.len()); // the crate zips (lib.rs:196); the ABI rejects a mismatch
+        // the crate zips xs with ys (lib.rs:196-198): min(len) points, extra ys rows untouched
+        let m = xs.len().min(ys.len());
+        let (xs, ys) = (&xs[..m], &mut ys[..m]);
         let cwb = share_to_cwb::<N, LAMBDA>(k);
         let prgs: Vec<*mut ffi::DcfPrg> = self.devs.iter().map(|d| d.raw()).collect();
         let xb: Vec<u8> = xs.iter().flat_map(|x| x.iter().copied()).collect();

@@ -83,3 +83,42 @@ fn test_bit_exact_with_the_crate_cpu_impl() {
         assert_eq!(yc, ym);
     }
 }
+
+/// `DcfImpl` is `Sync` with a `Sync` PRG (lib.rs:34,52): callers share one instance across
+/// threads.  One `DcfHip` driven from 8 threads at once, each with its own key and points,
+/// must match the crate's CPU `DcfImpl` bit for bit; and a `ys` longer than `xs` is zipped
+/// (lib.rs:196-198): the extra rows stay untouched.
+#[test]
+fn test_one_instance_many_threads_and_zip_semantics() {
+    use std::sync::Arc;
+    let cpu = Arc::new(DcfImpl::<16, 16, _>::new(Aes256HirosePrg::<16, 2>::new(KEYS)));
+    let gpu = Arc::new(DcfHip::<16, 16>::new(KEYS, 0));
+    let handles: Vec<_> = (0..8)
+        .map(|i| {
+            let (cpu, gpu) = (Arc::clone(&cpu), Arc::clone(&gpu));
+            std::thread::spawn(move || {
+                let s0s: [[u8; 16]; 2] = thread_rng().gen();
+                let f = CmpFn { alpha: thread_rng().gen(), beta: thread_rng().gen() };
+                let k = gpu.gen(&f, [&s0s[0], &s0s[1]], BoundState::LtBeta);
+                let xs: Vec<[u8; 16]> = (0..[1, 7, 5000, 300_000][i % 4]).map(|_| thread_rng().gen()).collect();
+                let xr: Vec<&[u8; 16]> = xs.iter().collect();
+                let kb = Share { s0s: vec![k.s0s[0]], cws: k.cws.clone(), cw_np1: k.cw_np1 };
+                let mut yc = vec![[0; 16]; xs.len()];
+                let mut yg = vec![[0; 16]; xs.len()];
+                cpu.eval(false, &kb, &xr, &mut yc.iter_mut().collect::<Vec<_>>());
+                gpu.eval(false, &kb, &xr, &mut yg.iter_mut().collect::<Vec<_>>());
+                assert_eq!(yc, yg);
+            })
+        })
+        .collect();
+    for h in handles {
+        h.join().unwrap();
+    }
+    let s0s: [[u8; 16]; 2] = thread_rng().gen();
+    let f = CmpFn { alpha: thread_rng().gen(), beta: thread_rng().gen() };
+    let k = gpu.gen(&f, [&s0s[0], &s0s[1]], BoundState::GtBeta);
+    let kb = Share { s0s: vec![k.s0s[0]], cws: k.cws.clone(), cw_np1: k.cw_np1 };
+    let mut ys = vec![[0xAB; 16]; ALPHAS.len() + 2];
+    gpu.eval(false, &kb, ALPHAS, &mut ys.iter_mut().collect::<Vec<_>>());
+    assert_eq!(&ys[ALPHAS.len()..], &[[0xAB; 16]; 2]);
+}

@@ -36,3 +36,11 @@ def test_bench_two_ranks_strong_scaling_check():
     assert d["config"]["points_per_gpu"] in ((1 << 21) + 1, (1 << 21) + 2)
     assert d["value"] > 0
     assert d["slice_check"]["slices_match"], d["slice_check"]
+    # the N > 1 line explains a scaling curve: per-rank kernel / wall / table-build times
+    pr = d["per_rank"]
+    assert [r["rank"] for r in pr["ranks"]] == [0, 1]
+    assert sum(r["points"] for r in pr["ranks"]) == (1 << 22) + 3
+    for r in pr["ranks"]:
+        assert r["kernel_ms"] > 0 and r["walk_ms"] > 0 and r["table_ms"] >= 0 and r["prefix_levels"] == 21
+    assert pr["imbalance"] >= 1.0
+    assert d["key_broadcast"]["ms"] is not None and d["key_broadcast"]["bytes"] > 0

@@ -31,13 +31,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, ws, port, out_path):
+def _worker(rank, ws, port, out_path, total, pass_counts):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     from oracle import oracle as O
     keys = [bytes([7]) * 32, bytes([9]) * 32]
     P = O.OraclePrg(keys, 16)
-    nb, lam, total = 4, 16, 203
+    nb, lam = 4, 16
     n = 8 * nb
     cwb = torch.zeros(2 * n * lam + n + lam, dtype=torch.uint8)
     seeds = torch.zeros((2, lam), dtype=torch.uint8)
@@ -55,10 +55,11 @@ def _worker(rank, ws, port, out_path):
     k.cw_v[:] = c[n * lam:2 * n * lam].reshape(n, lam)
     k.cw_t[:] = c[2 * n * lam:2 * n * lam + n]
     k.cw_np1[:] = c[2 * n * lam + n:]
-    xs_all = np.random.default_rng(11).integers(0, 256, (total + 1, nb), dtype=np.uint8)  # +1: pad to even
-    start, cnt = point_slice(total + 1, ws, rank)
-    ys = O.eval_(P, 0, k, seeds[0].numpy().tobytes(), xs_all[start:start + cnt])
-    full = gather_shares(torch.from_numpy(ys))
+    xs_all = np.random.default_rng(11).integers(0, 256, (total, nb), dtype=np.uint8)
+    start, cnt = point_slice(total, ws, rank)  # uneven when total % ws != 0
+    ys = O.eval_(P, 0, k, seeds[0].numpy().tobytes(), xs_all[start:start + cnt]).reshape(cnt, lam)
+    counts = [point_slice(total, ws, r)[1] for r in range(ws)] if pass_counts else None
+    full = gather_shares(torch.from_numpy(ys), counts=counts)
     if rank == 0:
         ref = O.eval_(P, 0, k, seeds[0].numpy().tobytes(), xs_all)
         np.save(out_path, np.stack([full.numpy(), ref]))
@@ -66,8 +67,11 @@ def _worker(rank, ws, port, out_path):
     dist.destroy_process_group()
 
 
-def test_two_rank_bcast_shard_gather(tmp_path):
+@pytest.mark.parametrize("ws,total,pass_counts", [(2, 203, False), (2, 1, False), (3, 101, True)])
+def test_bcast_shard_gather_uneven(tmp_path, ws, total, pass_counts):
+    """Odd totals: the slices differ in length (and one is empty at total = 1); the gather
+    pads and trims, so the concatenation equals one process's eval of every point."""
     out = str(tmp_path / "res.npy")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(ws, _free_port(), out, total, pass_counts), nprocs=ws, join=True)
     full, ref = np.load(out)
     assert np.array_equal(full, ref)

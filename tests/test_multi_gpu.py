@@ -1,9 +1,11 @@
 """Host-pointer pipeline and the multi-GPU C ABI (dcf_eval_multi_gpu[_device]).
 
 On the 1-GPU box, G "devices" are G distinct dcf_prg objects on device 0 (each with
-its own streams, staging and work counter): slice placement, per-slice key copies,
-the threads of the host variant and the gather are exercised exactly as on 8 GPUs;
-only the peer copy degenerates to a device-local one.  Every result must be
+its own workspaces: streams, staging and work counter): slice placement, per-slice key
+copies, the threads of the host variant and the gather are exercised exactly as on 8
+GPUs; only the peer copy degenerates to a device-local one — the cross-device branch of
+dcf_eval_multi_gpu_device (hipDeviceEnablePeerAccess + hipMemcpyPeerAsync over xGMI) is
+NOT executed on this box and is untested here.  Every result must be
 byte-identical to dcf_eval_device over the whole batch (the reference
 splits Dcf::eval over host cores inside one call, lib.rs:194-199).
 """
