@@ -1352,9 +1352,14 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     // single key, x in registers: N = 16 (C1 / C3) and N = 4 (C2) with the x width fixed at
     // compile time (a point's start loads x without width branches: C2 starts a point every
     // ~13 AES slots)
+#ifndef DCF_MK_PFXT
+#define DCF_MK_PFXT 1  // multi-key: a kernel instance for "per-key top trees present" (no root-seed start path:
+                       // 48 -> 33 SGPR spills; C5 r03c A/B, same box, 2 runs: 414.6 / 413.7 vs 408.5 / 408.1 M evals/s)
+#endif
 #define DCF_STREAM(XR, MK)                                                                                    \
   do {                                                                                                        \
-    if (MK) DCF_STREAM_K(XR, MK, false, false);                                                               \
+    if (MK && DCF_MK_PFXT && lpf.levels) DCF_STREAM_K(XR, MK, true, false);                                   \
+    else if (MK) DCF_STREAM_K(XR, MK, false, false);                                                          \
     else if (pfx) DCF_STREAM_K(XR, false, true, DCF_STREAM_D48 != 0);                                          \
     else if (XR && DCF_STREAM_NBC && n_bytes == 16) DCF_STREAM_KN(XR, false, false, DCF_STREAM_D48 != 0, 16);    \
     else if (XR && DCF_STREAM_NBC && n_bytes == 4) DCF_STREAM_KN(XR, false, false, DCF_STREAM_D48 != 0, 4);      \
@@ -1966,7 +1971,7 @@ int dcf_eval_multi_gpu_device(dcf_prg* const* prgs, size_t G, size_t n_bytes, in
 
 #ifdef DCF_CLOCK_STAMPS
 // Diagnostic builds only (not in include/dcf_hip.h): the in-kernel clock stamps of slot `slot`
-// (0 = k_eval_wide_tail2, 1 = k_eval_wide_head_stream, 2 = k_eval16_stream) of the last launch:
+// (0 = k_eval_wide_tail2, 1 = k_eval_wide_head_stream, 2 = k_eval16_stream, 3 = k_eval16_oct) of the last launch:
 // per workgroup {memtime, realtime} at start and end, kClkGroups x 4 u64.
 int dcf_debug_clock_stamps(int device, int slot, unsigned long long* out, size_t n) {
   if (!out || slot < 0 || slot >= (int)kClkSlots || n < (size_t)kClkGroups * 4) return fail(DCF_ERR_ARG, "bad argument");

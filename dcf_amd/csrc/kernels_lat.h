@@ -38,17 +38,32 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
 
 // Column j of AES-256(in) for the lane quad holding the block's four columns (lane j of the
 // quad holds column j); kw[r] = word j of round key r.
+#ifndef DCF_COL_LATE_DPP
+#define DCF_COL_LATE_DPP 1  // rounds 1-13: look up the lane's own four bytes, rotate the results
+#endif
 __device__ __forceinline__ uint32_t aes256_col(uint32_t st, const uint32_t (&kw)[15], const uint32_t* lds,
                                                uint32_t lc) {
   st ^= kw[0];
 #pragma unroll
   for (int r = 1; r < 14; ++r) {
-    const uint32_t w1 = dpp<kQpRot1>(st), w2 = dpp<kQpRot2>(st), w3 = dpp<kQpRot3>(st);
-    const uint32_t a = lk<0, 0>(lds, st, lc);
-    const uint32_t c = lk<1, 1>(lds, w1, lc);
-    const uint32_t d = lk<2, 2>(lds, w2, lc);
-    const uint32_t e = lk<3, 3>(lds, w3, lc);
-    st = xor3(xor3(a, c, d), e, kw[r]);
+    if (DCF_COL_LATE_DPP) {
+      // out_j = T0[s_j.b0] ^ T1[s_{j+1}.b1] ^ T2[s_{j+2}.b2] ^ T3[s_{j+3}.b3]: lane j looks up all
+      // four bytes of ITS word (T1[s_j.b1] is lane j-1's term, ...) and the quad rotations move
+      // the results instead of the inputs — the lookups start right after the previous round's
+      // XOR (no DPP hazard wait, no moves in front of them) and the moves fold into the XORs.
+      const uint32_t a = lk<0, 0>(lds, st, lc);
+      const uint32_t c = lk<1, 1>(lds, st, lc);
+      const uint32_t d = lk<2, 2>(lds, st, lc);
+      const uint32_t e = lk<3, 3>(lds, st, lc);
+      st = (a ^ kw[r]) ^ dpp<kQpRot1>(c) ^ dpp<kQpRot2>(d) ^ dpp<kQpRot3>(e);
+    } else {
+      const uint32_t w1 = dpp<kQpRot1>(st), w2 = dpp<kQpRot2>(st), w3 = dpp<kQpRot3>(st);
+      const uint32_t a = lk<0, 0>(lds, st, lc);
+      const uint32_t c = lk<1, 1>(lds, w1, lc);
+      const uint32_t d = lk<2, 2>(lds, w2, lc);
+      const uint32_t e = lk<3, 3>(lds, w3, lc);
+      st = xor3(xor3(a, c, d), e, kw[r]);
+    }
   }
   // final round: SubBytes + ShiftRows + AddRoundKey (S(x) sits in byte r of T_{(r+2)&3})
   const uint32_t w1 = dpp<kQpRot1>(st), w2 = dpp<kQpRot2>(st), w3 = dpp<kQpRot3>(st);
@@ -61,17 +76,23 @@ __device__ __forceinline__ uint32_t aes256_col(uint32_t st, const uint32_t (&kw)
 
 // The 128 KiB replicated T-tables (lds_fill_tables' layout), every load of a thread issued
 // before its stores: a latency kernel cannot afford 32 dependent load/store round trips.
-__device__ __forceinline__ void lds_fill_tables_fast(uint32_t* lds, const uint32_t* __restrict__ tab) {
-  constexpr int kPer = kLdsWords / kBlock;
-  uint32_t v[kPer];
+constexpr int kFillPer = kLdsWords / kBlock;
+__device__ __forceinline__ void lds_fill_load(uint32_t (&v)[kFillPer], const uint32_t* __restrict__ tab) {
 #pragma unroll
-  for (int i = 0; i < kPer; ++i) {
+  for (int i = 0; i < kFillPer; ++i) {
     const int idx = (int)threadIdx.x + i * kBlock;
     const int half = idx >> 14, rem = idx & 16383;
     v[i] = tab[(2 * half + ((rem & 63) >> 5)) * 256 + (rem >> 6)];
   }
+}
+__device__ __forceinline__ void lds_fill_store(uint32_t* lds, const uint32_t (&v)[kFillPer]) {
 #pragma unroll
-  for (int i = 0; i < kPer; ++i) lds[(int)threadIdx.x + i * kBlock] = v[i];
+  for (int i = 0; i < kFillPer; ++i) lds[(int)threadIdx.x + i * kBlock] = v[i];
+}
+__device__ __forceinline__ void lds_fill_tables_fast(uint32_t* lds, const uint32_t* __restrict__ tab) {
+  uint32_t v[kFillPer];
+  lds_fill_load(v, tab);
+  lds_fill_store(lds, v);
 }
 
 __device__ __forceinline__ void col_round_keys(const RoundKeys& rk, uint32_t j, uint32_t (&kw)[15]) {
@@ -102,10 +123,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_oct(
   // stage the key (single-key CWB, include/dcf_hip.h: 16-byte multiple) and this group's x rows
   const uint32_t np1_off = (2u * n * 16u + n + 15u) & ~15u;
   const uint32_t kq = np1_off / 16u + 1u;
-  for (uint32_t i = threadIdx.x; i < kq; i += blockDim.x) key[i] = reinterpret_cast<const uint4*>(cwb)[i];
-  for (uint32_t i = threadIdx.x; i < np * nbytes; i += blockDim.x) xsh[i] = xs[p0 * nbytes + i];
-  lds_fill_tables_fast(lds, tab);
+  // every load first (the T-tables from L2, the key and x rows possibly over PCIe from mapped
+  // host memory), then every LDS store: one memory latency in the prologue, not three
+  uint32_t tv[kFillPer];
+  lds_fill_load(tv, tab);
+  const bool kl = threadIdx.x < kq, xl = threadIdx.x < np * nbytes;
+  const uint4 kv = kl ? reinterpret_cast<const uint4*>(cwb)[threadIdx.x] : make_uint4(0u, 0u, 0u, 0u);
+  const uint8_t xv = xl ? xs[p0 * nbytes + threadIdx.x] : (uint8_t)0;
+  lds_fill_store(lds, tv);
+  if (kl) key[threadIdx.x] = kv;
+  if (xl) xsh[threadIdx.x] = xv;
+  for (uint32_t i = threadIdx.x + blockDim.x; i < kq; i += blockDim.x) key[i] = reinterpret_cast<const uint4*>(cwb)[i];
+  for (uint32_t i = threadIdx.x + blockDim.x; i < np * nbytes; i += blockDim.x) xsh[i] = xs[p0 * nbytes + i];
   __syncthreads();
+  DCF_CLK(3, 0);
   const uint32_t lc = lane_const();
   const uint32_t oct = threadIdx.x >> 3, b = (threadIdx.x >> 2) & 1u, j = threadIdx.x & 3u;
   if (oct >= np) return;  // whole octets (and whole quads) leave together: after the only barrier
@@ -150,6 +181,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_oct(
   }
   if (b == 0u)  // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), column j of point p0 + oct
     reinterpret_cast<uint32_t*>(ys)[(p0 + oct) * 4u + j] = v ^ s ^ ((0u - t) & np1);
+  DCF_CLK(3, 1);
 }
 
 // Dcf::gen (lib.rs:86-161) of num_keys keys, 16 lanes per key: `kpw` keys per workgroup of

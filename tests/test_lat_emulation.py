@@ -66,11 +66,20 @@ def _ror(vals, n):
 ROT1, ROT2, ROT3, BC0 = (1, 2, 3, 0), (2, 3, 0, 1), (3, 0, 1, 2), (0, 0, 0, 0)
 
 
+LATE_DPP = True  # kernels_lat.h DCF_COL_LATE_DPP: rotate the lookup results instead of the inputs
+
+
 def aes_cols(st, rk):
     """aes256_col for every lane of `st` (lane i holds column i & 3 of its quad's block)."""
     kw = lambda r, i: rk[4 * r + (i & 3)]  # noqa: E731
     st = [s ^ kw(0, i) for i, s in enumerate(st)]
     for r in range(1, 14):
+        if LATE_DPP:  # each lane looks up its own word's four bytes; the results rotate
+            a = [T[0][_byte(w, 0)] for w in st]
+            c, d, e = ([T[k][_byte(w, k)] for w in st] for k in (1, 2, 3))
+            c1, d2, e3 = _quad(c, ROT1), _quad(d, ROT2), _quad(e, ROT3)
+            st = [a[i] ^ kw(r, i) ^ c1[i] ^ d2[i] ^ e3[i] for i in range(len(st))]
+            continue
         w1, w2, w3 = _quad(st, ROT1), _quad(st, ROT2), _quad(st, ROT3)
         st = [T[0][_byte(st[i], 0)] ^ T[1][_byte(w1[i], 1)] ^ T[2][_byte(w2[i], 2)] ^ T[3][_byte(w3[i], 3)] ^ kw(r, i)
               for i in range(len(st))]
@@ -179,13 +188,17 @@ def col_gen(rk, alpha, beta, s0_0, s0_1, bound):
 
 
 def test_column_aes_matches_fips197():
-    # FIPS-197 C.3: AES-256
+    # FIPS-197 C.3: AES-256, both round forms of aes256_col
+    global LATE_DPP
     key = bytes(range(32))
     pt = bytes.fromhex("00112233445566778899aabbccddeeff")
     rk = _expand256(key)
     st = [int.from_bytes(pt[4 * (i & 3):4 * (i & 3) + 4], "little") for i in range(4)]
-    out = b"".join(w.to_bytes(4, "little") for w in aes_cols(st, rk))
-    assert out.hex() == "8ea2b7ca516745bfeafc49904b496089"
+    for late in (True, False):
+        LATE_DPP = late
+        out = b"".join(w.to_bytes(4, "little") for w in aes_cols(st, rk))
+        assert out.hex() == "8ea2b7ca516745bfeafc49904b496089"
+    LATE_DPP = True
 
 
 def test_oct_and_col_lane_algorithm_vs_oracle():
