@@ -300,6 +300,56 @@ __device__ __forceinline__ void aes_tt_bk(uint32_t (&st)[NB][4], uint32_t (&ko)[
   }
 }
 
+// NB independent AES-NR encryptions, block b under schedule A (hm[b] = 0) or schedule B
+// (hm[b] = ~0).  Both schedules' round keys come by uniform global loads (one address per
+// wave: a single vector-L1 request, unlike aes_tt_bk's per-lane offsets), AHEAD rounds before
+// their use, and each lane picks its word with one v_bitop3.  qa / qb[(r - 1) % AHEAD] hold
+// round key r; the caller has loaded keys 1 .. AHEAD - 1 and XORed key 0 into st.
+template <int NR, int NB, int AHEAD>
+__device__ __forceinline__ void aes_tt_gk2(uint32_t (&st)[NB][4], const uint32_t (&hm)[NB],
+                                           const uint4* __restrict__ ka, const uint4* __restrict__ kb,
+                                           uint4 (&qa)[AHEAD], uint4 (&qb)[AHEAD], const uint32_t* lds, uint32_t lc) {
+  uint32_t zb = 0u;
+#pragma unroll
+  for (int r = 1; r <= NR; ++r) {
+    // zb: a zero "redefined" after the previous round's state, so the loads stay AHEAD rounds
+    // ahead instead of being hoisted into 2 (NR + 1) live keys
+    asm volatile("" : "+v"(zb) : "v"(st[0][0]), "v"(st[NB - 1][0]));
+    const int rn = r + AHEAD - 1;
+    if (rn <= NR) {
+      qa[(rn - 1) % AHEAD] = ka[rn + zb];
+      qb[(rn - 1) % AHEAD] = kb[rn + zb];
+    }
+    const uint4 a4 = qa[(r - 1) % AHEAD], b4 = qb[(r - 1) % AHEAD];
+    const uint32_t aw[4] = {a4.x, a4.y, a4.z, a4.w}, bw[4] = {b4.x, b4.y, b4.z, b4.w};
+    uint32_t o[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t kw = __builtin_amdgcn_bitop3_b32(hm[b], bw[j], aw[j], 0xCA);  // hm ? B : A
+        if (r < NR) {
+          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(xor3(a, c, d), e, kw);
+        } else {  // final round: S(x) sits in byte r of T_{(r+2)&3}
+          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
+          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
+          o[b][j] = xor3(__builtin_amdgcn_perm(c, a, 0x0c0c0500u), __builtin_amdgcn_perm(e, d, 0x07020c0cu), kw);
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
+  }
+}
+
 // NB independent AES encryptions with NR rounds (10: AES-128, 14: AES-256), each
 // under its own key schedule read from LDS: rk[b] points at NR + 1 uint4 round
 // keys (per lane, so a lane may pick its schedule; lanes reading the same

@@ -216,7 +216,17 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     // the CW loads, so waiting for them never waits for those; later rounds 3 ahead in the AES)
     uint32_t ko[NS];
     uint4 kq[NS][3], k0g[NS];
-    if (DCF_WHS_GK) {
+    // DCF_WHS_GK == 2: both schedules by uniform loads (rounds 0 .. 2 here, before the CW loads)
+    constexpr int GA = 3;
+    uint4 qa[GA], qb[GA];
+    if (DCF_WHS_GK == 2) {
+#pragma unroll
+      for (int q = 0; q < GA; ++q) {
+        qa[q] = rk2[q];
+        qb[q] = rk2[15 + q];
+      }
+    }
+    if (DCF_WHS_GK == 1) {
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 #pragma unroll
       for (int i = 0; i < NS; ++i) {
@@ -252,7 +262,11 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       // re-associating base + 16 r (rks_a is a link-time symbol: 14 materialised constants and
       // a v_mad per round); the mask proves the sign bit clear, so +16 r folds into ds_read
       uint4 k0;
-      if (DCF_WHS_GK) {
+      if (DCF_WHS_GK == 2) {
+        const uint32_t m = 0u - hi;
+        k0 = make_uint4(pick(m, qb[0].x, qa[0].x), pick(m, qb[0].y, qa[0].y), pick(m, qb[0].z, qa[0].z),
+                        pick(m, qb[0].w, qa[0].w));
+      } else if (DCF_WHS_GK == 1) {
         k0 = k0g[i];
       } else {
         uint32_t kb = rks_a + 368u * hi;
@@ -268,7 +282,21 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
         st[i][j] = xor3(sel[i][j], inv[i], k0w[j]);  // round key 0 folded in
       }
     }
-    if (DCF_WHS_GK)
+    if (DCF_WHS_GK == 2) {
+      uint32_t hms[NS];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) hms[i] = 0u - ((L.ph[i] != 0u) & (L.cur[i] >> 31));
+      // rounds 1 .. GA - 1 are in qa / qb[0 .. GA - 2] after a shift by one slot
+      uint4 ra[GA], rb[GA];
+#pragma unroll
+      for (int q = 0; q + 1 < GA; ++q) {
+        ra[q] = qa[q + 1];
+        rb[q] = qb[q + 1];
+      }
+      ra[GA - 1] = qa[0];
+      rb[GA - 1] = qb[0];
+      aes_tt_gk2<14, NS, GA>(st, hms, rk2, rk2 + 15, ra, rb, lds, lc);
+    } else if (DCF_WHS_GK == 1)
       aes_tt_bk<14, NS, 3>(st, ko, rkrs, kq, lds, lc);
     else
       aes_tt_lka<14, NS, true>(st, ka, lds, lc);
