@@ -37,9 +37,6 @@
 #include "kernels_lat.h"
 #include "kernels_wide.h"
 #include "kernels_bs.h"
-#ifndef DCF_STREAM_PFN
-#define DCF_STREAM_PFN 0  // N = 4 below a shared prefix: per-lane next-point slot (kernels_stream.h PFN; 1 row + x, 2 x only)
-#endif
 #include "kernels_stream.h"
 #include "kernels_mmo.h"
 #include "kernels_mmo_wide.h"
@@ -1347,16 +1344,14 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     uint8_t* lys = ys + c0 * lam;
     const uint8_t* ls0 = s0s + k0 * lam;
     const PrefixTable lpf = (multi && pf.levels) ? PrefixTable{pf.sv + 2 * (k0 << pf.levels), pf.levels} : pf;
-#define DCF_STREAM_KNP(XR, MK, PF, D4, NBC, PN)                                                               \
-  hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK, kBlock, false, PF, D4, NBC, PN>), dim3((unsigned)blocks), block, 0, st, \
+#define DCF_STREAM_KN(XR, MK, PF, D4, NBC)                                                                    \
+  hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK, kBlock, false, PF, D4, NBC>), dim3((unsigned)blocks), block, 0, st, \
                      p->d_tab, p->rk[0], lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes, \
                      (uint64_t)kc, (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0)
-#define DCF_STREAM_KN(XR, MK, PF, D4, NBC) DCF_STREAM_KNP(XR, MK, PF, D4, NBC, false)
 #define DCF_STREAM_K(XR, MK, PF, D4) DCF_STREAM_KN(XR, MK, PF, D4, 0)
     // single key, x in registers: N = 16 (C1 / C3) and N = 4 (C2) with the x width fixed at
     // compile time (a point's start loads x without width branches: C2 starts a point every
     // ~13 AES slots)
-
 #ifndef DCF_MK_PFXT
 #define DCF_MK_PFXT 1  // multi-key: a kernel instance for "per-key top trees present" (no root-seed start path:
                        // 48 -> 33 SGPR spills; C5 r03c A/B, same box, 2 runs: 414.6 / 413.7 vs 408.5 / 408.1 M evals/s)
@@ -1367,8 +1362,6 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     else if (MK) DCF_STREAM_K(XR, MK, false, false);                                                          \
     else if (pfx) DCF_STREAM_K(XR, false, true, DCF_STREAM_D48 != 0);                                          \
     else if (XR && DCF_STREAM_NBC && n_bytes == 16) DCF_STREAM_KN(XR, false, false, DCF_STREAM_D48 != 0, 16);    \
-    else if (XR && DCF_STREAM_NBC && n_bytes == 4 && DCF_STREAM_PFN && lpf.levels)                              \
-      DCF_STREAM_KNP(XR, false, false, false, 4, XR);                                                          \
     else if (XR && DCF_STREAM_NBC && n_bytes == 4) DCF_STREAM_KN(XR, false, false, DCF_STREAM_D48 != 0, 4);      \
     else DCF_STREAM_K(XR, false, false, DCF_STREAM_D48 != 0);                                                  \
   } while (0)
@@ -1390,7 +1383,6 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
 #undef DCF_STREAM
 #undef DCF_STREAM_K
 #undef DCF_STREAM_KN
-#undef DCF_STREAM_KNP
   } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
     phase_mark(p, L, 1);

@@ -297,55 +297,6 @@ __device__ __forceinline__ void stream_claim(StreamLane<NS, XREG, MULTI>& L, int
   }
 }
 
-// Hand the next point index to every lane with `mine` set (got / pnew), touching no stream:
-// the claim behind the per-lane next-point slot (PFN below).  Wave-uniform control flow.
-template <uint32_t UNIT = kStreamUnit>
-__device__ __forceinline__ void point_claim(bool mine, uint32_t& unext, uint32_t& uend, bool& exhausted,
-                                            uint32_t* __restrict__ ctr, uint32_t nunits, uint32_t total,
-                                            uint32_t& pnew, bool& got) {
-  uint64_t need = __ballot(mine);
-  while (need) {
-    if (unext >= uend && !exhausted) {
-      const uint32_t u = dequeue_unit(ctr);
-      if (u >= nunits) {
-        exhausted = true;
-      } else {
-        unext = u * UNIT;
-        uend = min(unext + UNIT, total);
-      }
-    }
-    if (exhausted && unext >= uend) break;
-    const uint32_t rank = lane_rank(need);
-    const bool take = mine && rank < uend - unext;
-    pnew = take ? unext + rank : pnew;
-    got = got || take;
-    const uint64_t taken = __ballot(take);
-    unext += (uint32_t)__popcll(taken);
-    need &= ~taken;
-    mine = mine && !take;
-  }
-}
-
-// Start stream i (single key, x in registers, one x word: N = 4) at point p below a shared
-// prefix of D levels from a table row already in registers (the PFN slot): no memory access.
-template <int NS, bool MULTI>
-__device__ __forceinline__ void stream_start_row(StreamLane<NS, true, MULTI>& L, int i, uint32_t p, uint32_t xw,
-                                                 uint4 sv, const uint4 vv, uint32_t D) {
-  const uint32_t w0 = bswap32(xw);
-  L.t[i] = (sv.w >> 24) & 1u;  // prefix_row: t rides in bit 0 of byte 15
-  sv.w &= kMaskLast;
-  L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
-  L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
-  L.ph[i] = 0u;
-  L.lev[i] = D;
-  L.ci[i] = D;
-  L.pt[i] = p;
-  L.alive[i] = true;
-  L.cur[i] = w0 << D;
-  L.xw[i][0] = 0u; L.xw[i][1] = 0u; L.xw[i][2] = 0u; L.xw[i][3] = 0u;
-  L.fresh[i] = false;
-}
-
 // The stream's next 32 x bits at level nl (a multiple of 32): from the queue (XREG) or x.
 template <int NS, bool XREG, bool MULTI>
 __device__ __forceinline__ void stream_next_word(StreamLane<NS, XREG, MULTI>& L, int i, uint32_t nl, uint32_t nlev,
@@ -404,18 +355,8 @@ __global__ void k_cw_rows48(const uint4* __restrict__ cw_s, const uint4* __restr
 }
 
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
-//
-// PFN (single key, N = 4, a shared-prefix table present — C2's 8-level walks, which start a point
-// every ~5 steps of a wave): a per-lane next-point slot.  Without it a refill waits for two
-// dependent round trips (the x word, then the point's table row, a random 32-B gather from a
-// 2^24-row table), during which the wave's other stream stalls too; probes with the row gather
-// (or the x load) removed ran the walk 7.5 % (3 %) faster.  The slot claims a point ahead, loads
-// its x word at a refill, gathers its table row in a later iteration without a refill (its x
-// load is then older than that iteration's CW loads, which the update has waited for), and the
-// next stream to finish starts from it with no memory access.  Loads into the slot are issued
-// only in iterations that do not read it, so no wait the compiler places for them stalls.
 template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false, int HK = 0,
-          bool PFX = false, bool D48 = false, int SL = -1, int NBC = 0, int SK = 0, bool PFN = false>
+          bool PFX = false, bool D48 = false, int SL = -1, int NBC = 0, int SK = 0>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -447,22 +388,6 @@ __device__ __forceinline__ void stream_run(
   for (int i = 0; i < NS; ++i)
     stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, true, unext, uend, exhausted, ctr, nunits, total32, s0s,
                                                   s0v, party, xs, nbytes, ppk, pf);
-  // PFN slot: nq = 0 empty, 1 point npt claimed and its x word nxw loading, 2 its row in nsr / nvr
-  constexpr bool PN = PFN && XREG && !MULTI && NBC == 4 && DCF_REFILL_ONCE && DCF_STREAM_PFN != 0;
-  uint32_t nq = 0u, npt = 0u, nxw = 0u;
-  uint4 nsr = make_uint4(0u, 0u, 0u, 0u), nvr = nsr;
-  const uint32_t* xs32 = reinterpret_cast<const uint32_t*>(xs);
-  auto slot_claim = [&]() {  // wave-uniform: lanes with an empty slot claim a point and load its x
-    uint32_t pnew = 0u;
-    bool got = false;
-    point_claim<UNIT>(nq == 0u, unext, uend, exhausted, ctr, nunits, total32, pnew, got);
-    if (got) {
-      npt = pnew;
-      nxw = xs32[pnew];
-      nq = 1u;
-    }
-  };
-  if (PN) slot_claim();
 
   uint64_t nblk = 0;  // AES blocks this wave encrypts for live streams (wave-uniform)
   for (;;) {
@@ -679,23 +604,6 @@ __device__ __forceinline__ void stream_run(
 #endif
       L.lev[i] = nl;
     }
-    if constexpr (PN && DCF_STREAM_PFN != 2) {  // (2: the slot holds the x word only)
-      bool anyd = false;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) anyd = anyd || (L.alive[i] && L.lev[i] == nlev);
-      if (!__ballot(anyd)) {  // no stream finished: gather the rows of slots whose x word is in
-        const bool g = nq == 1u;
-        if (__ballot(g)) {
-          if (g) {
-            const uint32_t r = bswap32(nxw) >> (32u - pf.levels);
-            nsr = pf.sv[2u * r];
-            nvr = pf.sv[2u * r + 1u];
-          }
-          nq = g ? 2u : nq;
-        }
-        continue;  // nothing to store or refill
-      }
-    }
     // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.
     if constexpr (BATCH) {
       // Per stream: claim the new point, load its x words, store the finished y (the old state
@@ -735,32 +643,14 @@ __device__ __forceinline__ void stream_run(
         yp = L.pt[i];
         if (!DCF_STREAM_LATE_STORE) ys[yp] = yv;
       }
-      if (__ballot(done)) {
-        if constexpr (PN) {  // the slot's point first (row in registers, or gathered now)
-          const bool s2 = done && nq == 2u, s1 = done && nq == 1u;
-          if (s2) stream_start_row<NS, MULTI>(L, i, npt, nxw, nsr, nvr, pf.levels);
-          if (__ballot(s1)) {
-            if (s1) {
-              L.xw[i][0] = nxw; L.xw[i][1] = 0u; L.xw[i][2] = 0u; L.xw[i][3] = 0u;
-              stream_start<NS, XREG, MULTI, PFX, NBC, true>(L, i, npt, s0s, s0v, party, xs, nbytes, ppk, pf);
-            }
-          }
-          nq = (s1 || s2) ? 0u : nq;
-          const bool rest = done && !s1 && !s2;
-          if (__ballot(rest))
-            stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, rest, unext, uend, exhausted, ctr, nunits, total32,
-                                                          s0s, s0v, party, xs, nbytes, ppk, pf);
-        } else {
-          stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total32, s0s,
-                                                        s0v, party, xs, nbytes, ppk, pf);
-        }
-      }
+      if (__ballot(done))
+        stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total32, s0s,
+                                                  s0v, party, xs, nbytes, ppk, pf);
       if (DCF_STREAM_LATE_STORE && done) {
         asm volatile("" ::: "memory");  // keep the store below the refill's loads
         ys[yp] = yv;
       }
     }
-    if (PN) slot_claim();
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
   if ((threadIdx.x & 63u) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, (unsigned long long)nblk);
@@ -768,7 +658,7 @@ __device__ __forceinline__ void stream_run(
 
 // TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.
 template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false, bool PFX = false, bool D48 = false,
-          int NBC = 0, bool PFN = false>
+          int NBC = 0>
 __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -797,7 +687,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   constexpr int SL = (MULTI && !TT2) ? DCF_MK_SL : -1;
   constexpr int SK = (MULTI && !TT2) ? DCF_MK_SK : 0;
   DCF_CLK(2, 0);
-  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC, SK, PFN>(
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC, SK>(
       lds, (GK || HK || SK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total,
       ctr, ys, pf);
   DCF_CLK(2, 1);
