@@ -6,16 +6,6 @@
 
 namespace {
 
-// A uniform read (a correction word of the level every lane is on) as a VECTOR load: the index
-// gets a zero the compiler cannot see through, so the load is not scalarised.  A scalar load
-// shares lgkmcnt with the LDS lookups and may return out of order, so every T-table round
-// after it would wait with lgkmcnt(0) for all its lookups at once instead of in batches.
-template <typename T>
-__device__ __forceinline__ T vload(const T* __restrict__ p, uint64_t i) {
-  uint32_t z = 0u;
-  asm volatile("" : "+v"(z));
-  return p[i + z];
-}
 
 // ------------------------------------------------------------------------
 // k_eval16: DcfImpl::eval (lib.rs:163-204) at LAMBDA = 16.
@@ -50,9 +40,9 @@ __device__ __forceinline__ uint4 tt_eval_one(const uint32_t* lds, uint32_t lc, c
       }
       aes256_tt<2>(st, rk, lds, lc);  // st[0] = A, st[1] = B
       const uint64_t ci = (uint64_t)lev * num_keys + key;
-      const uint4 cs = vload(cw_s, ci);
-      const uint4 cv = vload(cw_v, ci);
-      const uint32_t ct = vload(cw_t, ci);
+      const uint4 cs = cw_s[ci];
+      const uint4 cv = cw_v[ci];
+      const uint32_t ct = cw_t[ci];
       const uint32_t xb = cur >> 31;  // Msb0 bit of x (lib.rs:181)
       cur <<= 1;
       const uint32_t keepA = xb - 1u;  // all ones when going left
@@ -216,9 +206,9 @@ __device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, 
         B[j] = odd ? st[0][j] : other;
       }
       const uint64_t ci = (uint64_t)lev * num_keys + key;
-      const uint4 cs = vload(cw_s, ci);
-      const uint4 cv = vload(cw_v, ci);
-      const uint32_t ct = vload(cw_t, ci);
+      const uint4 cs = cw_s[ci];
+      const uint4 cv = cw_v[ci];
+      const uint32_t ct = cw_t[ci];
       const uint32_t xb = cur >> 31;  // Msb0 bit of x (lib.rs:181)
       cur <<= 1;
       const uint32_t keepA = xb - 1u;  // all ones when going left
@@ -774,9 +764,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
   for (uint32_t lev = S; lev < D - H; ++lev) {
     const uint32_t np = 1u << (lev - S);  // this workgroup's parents at level lev
     const bool last = lev + 1u == D;
-    const uint4 cs = vload(cw_s, lev), cv = vload(cw_v, lev);
+    const uint4 cs = cw_s[lev], cv = cw_v[lev];
     const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
-    const uint32_t ct = vload(cw_t, lev);
+    const uint32_t ct = cw_t[lev];
     const uint4* xs_ = reinterpret_cast<const uint4*>(X);
     const uint4* xv_ = xs_ + R;
     const uint8_t* xt_ = X + (uint64_t)R * 32u;
@@ -857,12 +847,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
         k = d + 1u;
       }
       for (;; ++k) {  // expand depth k (level B + k)
-        const uint4 cs = vload(cw_s, B + k), cv = vload(cw_v, B + k);
-        const uint32_t ct = vload(cw_t, B + k);
+        const uint4 cs = cw_s[B + k], cv = cw_v[B + k];
         const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
         const uint32_t s[4] = {n[0], n[1], n[2], n[3]}, v[4] = {n[4], n[5], n[6], n[7]};
         uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
-        fd_children<GKB>(lds, lc, rk, csw, cvw, ct, s, v, n[8], sl, vl, tl, sr, vr, tr, rkg);
+        fd_children<GKB>(lds, lc, rk, csw, cvw, cw_t[B + k], s, v, n[8], sl, vl, tl, sr, vr, tr, rkg);
         if (k + 1u == H) {  // bottom: leaves 2i, 2i + 1 of this node's block of rows
           uint4* row = rows + 4u * i;
           row[0] = make_uint4(sl[0], sl[1], sl[2], (sl[3] & kMaskLast) | (tl << 24));
@@ -936,12 +925,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_dfs16(
         k = d + 1u;
       }
       for (;; ++k) {  // expand depth k (level lev0 + k)
-        const uint4 cs = vload(cw_s, lev0 + k), cv = vload(cw_v, lev0 + k);
-        const uint32_t ct = vload(cw_t, lev0 + k);
+        const uint4 cs = cw_s[lev0 + k], cv = cw_v[lev0 + k];
         const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
         const uint32_t s[4] = {n[0], n[1], n[2], n[3]}, v[4] = {n[4], n[5], n[6], n[7]};
         uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
-        fd_children(lds, lc, rk, csw, cvw, ct, s, v, n[8], sl, vl, tl, sr, vr, tr);
+        fd_children(lds, lc, rk, csw, cvw, cw_t[lev0 + k], s, v, n[8], sl, vl, tl, sr, vr, tr);
         if (k + 1u == (uint32_t)H) {  // leaves: y = v ^ s ^ t * cw_np1 (lib.rs:192)
           if (live) {
             const uint32_t ml = 0u - tl, mr = 0u - tr;
