@@ -556,7 +556,7 @@ __device__ __forceinline__ void stream_run(
         L.cur[i] <<= (rr & 1u);
         L.ci[i] += rr & 1u;
         if (rr && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
-        if (DCF_REUSE_CHAIN) {
+        if (DCF_REUSE_CHAIN && !MULTI) {  // (multi-key instances: no registers to spare)
           // Chain: the reused right step ran at t = 0 and B's bit b = lsb(B^~s) is 0, so t' = b = 0
           // and s is unchanged again — and so on for every further right step: each one is
           // v ^= ~s & M with no CW (t = 0) and no AES (lib.rs:176-185).  Take the whole run of 1
@@ -564,19 +564,23 @@ __device__ __forceinline__ void stream_run(
           // inside the word is a left step whose B half (B^~s) & M = d & M is applied now, A next.
           const uint32_t zm = rr & (tm1 ^ 0xFFFFFFFFu) & ((d0 & 1u) - 1u);  // all ones: chain
           const uint32_t room = min(32u - (nl & 31u), nlev - nl);          // levels left in this word
-          const uint32_t run = min((uint32_t)__clz((int)~L.cur[i]), room) & zm;
+          const uint32_t ones = (uint32_t)__clz((int)~L.cur[i]);
+          // DCF_REUSE_CHAIN 2: the run stops one level short of the word's end, so the chain never
+          // fetches the next x word (a run reaching it leaves its last right step to the AES slot)
+          const uint32_t run = (DCF_REUSE_CHAIN == 2 ? min(ones, room - 1u) : min(ones, room)) & zm;
           const uint32_t om = 0u - (run & 1u);                                // odd run: v ^= ~s & M once
-          const uint32_t lm = zm & (0u - (uint32_t)(run < room));            // the run ends at a left step
+          const uint32_t lm = zm & (0u - (uint32_t)(DCF_REUSE_CHAIN == 2 ? ones < room : run < room));  // ends at a left step
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
             L.v[i][j] ^= ((om & ~L.s[i][j]) ^ (lm & d[j])) & msk;
           }
           nl += run;
-          L.cur[i] = run >= 32u ? 0u : (L.cur[i] << run);
+          L.cur[i] = (DCF_REUSE_CHAIN == 2 || run < 32u) ? (L.cur[i] << run) : 0u;
           L.ci[i] += run;
           L.ph[i] = lm ? 1u : L.ph[i];
-          if (run && run == room && nl < nlev) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+          if (DCF_REUSE_CHAIN != 2 && run && run == room && nl < nlev)
+            stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
         }
       }
 #else
