@@ -567,7 +567,8 @@ __device__ __forceinline__ void stream_run(
           const uint32_t ones = (uint32_t)__clz((int)~L.cur[i]);
           // DCF_REUSE_CHAIN 2: the run stops one level short of the word's end, so the chain never
           // fetches the next x word (a run reaching it leaves its last right step to the AES slot)
-          const uint32_t run = (DCF_REUSE_CHAIN == 2 ? min(ones, room - 1u) : min(ones, room)) & zm;
+          // (room is 0 once the reused step ended the point: no run then)
+          const uint32_t run = (DCF_REUSE_CHAIN == 2 ? min(ones, room ? room - 1u : 0u) : min(ones, room)) & zm;
           const uint32_t om = 0u - (run & 1u);                                // odd run: v ^= ~s & M once
           const uint32_t lm = zm & (0u - (uint32_t)(DCF_REUSE_CHAIN == 2 ? ones < room : run < room));  // ends at a left step
 #pragma unroll
