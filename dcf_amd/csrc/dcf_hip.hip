@@ -284,6 +284,9 @@ uint32_t prefix_split(uint32_t levels) { return levels > 18u ? 8u : (levels > 10
 #ifndef DCF_FD_DFS
 #define DCF_FD_DFS 1
 #endif
+#ifndef DCF_FD_BUILD
+#define DCF_FD_BUILD 1  // full domain: the levels above the depth-first tail by one k_prefix_build16 launch
+#endif
 #ifndef DCF_FD_TAIL
 #define DCF_FD_TAIL (DCF_FD_DFS ? 4 : 3)  // depth-first 5: 128 VGPRs + scratch spills
 #endif
@@ -1772,6 +1775,32 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   // node level in HBM is 2^(n - kFdTail).
   constexpr uint32_t kFdTail = DCF_FD_TAIL;
   const bool fused = p->kind == 0 && nlev > kFdTail;
+  const size_t n = 8 * n_bytes;
+  const uint4* cws = (const uint4*)cwb;
+  const uint4* cwv = (const uint4*)(cwb + n * lam);
+  const uint8_t* cwt = cwb + 2 * n * lam;
+  const uint4* np1 = (const uint4*)(cwb + dcf_cwb_np1_offset(n_bytes, lam, 1));
+  const uint32_t lev_end = fused ? nlev - kFdTail : nlev;
+  // Hirose with the depth-first tail: levels 0 .. lev_end - 1 in ONE launch of the shared-prefix
+  // table build (k_prefix_build16: workgroup subtrees, a depth-first register tail, 32-byte rows)
+  // instead of one breadth-first level launch per level with 33-byte SoA nodes through HBM;
+  // the tail then starts from the rows.  Falls back to the level kernels if the table and its
+  // build buffers (~65 B per node of level lev_end) cannot be allocated.
+  if (DCF_FD_BUILD && fused && DCF_FD_DFS && lev_end >= 12) {
+    PrefixTable pf{nullptr, 0u};
+    const int brc = build_prefix(p, L.w, n_bytes, party, cws, cwv, cwt, np1, s0, lev_end, &pf, st);
+    if (brc != DCF_OK && brc != kPrefixNoMem) return brc;
+    if (brc == DCF_OK) {
+      const uint64_t nodes = 1ull << lev_end;
+      if (int rc2 = ensure_ctr(L.w)) return rc2;
+      HIP_TRY(hipMemsetAsync(L.w->d_ctr, 0, kCtrBytes, st));
+      hipLaunchKernelGGL((k_fd_dfs16<kFdTail, true>), dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st,
+                         p->d_tab, p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, pf.sv, (const uint4*)nullptr,
+                         (const uint8_t*)nullptr, (uint4*)ys, L.w->d_ctr);
+      HIP_TRY(hipGetLastError());
+      return DCF_OK;
+    }
+  }
   const uint64_t maxnodes = fused ? (npts >> kFdTail) : npts / 2;
   const size_t nodeb = 33;
   // + one work counter per launch (64-node units, see next_wave_base) after the nodes
@@ -1787,14 +1816,8 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   uint4* s_b = (uint4*)(w + maxnodes * nodeb + 16 - (maxnodes * nodeb) % 16);
   uint4* v_b = s_b + maxnodes;
   uint8_t* t_b = (uint8_t*)(v_b + maxnodes);
-  const size_t n = 8 * n_bytes;
-  const uint4* cws = (const uint4*)cwb;
-  const uint4* cwv = (const uint4*)(cwb + n * lam);
-  const uint8_t* cwt = cwb + 2 * n * lam;
-  const uint4* np1 = (const uint4*)(cwb + dcf_cwb_np1_offset(n_bytes, lam, 1));
   hipLaunchKernelGGL(k_fd_root16, dim3(1), dim3(64), 0, st, (const uint4*)s0, (uint32_t)party, s_a, v_a, t_a);
   HIP_TRY(hipGetLastError());
-  const uint32_t lev_end = fused ? nlev - kFdTail : nlev;
   for (uint32_t lev = 0; lev < lev_end; ++lev) {
     const uint64_t parents = 1ull << lev;
     if (p->kind == 1)

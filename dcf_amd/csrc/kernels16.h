@@ -887,7 +887,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
 // with H, not 2^H as in k_fd_tail16, and H = 4..5 fits.  Leaf-parent i (bits Msb-first = the
 // choices at depths 0 .. H-2) resumes from the slot at the depth of i's lowest set bit; its
 // expansion writes y for leaves 2i, 2i + 1 of the node's 2^H contiguous outputs.
-template <int H>
+// ROWS: the nodes of level lev0 are PrefixTable rows (k_prefix_build16's output: s with t in bit 0
+// of byte 15, then v) at s_in; v_in / t_in unused.
+template <int H, bool ROWS = false>
 __global__ __launch_bounds__(kBlock, 1) void k_fd_dfs16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -906,7 +908,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_dfs16(
     const uint64_t jj = live ? j : nnodes - 1;
     uint32_t stk[H - 1][9];  // pending right children: s[4] | v[4] | t, by depth
     uint32_t n[9];
-    {
+    if (ROWS) {
+      const uint4 sv = s_in[2 * jj], vv = s_in[2 * jj + 1];
+      n[0] = sv.x; n[1] = sv.y; n[2] = sv.z; n[3] = sv.w & kMaskLast;
+      n[4] = vv.x; n[5] = vv.y; n[6] = vv.z; n[7] = vv.w;
+      n[8] = (sv.w >> 24) & 1u;
+    } else {
       const uint4 sv = s_in[jj], vv = v_in[jj];
       n[0] = sv.x; n[1] = sv.y; n[2] = sv.z; n[3] = sv.w;
       n[4] = vv.x; n[5] = vv.y; n[6] = vv.z; n[7] = vv.w;

@@ -525,9 +525,10 @@ def test_error_codes_on_device(dcf):
     assert e.value.code == -2
 
 
-@pytest.mark.parametrize("nb,lam", [(1, 16), (2, 16), (1, 32), (1, 64)])
+@pytest.mark.parametrize("nb,lam", [(1, 16), (2, 16), (3, 16), (1, 32), (1, 64)])
 def test_full_domain_eval_vs_oracle(dcf, nb, lam):
-    """Full-domain eval (tree expansion) == pointwise oracle eval over every x."""
+    """Full-domain eval (tree expansion) == pointwise oracle eval over every x.  N = 2 and 3 take
+    the one-launch table build for the levels above the depth-first tail (D = 12 and 20)."""
     import torch
     rng = np.random.default_rng(nb * 100 + lam)
     keys = [rng.bytes(32) for _ in range(2 if lam == 16 else 18)]
