@@ -661,180 +661,7 @@ __device__ __forceinline__ void stream_run(
   if ((threadIdx.x & 63u) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, (unsigned long long)nblk);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Skewed stream loop (DCF_STREAM_SKEW; single key, x in registers, x width fixed, NS = 2).
-// stream_run encrypts both streams' blocks in one AES pass and then runs both level updates,
-// so during the updates (VALU only: ~15 % of a step) the wave issues no LDS lookups.  Here the
-// two streams are half a step apart: each half-step encrypts stream p's block while it runs
-// stream q = 1 - p's update on the block encrypted in the previous half-step, in one basic
-// block, so the update's VALU fills the waits of the AES rounds' lookups.  One block per lane
-// per half-step instead of two per step (the T-table rounds alone reach the same rate with 1 or
-// 2 blocks per lane, scripts/micro/aes_rate.hip).  Per stream the work is stream_run's exactly:
-// same schedule, same update (stream_update1), same bytes.
-// ---------------------------------------------------------------------------------------------
-template <int NS, bool MULTI>
-__device__ __forceinline__ void stream_update1(StreamLane<NS, true, MULTI>& L, int i, const uint32_t (&st)[4],
-                                               const uint4 cs, const uint4 cv, uint32_t ct, const uint4 cs2,
-                                               const uint4 cv2, uint32_t ct2, bool maybe, uint32_t nlev,
-                                               uint32_t nbytes) {
-  {  // next 32 x bits from the word queue (a fresh stream, no shared prefix)
-    const bool nw = L.fresh[i];
-    L.cur[i] = nw ? bswap32(L.xw[i][0]) : L.cur[i];
-    L.xw[i][0] = nw ? L.xw[i][1] : L.xw[i][0];
-    L.xw[i][1] = nw ? L.xw[i][2] : L.xw[i][1];
-    L.xw[i][2] = nw ? L.xw[i][3] : L.xw[i][2];
-    L.fresh[i] = false;
-  }
-  const uint32_t p = L.ph[i], xb = L.cur[i] >> 31;  // Msb0 bit of x (lib.rs:181)
-  const uint32_t adv = L.alive[i] ? (p | xb) : 0u;   // this step finishes the level
-  const uint32_t inv = p - 1u;                        // all ones on a B step
-  const uint32_t keepB = xb - 1u;                     // all ones when going left
-  const uint32_t tm = 0u - L.t[i], am = 0u - adv, pm = 0u - p;
-  const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w};
-  const uint32_t cvw[4] = {cv.x, cv.y, cv.z, cv.w};
-  uint32_t d[4];  // (A^s) or (B^~s)
-#pragma unroll
-  for (int j = 0; j < 4; ++j) d[j] = st[j] ^ L.s[i][j] ^ inv;
-  const uint32_t d0 = d[0];
-  const bool reuse = maybe && (L.s[i][3] & ~kMaskLast) == 0u;  // see stream_run "B reuse"
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
-    const uint32_t in = L.s[i][j] ^ inv;
-    const uint32_t vhat = (in ^ (st[j] & keepB)) & msk;   // lib.rs:182/186
-    L.v[i][j] ^= inv & (vhat ^ (tm & cvw[j]));
-    const uint32_t sx = L.s[i][j] ^ (st[j] & pm);         // lib.rs:177-178
-    const uint32_t sn = (sx & msk) ^ (tm & csw[j]);
-    L.s[i][j] = (am & sn) | (~am & L.s[i][j]);
-  }
-  const uint32_t tb = (d0 ^ (L.t[i] & (ct >> xb))) & 1u;  // lib.rs:179-180
-  L.t[i] = (am & tb) | (~am & L.t[i]);
-  L.ph[i] = adv ^ 1u;
-  uint32_t nl = L.lev[i] + adv;
-  L.cur[i] <<= adv;
-  if (adv && (nl & 31u) == 0u) stream_next_word<NS, true, MULTI>(L, i, nl, nlev, nbytes);
-  L.ci[i] += adv;
-  {  // reuse: level nl with B known (branch-free)
-    const uint32_t xb2 = L.cur[i] >> 31, t1 = L.t[i], tm1 = 0u - t1;
-    const uint32_t rm = 0u - (uint32_t)reuse, rr = rm & (0u - xb2);
-    const uint32_t cs2w[4] = {cs2.x, cs2.y, cs2.z, cs2.w};
-    const uint32_t cv2w[4] = {cv2.x, cv2.y, cv2.z, cv2.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
-      L.v[i][j] ^= rm & ((((xb2 ? ~L.s[i][j] : d[j]) & msk) ^ (tm1 & cv2w[j])));
-      L.s[i][j] ^= rr & tm1 & cs2w[j];
-    }
-    L.t[i] = rr ? ((d0 ^ (t1 & (ct2 >> 1))) & 1u) : L.t[i];
-    L.ph[i] = (reuse && !xb2) ? 1u : L.ph[i];
-    nl += rr & 1u;
-    L.cur[i] <<= (rr & 1u);
-    L.ci[i] += rr & 1u;
-    if (rr && (nl & 31u) == 0u) stream_next_word<NS, true, MULTI>(L, i, nl, nlev, nbytes);
-  }
-  L.lev[i] = nl;
-}
-
-template <uint32_t UNIT, int NBC>
-__device__ __forceinline__ void stream_run_skew(const uint32_t* lds, const uint4* __restrict__ rkg,
-                                                const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
-                                                const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
-                                                const uint4* __restrict__ s0s, const uint32_t party,
-                                                const uint8_t* __restrict__ xs, const uint64_t total,
-                                                uint32_t* __restrict__ ctr, uint4* __restrict__ ys,
-                                                const PrefixTable& pf) {
-  constexpr int NS = 2;
-  const uint32_t nbytes = NBC;
-  const uint32_t lc = lane_const();
-  const uint32_t nlev = 8u * nbytes;
-  const uint32_t total32 = (uint32_t)total;
-  const uint32_t nunits = (uint32_t)((total + UNIT - 1) / UNIT);
-  uint32_t unext = 0, uend = 0;
-  bool exhausted = false;
-  const uint4 s0v = s0s[0];
-  StreamLane<NS, true, false> L;
-#pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    L.fresh[i] = false;
-    L.alive[i] = false;
-    L.ci[i] = 0;
-    L.lev[i] = 0;
-    L.ph[i] = 0u;
-  }
-  const uint4 np1v = cw_np1[0];
-#pragma unroll
-  for (int i = 0; i < NS; ++i)
-    stream_refill<NS, true, false, UNIT, false, NBC>(L, i, true, unext, uend, exhausted, ctr, nunits, total32, s0s,
-                                                     s0v, party, xs, nbytes, 1, pf);
-  const uint4 k0 = rkg[0];
-  const uint32_t k0w[4] = {k0.x, k0.y, k0.z, k0.w};
-  uint4 cs[NS], cv[NS], cs2[NS], cv2[NS];
-  uint32_t ct[NS], ct2[NS], sv[NS][4];
-  bool mb[NS];
-  uint64_t nblk = 0;
-  // Stage A of stream p: its CWs (current and next level, for its update one half-step later)
-  // and its AES block; the CW loads are pinned after the AES so their wait lands there.
-  auto stage_a = [&](int p) {
-    nblk += (uint64_t)__popcll(__ballot(L.alive[p]));
-    const uint32_t lv = L.lev[p];
-    cs[p] = cw_s[lv];
-    cv[p] = cw_v[lv];
-    ct[p] = cw_t[lv];
-    mb[p] = L.alive[p] && L.ph[p] == 0u && L.t[p] == 0u && !L.fresh[p] && (L.cur[p] >> 31) != 0u && lv + 1u < nlev;
-    const uint32_t c2 = lv + (lv + 1u < nlev ? 1u : 0u);
-    cs2[p] = cw_s[c2];
-    cv2[p] = cw_v[c2];
-    ct2[p] = cw_t[c2];
-    const uint32_t inv = L.ph[p] - 1u;
-    uint32_t st[1][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) st[0][j] = xor3(L.s[p][j], inv, k0w[j]);  // round key 0 folded in
-    aes256_tt_gk<1, true>(st, rkg, lds, lc);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) sv[p][j] = st[0][j];
-  };
-  auto pin = [&](int p) {
-    asm volatile("" : "+v"(cs[p].x), "+v"(cs[p].y), "+v"(cs[p].z), "+v"(cs[p].w), "+v"(cv[p].x), "+v"(cv[p].y),
-                 "+v"(cv[p].z), "+v"(cv[p].w), "+v"(ct[p]));
-    asm volatile("" : "+v"(cs2[p].x), "+v"(cs2[p].y), "+v"(cs2[p].z), "+v"(cs2[p].w), "+v"(cv2[p].x),
-                 "+v"(cv2[p].y), "+v"(cv2[p].z), "+v"(cv2[p].w), "+v"(ct2[p]));
-  };
-  // Stage B of stream q: its update on the block stage A encrypted, then y and the refill.
-  auto stage_b = [&](int q) {
-    stream_update1<NS, false>(L, q, sv[q], cs[q], cv[q], ct[q], cs2[q], cv2[q], ct2[q], mb[q], nlev, nbytes);
-  };
-  auto finish = [&](int q) {
-    const bool done = L.alive[q] && L.lev[q] == nlev;
-    if (done) {
-      const uint32_t tm = 0u - L.t[q];  // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192)
-      ys[L.pt[q]] = make_uint4(L.v[q][0] ^ L.s[q][0] ^ (tm & np1v.x), L.v[q][1] ^ L.s[q][1] ^ (tm & np1v.y),
-                               L.v[q][2] ^ L.s[q][2] ^ (tm & np1v.z), L.v[q][3] ^ L.s[q][3] ^ (tm & np1v.w));
-    }
-    if (__ballot(done))
-      stream_refill<NS, true, false, UNIT, false, NBC>(L, q, done, unext, uend, exhausted, ctr, nunits, total32,
-                                                       s0s, s0v, party, xs, nbytes, 1, pf);
-  };
-  stage_a(0);
-  pin(0);
-  for (;;) {
-    if (!__ballot(L.alive[0] || L.alive[1])) break;
-    stage_a(1);  // stream 1's block ...
-    stage_b(0);  // ... beside stream 0's update (one basic block)
-    pin(1);
-    finish(0);
-    stage_a(0);
-    stage_b(1);
-    pin(0);
-    finish(1);
-  }
-  // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
-  if ((threadIdx.x & 63u) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, (unsigned long long)nblk);
-}
-
 // TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.
-#ifndef DCF_STREAM_SKEW
-#define DCF_STREAM_SKEW 0  // single key, x in registers, x width fixed: the skewed loop (stream_run_skew)
-#endif
 template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false, bool PFX = false, bool D48 = false,
           int NBC = 0>
 __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
@@ -865,13 +692,9 @@ __global__ __launch_bounds__(WG, 1) void k_eval16_stream(
   constexpr int SL = (MULTI && !TT2) ? DCF_MK_SL : -1;
   constexpr int SK = (MULTI && !TT2) ? DCF_MK_SK : 0;
   DCF_CLK(2, 0);
-  if constexpr (DCF_STREAM_SKEW && NS == 2 && XREG && !MULTI && !TT2 && !PFX && !D48 && NBC != 0 && GK &&
-                DCF_REFILL_ONCE && !DCF_REUSE_CHAIN)
-    stream_run_skew<kStreamUnit, NBC>(lds, rkg, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, total, ctr, ys, pf);
-  else
-    stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC, SK>(
-        lds, (GK || HK || SK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total,
-        ctr, ys, pf);
+  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC, SK>(
+      lds, (GK || HK || SK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total,
+      ctr, ys, pf);
   DCF_CLK(2, 1);
 }
 
