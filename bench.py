@@ -751,7 +751,11 @@ def run_fd(args, world, rank):
                                   f"party 0; replicas on {world} GPU(s)"},
            "roofline": {"bound": "lds", "engine": "ttable",
                         "kernel": ("k_fd_level16_mmo (8N launches)" if mmo
-                                   else "k_fd_level16 (8N-4 launches) + k_fd_dfs16<4>"),
+                                   else "k_prefix_build16 (levels 0..8N-5, one launch) + k_fd_dfs16<4, rows>"),
+                        # HBM bytes: every output written once, plus (Hirose) the level-(8N-4) table rows
+                        # written by the build and read back by the tail (32 B each)
+                        "traffic": npts * lam + (0 if mmo else 2 * 32 * (npts >> 4)),
+                        "traffic_source": "algorithmic bytes (no PMC profile of this launch shape)",
                         "achieved": blocks / kern_s / 1e9, "peak": peak / 1e9,
                         "measured_ceiling": None if mmo else measured_ceiling(blocks / kern_s),
                         "unit": f"G AES-{128 if mmo else 256} blocks/s", "frac": blocks / kern_s / peak, "kernel_ms": kern_s * 1e3,
