@@ -160,7 +160,8 @@ __global__ void k_cw_digest(const uint8_t* __restrict__ cw_s, const uint8_t* __r
 #endif
 #ifndef DCF_WHS_GK
 #define DCF_WHS_GK 0  // 1: round keys by buffer loads (vector L1) instead of LDS reads (C4 A/B: 38.4-38.5 vs 36.5 ms: the
-                      // key waits retire in order behind the CW loads)
+                      // key waits retire in order behind the CW loads); 2: both schedules by uniform loads, the lane's
+                      // key picked per word (r03f: 36.6-36.8 vs 35.3-35.4 ms, 56 more VALU per block)
 #endif
 // Single key `key` of a num_keys-key CWB; count <= 2^20 points per launch.
 template <int NS, bool MASK_HEAD, bool XREG, int WG = kBlock>
