@@ -587,3 +587,30 @@ def test_gen_batch_large_counter_path(dcf, nb):
     lt[has] = X[has, first[has]] < A[has, first[has]]
     rec = Y0 ^ Y1
     assert np.array_equal(rec[lt], B[lt]) and not rec[~lt].any()
+
+
+def test_wide_largest_n_and_beyond(dcf):
+    """LAMBDA >= 32 at the largest supported input, N = 31 (248 levels: the head's t-vector holds
+    rows 0..248 of its 256, the 63-chunk 4-bit tail), both parties vs the oracle; N = 32 is refused
+    with DCF_ERR_UNSUPPORTED (-7) rather than evaluated wrong.  Gen has no such limit."""
+    lam, m = 128, 64
+    rng = np.random.default_rng(0x31)
+    keys = [rng.bytes(32) for _ in range(18)]
+    prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    for nb in (31, 32):
+        d = dcf.DcfImpl(nb, lam, prg)
+        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+        ok = O.gen(P, alpha, beta, s0, s1, 0)
+        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
+        raw = ok.cw_s.tobytes() + ok.cw_v.tobytes() + ok.cw_t.tobytes()
+        assert dcf.share_to_cwb(k, nb, lam) == raw + bytes((-len(raw)) % 16) + ok.cw_np1.tobytes()
+        xs = _rand(rng, (m, nb))
+        xs[0] = np.frombuffer(alpha, np.uint8)
+        for b, s in ((0, s0), (1, s1)):
+            if nb == 31:
+                got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+                assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), b
+            else:
+                with pytest.raises(dcf.DcfError) as e:
+                    d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+                assert e.value.code == -7
