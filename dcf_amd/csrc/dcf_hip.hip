@@ -132,6 +132,8 @@ struct Workspace {
   size_t d_stage_bytes = 0;
   uint8_t* h_tiny = nullptr;  // small host calls: pinned, device-mapped, coherent (read/written by the kernel)
   size_t tiny_bytes = 0;
+  uint8_t* h_mid = nullptr;   // mid-size host evals: pinned, device-mapped, coarse-grained (x in, y out)
+  size_t mid_bytes = 0;
   // Ordering of the device work of successive leases (see above).
   hipEvent_t done = nullptr;
   hipStream_t done_stream = nullptr;
@@ -835,6 +837,7 @@ static void free_workspace(Workspace* w) {
     if (b) (void)hipFree(b);
   if (w->h_stage) (void)hipHostFree(w->h_stage);
   if (w->h_tiny) (void)hipHostFree(w->h_tiny);
+  if (w->h_mid) (void)hipHostFree(w->h_mid);
   for (hipStream_t s : w->hs)
     if (s) (void)hipStreamDestroy(s);
   for (hipEvent_t e : w->hev)
@@ -924,7 +927,7 @@ size_t dcf_prg_host_pinned_bytes(const dcf_prg* p) {
   if (!p) return 0;
   size_t b = 0;
   std::lock_guard<std::mutex> g(const_cast<dcf_prg*>(p)->pool_mu);
-  for (const Workspace* w : p->all_ws) b += w->h_stage_bytes + w->tiny_bytes;
+  for (const Workspace* w : p->all_ws) b += w->h_stage_bytes + w->tiny_bytes + w->mid_bytes;
   return b;
 }
 
@@ -1456,6 +1459,10 @@ constexpr size_t kHostChunkBytes = 128ull << 20;
 // Tiny host calls (the latency kernels' batch sizes): inputs and outputs through one pinned,
 // device-mapped buffer that the kernel reads and writes itself — one launch, no copy commands.
 constexpr size_t kTinyBytes = 1ull << 20;
+constexpr size_t kHostMidBytes = 64ull << 20;  // x + y of a mid-size host eval through the mapped buffer
+#ifndef DCF_HOST_MID
+#define DCF_HOST_MID 1
+#endif
 
 static int ensure_host_path(Workspace* w) {
   if (w->hs[0]) return DCF_OK;
@@ -1493,6 +1500,21 @@ static int ensure_tiny(Workspace* w, uint8_t** dptr) {
     w->tiny_bytes = kTinyBytes;
   }
   HIP_TRY(hipHostGetDevicePointer((void**)dptr, w->h_tiny, 0));
+  return DCF_OK;
+}
+
+// The mid-size host buffer: mapped into the device's address space, coarse-grained (the GPU may
+// cache it; the host reads the outputs only after the stream has passed the kernel).  Grown on
+// demand and kept.  Returns its device address.
+static int ensure_mid(Workspace* w, size_t bytes, uint8_t** dptr) {
+  if (w->mid_bytes < bytes) {
+    if (w->h_mid) HIP_TRY(hipHostFree(w->h_mid));
+    w->h_mid = nullptr;
+    w->mid_bytes = 0;
+    HIP_TRY(hipHostMalloc((void**)&w->h_mid, bytes, hipHostMallocMapped | hipHostMallocNonCoherent));
+    w->mid_bytes = bytes;
+  }
+  HIP_TRY(hipHostGetDevicePointer((void**)dptr, w->h_mid, 0));
   return DCF_OK;
 }
 
@@ -1545,6 +1567,29 @@ static int host_eval(dcf_prg* p, Lease& L, size_t nb, int party, const uint8_t* 
     if (int rc = eval_launch(p, L, nb, 1, m, party, d + ko, d + so0, d + xo, d + yo)) return rc;
     HIP_TRY(hipStreamSynchronize(L.st));
     memcpy(ys, h + yo, m * lam);
+    return DCF_OK;
+  }
+  // Mid-size batches (the small-batch kernels' range, LAMBDA = 16): the kernel reads x from and
+  // writes y to a mapped pinned buffer, so the call is one host copy in, a 4 KiB key copy, one
+  // launch, one stream sync and one host copy out — no staging DMAs or chunk events (a C1-size
+  // call is one chunk, its copies cannot overlap its kernel anyway).  The key goes to device
+  // memory first: the walk reads a correction word per level.
+  if (DCF_HOST_MID && lam == 16 && p->eval_mode == DCF_EVAL_AUTO && m < (uint64_t)p->cus * kBlock * 2 &&
+      m * (nb + lam) <= kHostMidBytes) {
+    const size_t kb = align256(cwb_len) + align256(lam);
+    const size_t mx = align256(m * nb), need = kb + mx + m * lam;
+    uint8_t* d = nullptr;
+    if (int rc = ensure_mid(w, need, &d)) return rc;
+    if (int rc = ensure_stage(w, 0, kb)) return rc;
+    uint8_t* h = w->h_mid;
+    memcpy(h, cwb, cwb_len);
+    memcpy(h + align256(cwb_len), s0, lam);
+    memcpy(h + kb, xs, m * nb);
+    HIP_TRY(hipMemcpyAsync(w->d_stage, h, kb, hipMemcpyHostToDevice, L.st));
+    if (int rc = eval_launch(p, L, nb, 1, m, party, w->d_stage, w->d_stage + align256(cwb_len), d + kb, d + kb + mx))
+      return rc;
+    HIP_TRY(hipStreamSynchronize(L.st));
+    memcpy(ys, h + kb + mx, m * lam);
     return DCF_OK;
   }
   w->host_streams = 7u;

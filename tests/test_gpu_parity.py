@@ -614,3 +614,29 @@ def test_wide_largest_n_and_beyond(dcf):
                 with pytest.raises(dcf.DcfError) as e:
                     d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
                 assert e.value.code == -7
+
+
+@pytest.mark.parametrize("nb,m", [(16, 3000), (4, 70_000), (16, 100_000), (2, 1000)])
+def test_host_mid_path_vs_device_and_oracle(dcf, nb, m):
+    """Auto mode, host buffers, a batch in the small-batch kernels' range: dcf_eval reads x from and
+    writes y to a mapped pinned buffer (no staging DMAs).  Both parties: equal to the device-resident
+    eval of the same points and, on a sample (every row at m <= 3000), to the oracle."""
+    import torch
+    rng = np.random.default_rng(0x1D + nb + m)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    d = dcf.DcfImpl(nb, 16, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
+    ok = O.gen(P, alpha, beta, s0, s1, 0)
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
+    cwb = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, nb, 16), np.uint8).copy()).cuda()
+    xs = _rand(rng, (m, nb))
+    xs[0] = np.frombuffer(alpha, np.uint8)
+    idx = np.arange(m) if m <= 3000 else np.concatenate([np.arange(1500), np.arange(m - 1500, m)])
+    for b, s in ((0, s0), (1, s1)):
+        got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+        dev = d.eval_device(bool(b), cwb, torch.from_numpy(np.frombuffer(s, np.uint8).copy()).cuda(),
+                            torch.from_numpy(xs).cuda())
+        torch.cuda.synchronize()
+        assert np.array_equal(got, dev.cpu().numpy()), b
+        assert np.array_equal(got[idx], O.eval_(P, b, ok, s, xs[idx], nthreads=8)), b
