@@ -982,6 +982,9 @@ int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priorit
 #ifndef DCF_EVAL_OCT_MAX
 #define DCF_EVAL_OCT_MAX 32768  // points (one key) up to which auto-mode eval runs k_eval16_oct
 #endif                          // (r03a sweep, us per device call: 32768 oct 187 vs pair 273; 100k 623 vs 485)
+#ifndef DCF_EVAL_ROW_MAX
+#define DCF_EVAL_ROW_MAX 8192   // points up to which auto-mode eval runs k_eval16_row (32 lanes per point)
+#endif
 #ifndef DCF_GEN_COL_MAX
 #define DCF_GEN_COL_MAX 16384   // keys up to which gen runs k_gen16_col (r03a: 4096 keys 232 vs 562 us quads)
 #endif
@@ -1158,6 +1161,16 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
   }
   const bool bs_ok = (num_keys == 1 && n_bytes <= 16);
   int mode = p->eval_mode;
+  if (mode == DCF_EVAL_AUTO && oct_eval(p, n_bytes, num_keys, total) && total <= (uint64_t)DCF_EVAL_ROW_MAX) {
+    // The smallest batches: 32 lanes per point, one table lookup per lane and AES round
+    // (k_eval16_row: a lone point's level is one 16-lane AES chain).
+    phase_mark(p, L, 1);
+    const uint32_t ppw = per_wg(total, p->cus, kBlock / 32);
+    hipLaunchKernelGGL(k_eval16_row, dim3((unsigned)((total + ppw - 1) / ppw)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], cwb, s0s, (uint32_t)party, xs, (uint32_t)n_bytes, ppw, (uint64_t)total, ys, w->d_ctr);
+    HIP_TRY(hipGetLastError());
+    return DCF_OK;
+  }
   if (mode == DCF_EVAL_AUTO && oct_eval(p, n_bytes, num_keys, total)) {
     // Tiny batches (a single point through the C ABI: benches/dcf.rs bench_eval) are latency-
     // bound: 8 lanes per point, one AES column each, A and B side by side (k_eval16_oct).

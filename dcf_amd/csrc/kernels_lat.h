@@ -74,6 +74,47 @@ __device__ __forceinline__ uint32_t aes256_col(uint32_t st, const uint32_t (&kw)
   return xor3(__builtin_amdgcn_perm(c, a, 0x0c0c0500u), __builtin_amdgcn_perm(e, d, 0x07020c0cu), kw[14]);
 }
 
+// AES-256 with a block on a 16-lane row, ONE table lookup per lane and round (k_eval16_row).
+// Layout A: lane p of the row holds column p&3 of the state; layout B: column p>>2.  From A,
+// lane p computes the term T_k[byte k of its column] of output column j = p>>2 (k = (p&3) - j):
+// the XOR over its quad is column j, so one round leaves layout B (FIPS-197 §5.1 T-table form,
+// out_j = T0[s_j.b0] ^ T1[s_{j+1}.b1] ^ T2[s_{j+2}.b2] ^ T3[s_{j+3}.b3] ^ rk_j); from B the
+// roles transpose and a stride-4 XOR over the row (row_ror 4, 8) returns to layout A.  Per
+// round: one v_perm address, one ds_read_b32, two DPP XORs and the round-key XOR — 7
+// instructions in one lane's dependent chain against aes256_col's 18; a lone wave pays ~10
+// cycles per dependent VALU and 64 per dependent LDS read on gfx950, so the block takes 1234
+// instead of 1692 cycles (scripts/micro/lat_chain.hip, profiles/r03v_lat_chain.json).
+// Fourteen lookup rounds leave layout A again; rkA[r] / rkB[r] = word p&3 / p>>2 of round key r.
+__device__ __forceinline__ uint32_t col16_sel(uint32_t k, uint32_t tbl) {  // lk()'s selector, k per lane
+  return ((tbl & 1u) ? 1u : 0u) | ((4u + k) << 8) | (((tbl >> 1) ? 2u : 0x0cu) << 16) | (0x0cu << 24);
+}
+__device__ __forceinline__ uint32_t aes256_col16(uint32_t st, const uint32_t (&rkA)[15], const uint32_t (&rkB)[15],
+                                                 const uint32_t* lds, uint32_t lc, uint32_t selA, uint32_t selB,
+                                                 uint32_t selF, uint32_t fmask) {
+  st ^= rkA[0];
+#pragma unroll
+  for (int r = 1; r < 14; ++r) {
+    const bool fromA = r & 1;
+    uint32_t x = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) +
+                                                    __builtin_amdgcn_perm(st, lc, fromA ? selA : selB));
+    if (fromA) {  // XOR over the quad: output column p>>2 (layout B)
+      x ^= dpp<1 | (0 << 2) | (3 << 4) | (2 << 6)>(x);
+      x ^= dpp<kQpRot2>(x);
+      st = x ^ rkB[r];
+    } else {      // XOR over lanes p, p-4, p-8, p-12: output column p&3 (layout A)
+      x ^= dpp<kRowRor4>(x);
+      x ^= dpp<kRowRor8>(x);
+      st = x ^ rkA[r];
+    }
+  }
+  // final round from layout B: SubBytes + ShiftRows (S(x) sits in byte k of T_{(k+2)&3}), the
+  // lane keeps byte k of its lookup; the row XOR assembles the column
+  uint32_t x = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + __builtin_amdgcn_perm(st, lc, selF)) & fmask;
+  x ^= dpp<kRowRor4>(x);
+  x ^= dpp<kRowRor8>(x);
+  return x ^ rkA[14];
+}
+
 // The 128 KiB replicated T-tables (lds_fill_tables' layout), every load of a thread issued
 // before its stores: a latency kernel cannot afford 32 dependent load/store round trips.
 constexpr int kFillPer = kLdsWords / kBlock;
@@ -181,6 +222,90 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_oct(
   }
   if (b == 0u)  // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), column j of point p0 + oct
     reinterpret_cast<uint32_t*>(ys)[(p0 + oct) * 4u + j] = v ^ s ^ ((0u - t) & np1);
+  DCF_CLK(3, 1);
+}
+
+// Dcf::eval (lib.rs:163-204) of one key at m points, 32 lanes per point: row 0 (lanes 0-15)
+// encrypts A = AES(s), row 1 B = AES(~s), each with aes256_col16; v_permlane16_swap hands
+// each row the other's block (gfx950: odd rows of the first operand trade places with even
+// rows of the second, so with x in both, the results hold row 0's and row 1's x in every
+// lane); every lane then runs the level update for its column (p & 3), t comes from column 0.
+// The tiny-batch kernel (auto mode, up to DCF_EVAL_ROW_MAX points): a lone point's level costs
+// one 16-lane AES chain instead of aes256_col's.  `ppw` points per workgroup (<= 32), spread
+// over the CUs like k_eval16_oct.  cwb / s0 / xs / ys may be host-mapped.
+__global__ __launch_bounds__(kBlock, 1) void k_eval16_row(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ cwb,
+    const uint8_t* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint32_t ppw, const uint64_t m, uint8_t* __restrict__ ys, uint32_t* __restrict__ ctr) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint4 key[2 * kColMaxLevels + kColMaxLevels / 16 + 2];  // cw_s | cw_v | cw_t | cw_np1
+  __shared__ uint8_t xsh[(kBlock / 32) * (kColMaxLevels / 8)];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint4*>(ctr) = make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t n = 8u * nbytes;
+  const uint64_t p0 = (uint64_t)blockIdx.x * ppw;
+  const uint32_t np = (uint32_t)min<uint64_t>(ppw, m - p0);
+  const uint32_t np1_off = (2u * n * 16u + n + 15u) & ~15u;
+  const uint32_t kq = np1_off / 16u + 1u;
+  // every load first, then every LDS store (k_eval16_oct's prologue)
+  uint32_t tv[kFillPer];
+  lds_fill_load(tv, tab);
+  const bool kl = threadIdx.x < kq, xl = threadIdx.x < np * nbytes;
+  const uint4 kv = kl ? reinterpret_cast<const uint4*>(cwb)[threadIdx.x] : make_uint4(0u, 0u, 0u, 0u);
+  const uint8_t xv = xl ? xs[p0 * nbytes + threadIdx.x] : (uint8_t)0;
+  lds_fill_store(lds, tv);
+  if (kl) key[threadIdx.x] = kv;
+  if (xl) xsh[threadIdx.x] = xv;
+  for (uint32_t i = threadIdx.x + blockDim.x; i < kq; i += blockDim.x) key[i] = reinterpret_cast<const uint4*>(cwb)[i];
+  __syncthreads();
+  DCF_CLK(3, 0);
+  const uint32_t lc = lane_const();
+  const uint32_t pt = threadIdx.x >> 5, p = threadIdx.x & 15u, a = p & 3u, bq = p >> 2;
+  if (pt >= np) return;  // whole points (two whole rows) leave together, after the only barrier
+  const uint32_t row = (threadIdx.x >> 4) & 1u;
+  // per-lane round-key words and lookup selectors (aes256_col16)
+  uint32_t rkA[15], rkB[15];
+#pragma unroll
+  for (int r = 0; r < 15; ++r) {
+    const uint32_t w0 = rk.w[4 * r], w1 = rk.w[4 * r + 1], w2 = rk.w[4 * r + 2], w3 = rk.w[4 * r + 3];
+    rkA[r] = (a & 2u) ? ((a & 1u) ? w3 : w2) : ((a & 1u) ? w1 : w0);
+    rkB[r] = (bq & 2u) ? ((bq & 1u) ? w3 : w2) : ((bq & 1u) ? w1 : w0);
+  }
+  const uint32_t kA = (a - bq) & 3u, kB = (bq - a) & 3u;
+  const uint32_t selA = col16_sel(kA, kA), selB = col16_sel(kB, kB), selF = col16_sel(kB, (kB + 2u) & 3u);
+  const uint32_t fmask = 0xFFu << (8u * kB);
+  const uint32_t* kcs = reinterpret_cast<const uint32_t*>(key);             // cw_s[l] word a: kcs[4l + a]
+  const uint32_t* kcv = kcs + 4u * n;                                        // cw_v
+  const uint8_t* kct = reinterpret_cast<const uint8_t*>(key) + 32u * n;     // cw_t[l]
+  const uint32_t np1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(key) + np1_off)[a];
+  const uint8_t* x = xsh + pt * nbytes;
+  const uint32_t inv = 0u - row;                                    // row 1 encrypts ~s (B)
+  const uint32_t msk = (a == 3u) ? kMaskLast : 0xFFFFFFFFu;         // clear bit 0 of byte 15 (prg.rs:65-68)
+  uint32_t s = reinterpret_cast<const uint32_t*>(s0)[a];            // k.s0s[0] (lib.rs:168)
+  uint32_t v = 0u, t = party, cur = 0u;
+  for (uint32_t lev = 0; lev < n; ++lev) {
+    if ((lev & 31u) == 0u) {  // next 32 bits of x, Msb0 (lib.rs:181)
+      const uint32_t c = lev >> 5;
+      uint32_t wv = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wv = (wv << 8) | (4u * c + k < nbytes ? (uint32_t)x[4u * c + k] : 0u);
+      cur = wv;
+    }
+    const uint32_t cs = kcs[4u * lev + a], cv = kcv[4u * lev + a], ct = kct[lev];
+    const uint32_t mine = aes256_col16(s ^ inv, rkA, rkB, lds, lc, selA, selB, selF, fmask);
+    const auto sw = __builtin_amdgcn_permlane16_swap(mine, mine, false, false);
+    const uint32_t A = sw[0], B = sw[1];  // row 0's block (A) and row 1's (B), column a, in every lane
+    const uint32_t xb = cur >> 31;
+    cur <<= 1;
+    const uint32_t keepA = xb - 1u, tm = 0u - t;
+    // t' = lsb(side)[0] ^ t & cw.t(side): column 0 holds byte 0 (lib.rs:179-180, 183/187)
+    const uint32_t tl = (A ^ s) & 1u, tr = (B ^ ~s) & 1u;
+    const uint32_t tn = dpp<kQpBcast0>((xb ? tr : tl) ^ (t & (ct >> xb) & 1u));
+    v ^= ((~s ^ (B & keepA)) & msk) ^ (tm & cv);   // v ^= v_hat(side) ^ t*cw.v   (lib.rs:182/186)
+    s = ((s ^ (A & keepA)) & msk) ^ (tm & cs);      // s' = s(side) ^ t*cw.s      (lib.rs:177-178)
+    t = tn;
+  }
+  if (row == 0u && p < 4u)  // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), column a of point p0 + pt
+    reinterpret_cast<uint32_t*>(ys)[(p0 + pt) * 4u + a] = v ^ s ^ ((0u - t) & np1);
   DCF_CLK(3, 1);
 }
 

@@ -1,5 +1,6 @@
 """CPU emulation of the latency kernels' lane algorithm (dcf_amd/csrc/kernels_lat.h) against
 the oracle: the per-lane column AES (DPP quad_perm rotations bring columns j+1..j+3), the
+16-lane-row AES of k_eval16_row (one lookup per lane, quad / stride-4 XOR reductions), the
 octet's A/B exchange (row_ror 4 / 12) and the gen row's block exchange (row_ror 4 / 8 / 12),
 with DPP semantics dst[i] = src[(i - n) mod 16] (row_ror:n) and dst[j] = src[sel[j]] within a
 quad (quad_perm).  This pins the lane decomposition on CPU; the GPU tests
@@ -221,3 +222,36 @@ def test_oct_and_col_lane_algorithm_vs_oracle():
                 got = oct_eval(rk, [bytes(r) for r in ok.cw_s], [bytes(r) for r in ok.cw_v], [int(c) for c in ok.cw_t],
                                bytes(ok.cw_np1), sp, party, xs)
                 assert [bytes(r) for r in want] == got
+
+
+def aes_col16(st, rk):
+    """aes256_col16 for one 16-lane row: lane p holds column p&3 of the block (layout A) on entry
+    and exit; DPP row_ror:n is dst[i] = src[(i - n) mod 16]."""
+    p = list(range(16))
+    a, b = [i & 3 for i in p], [i >> 2 for i in p]
+    kA, kB = [(a[i] - b[i]) & 3 for i in p], [(b[i] - a[i]) & 3 for i in p]
+    st = [st[i] ^ rk[a[i]] for i in p]
+    for r in range(1, 14):
+        if r & 1:  # from layout A: lane p looks up T_k[byte k] of its column for output column p>>2
+            x = [T[kA[i]][_byte(st[i], kA[i])] for i in p]
+            x = [x[i] ^ x[i ^ 1] for i in p]          # quad_perm [1,0,3,2]
+            x = [x[i] ^ x[i ^ 2] for i in p]          # quad_perm [2,3,0,1]
+            st = [x[i] ^ rk[4 * r + b[i]] for i in p]
+        else:      # from layout B: stride-4 reduction over the row
+            x = [T[kB[i]][_byte(st[i], kB[i])] for i in p]
+            x = [x[i] ^ x[(i - 4) % 16] for i in p]   # row_ror:4
+            x = [x[i] ^ x[(i - 8) % 16] for i in p]   # row_ror:8
+            st = [x[i] ^ rk[4 * r + a[i]] for i in p]
+    x = [T[(kB[i] + 2) & 3][_byte(st[i], kB[i])] & (0xFF << (8 * kB[i])) for i in p]
+    x = [x[i] ^ x[(i - 4) % 16] for i in p]
+    x = [x[i] ^ x[(i - 8) % 16] for i in p]
+    return [x[i] ^ rk[56 + a[i]] for i in p]
+
+
+def test_col16_aes_matches_fips197():
+    key = bytes(range(32))
+    pt = bytes.fromhex("00112233445566778899aabbccddeeff")
+    rk = _expand256(key)
+    out = aes_col16([int.from_bytes(pt[4 * (i & 3):4 * (i & 3) + 4], "little") for i in range(16)], rk)
+    for q in range(4):  # every quad holds the whole block
+        assert b"".join(w.to_bytes(4, "little") for w in out[4 * q:4 * q + 4]).hex() == "8ea2b7ca516745bfeafc49904b496089"

@@ -1,7 +1,8 @@
 """Latency kernels (kernels_lat.h: one AES column per lane) and concurrent use of one
 dcf_prg (include/dcf_hip.h "Threading"), on the GPU, byte-identical to the oracle.
 
-* k_eval16_oct (8 lanes per point) serves auto-mode single-key eval up to
+* k_eval16_row (32 lanes per point, one lookup per lane and round) serves auto-mode
+  single-key eval up to DCF_EVAL_ROW_MAX points and k_eval16_oct (8 lanes per point) up to
   DCF_EVAL_OCT_MAX points, through the device entry point and through the host entry
   point's tiny path (the kernel reads the key and points from, and writes the outputs
   to, mapped pinned memory); k_gen16_col (16 lanes per key) serves gen up to
@@ -36,7 +37,7 @@ def _T(b):
 
 
 @pytest.mark.parametrize("nb", [1, 3, 4, 16, 32])
-@pytest.mark.parametrize("m", [1, 2, 127, 128, 129, 2048])
+@pytest.mark.parametrize("m", [1, 2, 31, 33, 127, 128, 129, 2048, 12000])
 def test_oct_eval_vs_oracle(dcf, nb, m):
     import torch
     rng = np.random.default_rng(nb * 1000 + m)
@@ -50,6 +51,13 @@ def test_oct_eval_vs_oracle(dcf, nb, m):
     assert [cw.s for cw in k.cws] == [bytes(r) for r in ok.cw_s] and k.cw_np1 == bytes(ok.cw_np1)
     xs = rng.integers(0, 256, (m, nb), dtype=np.uint8)
     xs[0] = np.frombuffer(alpha, np.uint8)  # the boundary point itself
+    # bit patterns that drive each slot case of k_eval16_oct's schedule: runs of right steps
+    # (0xff), left steps (0x00), (R, L) pairs back to back (0xaa: the deferred-B queue full at
+    # every other pair), (L, R) (0x55), long runs ending at a word edge (0x0f / 0xf0), x ending
+    # in a right step (last level paired with a deferred B or alone)
+    pats = [b"\xff", b"\x00", b"\xaa", b"\x55", b"\x0f", b"\xf0", b"\x33", b"\xcc", b"\x01", b"\x80"]
+    for i, pt in enumerate(pats[:max(0, m - 1)]):
+        xs[1 + i] = np.frombuffer(pt * nb, np.uint8)
     cwb = dcf.share_to_cwb(k, nb, 16)
     for b, sb in ((0, s0), (1, s1)):
         want = O.eval_(P, b, ok, sb, xs, nthreads=CPU_THREADS)
