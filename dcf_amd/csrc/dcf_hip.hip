@@ -985,6 +985,9 @@ int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priorit
 #ifndef DCF_EVAL_ROW_MAX
 #define DCF_EVAL_ROW_MAX 8192   // points up to which auto-mode eval runs k_eval16_row (32 lanes per point)
 #endif
+#ifndef DCF_GEN_ROW_MAX
+#define DCF_GEN_ROW_MAX 1024    // keys up to which gen runs k_gen16_row (one wave per key; r03x: 1024 keys
+#endif                          // 125 vs 142 us col, 4096 keys 167 vs 147)
 #ifndef DCF_GEN_COL_MAX
 #define DCF_GEN_COL_MAX 16384   // keys up to which gen runs k_gen16_col (r03a: 4096 keys 232 vs 562 us quads)
 #endif
@@ -1042,6 +1045,16 @@ static int gen_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, con
                          cws, cwv, cwt, np1, w->d_ws);
       HIP_TRY(hipGetLastError());
     }
+    return DCF_OK;
+  }
+  if (col_gen(p, n_bytes, num_keys) && num_keys <= (uint64_t)DCF_GEN_ROW_MAX) {
+    // The smallest batches: one wave per key, one table lookup per lane and AES round
+    // (k_gen16_row: a lone key's level is one 16-lane AES chain).
+    const uint32_t kpw = per_wg(num_keys, p->cus, kBlock / 64);
+    hipLaunchKernelGGL(k_gen16_row, dim3((unsigned)((num_keys + kpw - 1) / kpw)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], alpha, beta, s0_0, s0_1, (uint32_t)bound, (uint32_t)n_bytes, kpw,
+                       (uint64_t)num_keys, cws, cwv, cwt, np1);
+    HIP_TRY(hipGetLastError());
     return DCF_OK;
   }
   if (col_gen(p, n_bytes, num_keys)) {
@@ -1559,7 +1572,7 @@ static int host_lease(Lease& L) {
 }
 
 // Dcf::eval over host buffers (caller: DeviceGuard held, arguments checked, m > 0).
-// Tiny batches: one launch of k_eval16_oct that reads the key and points from, and writes
+// Tiny batches: one launch of a latency kernel (k_eval16_row / k_eval16_oct) that reads the key and points from, and writes
 // the outputs to, the workspace's mapped pinned buffer.  Otherwise chunks of `chunk` points
 // flow through two staging slots on three streams: copy-in (pinned -> device), compute
 // (eval_launch), copy-out (device -> pinned); the host copies chunk c's x into pinned memory

@@ -386,4 +386,93 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16_col(
   if (q == 0u) reinterpret_cast<uint32_t*>(cw_np1)[k * 4u + j] = s0w ^ s1w ^ va;  // lib.rs:155
 }
 
+// Dcf::gen (lib.rs:86-161) of num_keys keys, one wave per key: row q (16 lanes) encrypts block q
+// of the level (A0, B0, A1, B1: prg.rs:42-73 on both parties' seeds, lib.rs:103-104) with
+// aes256_col16; v_permlane16_swap then v_permlane32_swap put column p&3 of all four blocks in
+// every lane, which runs k_gen16_col's level update (lib.rs:105-152) for its column.  The
+// tiny-batch gen (up to DCF_GEN_ROW_MAX keys), `kpw` keys per workgroup (<= 16).  Inputs and
+// the CWB output may be host-mapped.
+__global__ __launch_bounds__(kBlock, 1) void k_gen16_row(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ alpha,
+    const uint8_t* __restrict__ beta, const uint8_t* __restrict__ s0_0, const uint8_t* __restrict__ s0_1,
+    const uint32_t bound, const uint32_t nbytes, const uint32_t kpw, const uint64_t num_keys,
+    uint8_t* __restrict__ cw_s, uint8_t* __restrict__ cw_v, uint8_t* __restrict__ cw_t, uint8_t* __restrict__ cw_np1) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint8_t ash[(kBlock / 64) * (kColMaxLevels / 8)];
+  const uint32_t n = 8u * nbytes;
+  const uint64_t k0 = (uint64_t)blockIdx.x * kpw;
+  const uint32_t nk = (uint32_t)min<uint64_t>(kpw, num_keys - k0);
+  uint32_t tv[kFillPer];
+  lds_fill_load(tv, tab);
+  const bool al = threadIdx.x < nk * nbytes;
+  const uint8_t av = al ? alpha[k0 * nbytes + threadIdx.x] : (uint8_t)0;
+  lds_fill_store(lds, tv);
+  if (al) ash[threadIdx.x] = av;
+  __syncthreads();
+  const uint32_t lc = lane_const();
+  const uint32_t kk = threadIdx.x >> 6, q = (threadIdx.x >> 4) & 3u, p = threadIdx.x & 15u, a = p & 3u, bq = p >> 2;
+  if (kk >= nk) return;  // whole keys (whole waves) leave together, after the only barrier
+  const uint64_t k = k0 + kk;
+  uint32_t rkA[15], rkB[15];
+#pragma unroll
+  for (int r = 0; r < 15; ++r) {
+    const uint32_t w0 = rk.w[4 * r], w1 = rk.w[4 * r + 1], w2 = rk.w[4 * r + 2], w3 = rk.w[4 * r + 3];
+    rkA[r] = (a & 2u) ? ((a & 1u) ? w3 : w2) : ((a & 1u) ? w1 : w0);
+    rkB[r] = (bq & 2u) ? ((bq & 1u) ? w3 : w2) : ((bq & 1u) ? w1 : w0);
+  }
+  const uint32_t kA = (a - bq) & 3u, kB = (bq - a) & 3u;
+  const uint32_t selA = col16_sel(kA, kA), selB = col16_sel(kB, kB), selF = col16_sel(kB, (kB + 2u) & 3u);
+  const uint32_t fmask = 0xFFu << (8u * kB);
+  const uint32_t msk = (a == 3u) ? kMaskLast : 0xFFFFFFFFu;
+  uint32_t s0w = reinterpret_cast<const uint32_t*>(s0_0)[k * 4u + a];   // s0s[0] (lib.rs:98)
+  uint32_t s1w = reinterpret_cast<const uint32_t*>(s0_1)[k * 4u + a];   // s0s[1]
+  const uint32_t be = reinterpret_cast<const uint32_t*>(beta)[k * 4u + a];
+  uint32_t va = 0u, t0 = 0u, t1 = 1u, cur = 0u;  // lib.rs:99-100
+  const uint8_t* alk = ash + kk * nbytes;
+  const uint32_t inv = 0u - (q & 1u);            // blocks 1 and 3 encrypt ~s
+  for (uint32_t lev = 0; lev < n; ++lev) {
+    if ((lev & 31u) == 0u) {  // next 32 bits of alpha, Msb0 (lib.rs:106)
+      const uint32_t c = lev >> 5;
+      uint32_t wv = 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wv = (wv << 8) | (4u * c + e < nbytes ? (uint32_t)alk[4u * c + e] : 0u);
+      cur = wv;
+    }
+    const uint32_t mine = aes256_col16(((q >> 1) ? s1w : s0w) ^ inv, rkA, rkB, lds, lc, selA, selB, selF, fmask);
+    // rows (0,1) and (2,3) trade, then the wave halves: X[q] = column a of block q in every lane
+    const auto h = __builtin_amdgcn_permlane16_swap(mine, mine, false, false);  // {even row, odd row} of the pair
+    const auto e0 = __builtin_amdgcn_permlane32_swap(h[0], h[0], false, false);  // {A0, A1}
+    const auto e1 = __builtin_amdgcn_permlane32_swap(h[1], h[1], false, false);  // {B0, B1}
+    const uint32_t A0 = e0[0], A1 = e0[1], B0 = e1[0], B1 = e1[1];
+    const uint32_t ab = cur >> 31;  // alpha_i (lib.rs:106)
+    cur <<= 1;
+    const uint32_t am = 0u - ab;
+    const uint32_t bm = (bound == 0u) ? am : ~am;  // LtBeta: beta joins v_cw when alpha_i = 1 (lib.rs:114-125)
+    // PRG outputs per party: L = ((A^s)&M, (B^~s)&M), R = (s&M, ~s&M)
+    const uint32_t sl0 = (A0 ^ s0w) & msk, vl0 = (B0 ^ ~s0w) & msk, sr0 = s0w & msk, vr0 = ~s0w & msk;
+    const uint32_t sl1 = (A1 ^ s1w) & msk, vl1 = (B1 ^ ~s1w) & msk, sr1 = s1w & msk, vr1 = ~s1w & msk;
+    const uint32_t scw = (ab ? sl0 : sr0) ^ (ab ? sl1 : sr1);                       // lib.rs:112
+    const uint32_t vcw = (ab ? vl0 : vr0) ^ (ab ? vl1 : vr1) ^ va ^ (bm & be);      // lib.rs:113-125
+    va ^= (ab ? vr0 : vl0) ^ (ab ? vr1 : vl1) ^ vcw;                                 // lib.rs:126-129
+    // t bits from byte 0 (column 0 lanes), broadcast to the quad
+    const uint32_t tl0 = (A0 ^ s0w) & 1u, tr0 = (B0 ^ ~s0w) & 1u, tl1 = (A1 ^ s1w) & 1u, tr1 = (B1 ^ ~s1w) & 1u;
+    const uint32_t tlcw = tl0 ^ tl1 ^ ab ^ 1u, trcw = tr0 ^ tr1 ^ ab;  // lib.rs:130-131
+    const uint32_t tkcw = ab ? trcw : tlcw;
+    const uint32_t nt0 = (ab ? tr0 : tl0) ^ (t0 & tkcw), nt1 = (ab ? tr1 : tl1) ^ (t1 & tkcw);  // lib.rs:149-152
+    const uint32_t tp = dpp<kQpBcast0>(tlcw | (trcw << 1) | (nt0 << 2) | (nt1 << 3));
+    const uint32_t m0 = 0u - t0, m1 = 0u - t1;
+    s0w = (ab ? sr0 : sl0) ^ (m0 & scw);  // lib.rs:139-148
+    s1w = (ab ? sr1 : sl1) ^ (m1 & scw);
+    t0 = (tp >> 2) & 1u;
+    t1 = (tp >> 3) & 1u;
+    const uint64_t ci = (uint64_t)lev * num_keys + k;
+    if (p < 4u) {  // one quad per row stores: row 0 cw_s, row 1 cw_v, row 2 cw_t
+      if (q == 0u) reinterpret_cast<uint32_t*>(cw_s)[ci * 4u + a] = scw;
+      if (q == 1u) reinterpret_cast<uint32_t*>(cw_v)[ci * 4u + a] = vcw;
+      if (q == 2u && a == 0u) cw_t[ci] = (uint8_t)(tp & 3u);
+    }
+  }
+  if (q == 0u && p < 4u) reinterpret_cast<uint32_t*>(cw_np1)[k * 4u + a] = s0w ^ s1w ^ va;  // lib.rs:155
+}
+
 }  // namespace
