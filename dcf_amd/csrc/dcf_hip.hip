@@ -1532,12 +1532,16 @@ static int ensure_tiny(Workspace* w, uint8_t** dptr) {
 // The mid-size host buffer: mapped into the device's address space, coarse-grained (the GPU may
 // cache it; the host reads the outputs only after the stream has passed the kernel).  Grown on
 // demand and kept.  Returns its device address.
+#ifndef DCF_HOST_MID_COHERENT
+#define DCF_HOST_MID_COHERENT 0  // 1: fine-grained.  r03y2 C1 host path (3 runs): 143-148 vs 141-146 M evals/s,
+#endif                           // noise; buffer reuse with new x is tested for the default
 static int ensure_mid(Workspace* w, size_t bytes, uint8_t** dptr) {
   if (w->mid_bytes < bytes) {
     if (w->h_mid) HIP_TRY(hipHostFree(w->h_mid));
     w->h_mid = nullptr;
     w->mid_bytes = 0;
-    HIP_TRY(hipHostMalloc((void**)&w->h_mid, bytes, hipHostMallocMapped | hipHostMallocNonCoherent));
+    HIP_TRY(hipHostMalloc((void**)&w->h_mid, bytes,
+                          hipHostMallocMapped | (DCF_HOST_MID_COHERENT ? hipHostMallocCoherent : hipHostMallocNonCoherent)));
     w->mid_bytes = bytes;
   }
   HIP_TRY(hipHostGetDevicePointer((void**)dptr, w->h_mid, 0));

@@ -430,28 +430,38 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16_row(
   uint32_t va = 0u, t0 = 0u, t1 = 1u, cur = 0u;  // lib.rs:99-100
   const uint8_t* alk = ash + kk * nbytes;
   const uint32_t inv = 0u - (q & 1u);            // blocks 1 and 3 encrypt ~s
-  for (uint32_t lev = 0; lev < n; ++lev) {
-    if ((lev & 31u) == 0u) {  // next 32 bits of alpha, Msb0 (lib.rs:106)
-      const uint32_t c = lev >> 5;
-      uint32_t wv = 0u;
+  // Software-pipelined: a level's AES results feed only s' through scw (lib.rs:112, 139-148);
+  // the next level's AES starts right there, and this level's v / t / CW-store work (which the
+  // next level needs only after its AES) sits in the same basic block, so the compiler issues it
+  // in the lookups' LDS-latency gaps (a lone wave pays issue time for every instruction).  One
+  // extra AES runs after the last level.  The CW stores go from every lane (lanes of one column
+  // write the same word to the same address) so no branch splits the block.
+  auto alpha_word = [&](uint32_t c) {  // 32 bits of alpha from byte 4c, Msb0 (lib.rs:106)
+    uint32_t wv = 0u;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) wv = (wv << 8) | (4u * c + e < nbytes ? (uint32_t)alk[4u * c + e] : 0u);
-      cur = wv;
-    }
-    const uint32_t mine = aes256_col16(((q >> 1) ? s1w : s0w) ^ inv, rkA, rkB, lds, lc, selA, selB, selF, fmask);
+    for (int e = 0; e < 4; ++e) wv = (wv << 8) | (4u * c + e < nbytes ? (uint32_t)alk[4u * c + e] : 0u);
+    return wv;
+  };
+  cur = alpha_word(0);
+  uint32_t mine = aes256_col16(((q >> 1) ? s1w : s0w) ^ inv, rkA, rkB, lds, lc, selA, selB, selF, fmask);
+  for (uint32_t lev = 0; lev < n; ++lev) {
     // rows (0,1) and (2,3) trade, then the wave halves: X[q] = column a of block q in every lane
     const auto h = __builtin_amdgcn_permlane16_swap(mine, mine, false, false);  // {even row, odd row} of the pair
     const auto e0 = __builtin_amdgcn_permlane32_swap(h[0], h[0], false, false);  // {A0, A1}
     const auto e1 = __builtin_amdgcn_permlane32_swap(h[1], h[1], false, false);  // {B0, B1}
     const uint32_t A0 = e0[0], A1 = e0[1], B0 = e1[0], B1 = e1[1];
     const uint32_t ab = cur >> 31;  // alpha_i (lib.rs:106)
-    cur <<= 1;
+    // PRG outputs per party: L = ((A^s)&M, (B^~s)&M), R = (s&M, ~s&M)
+    const uint32_t sl0 = (A0 ^ s0w) & msk, sr0 = s0w & msk, sl1 = (A1 ^ s1w) & msk, sr1 = s1w & msk;
+    const uint32_t scw = (ab ? sl0 : sr0) ^ (ab ? sl1 : sr1);                       // lib.rs:112
+    const uint32_t m0 = 0u - t0, m1 = 0u - t1;
+    const uint32_t ns0 = (ab ? sr0 : sl0) ^ (m0 & scw);  // lib.rs:139-148
+    const uint32_t ns1 = (ab ? sr1 : sl1) ^ (m1 & scw);
+    mine = aes256_col16(((q >> 1) ? ns1 : ns0) ^ inv, rkA, rkB, lds, lc, selA, selB, selF, fmask);  // level lev+1
+    // --- the rest of level lev, off the chain
     const uint32_t am = 0u - ab;
     const uint32_t bm = (bound == 0u) ? am : ~am;  // LtBeta: beta joins v_cw when alpha_i = 1 (lib.rs:114-125)
-    // PRG outputs per party: L = ((A^s)&M, (B^~s)&M), R = (s&M, ~s&M)
-    const uint32_t sl0 = (A0 ^ s0w) & msk, vl0 = (B0 ^ ~s0w) & msk, sr0 = s0w & msk, vr0 = ~s0w & msk;
-    const uint32_t sl1 = (A1 ^ s1w) & msk, vl1 = (B1 ^ ~s1w) & msk, sr1 = s1w & msk, vr1 = ~s1w & msk;
-    const uint32_t scw = (ab ? sl0 : sr0) ^ (ab ? sl1 : sr1);                       // lib.rs:112
+    const uint32_t vl0 = (B0 ^ ~s0w) & msk, vr0 = ~s0w & msk, vl1 = (B1 ^ ~s1w) & msk, vr1 = ~s1w & msk;
     const uint32_t vcw = (ab ? vl0 : vr0) ^ (ab ? vl1 : vr1) ^ va ^ (bm & be);      // lib.rs:113-125
     va ^= (ab ? vr0 : vl0) ^ (ab ? vr1 : vl1) ^ vcw;                                 // lib.rs:126-129
     // t bits from byte 0 (column 0 lanes), broadcast to the quad
@@ -460,17 +470,16 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16_row(
     const uint32_t tkcw = ab ? trcw : tlcw;
     const uint32_t nt0 = (ab ? tr0 : tl0) ^ (t0 & tkcw), nt1 = (ab ? tr1 : tl1) ^ (t1 & tkcw);  // lib.rs:149-152
     const uint32_t tp = dpp<kQpBcast0>(tlcw | (trcw << 1) | (nt0 << 2) | (nt1 << 3));
-    const uint32_t m0 = 0u - t0, m1 = 0u - t1;
-    s0w = (ab ? sr0 : sl0) ^ (m0 & scw);  // lib.rs:139-148
-    s1w = (ab ? sr1 : sl1) ^ (m1 & scw);
     t0 = (tp >> 2) & 1u;
     t1 = (tp >> 3) & 1u;
+    s0w = ns0;
+    s1w = ns1;
     const uint64_t ci = (uint64_t)lev * num_keys + k;
-    if (p < 4u) {  // one quad per row stores: row 0 cw_s, row 1 cw_v, row 2 cw_t
-      if (q == 0u) reinterpret_cast<uint32_t*>(cw_s)[ci * 4u + a] = scw;
-      if (q == 1u) reinterpret_cast<uint32_t*>(cw_v)[ci * 4u + a] = vcw;
-      if (q == 2u && a == 0u) cw_t[ci] = (uint8_t)(tp & 3u);
-    }
+    reinterpret_cast<uint32_t*>(cw_s)[ci * 4u + a] = scw;
+    reinterpret_cast<uint32_t*>(cw_v)[ci * 4u + a] = vcw;
+    cw_t[ci] = (uint8_t)(tp & 3u);
+    cur <<= 1;
+    if (((lev + 1u) & 31u) == 0u) cur = alpha_word((lev + 1u) >> 5);
   }
   if (q == 0u && p < 4u) reinterpret_cast<uint32_t*>(cw_np1)[k * 4u + a] = s0w ^ s1w ^ va;  // lib.rs:155
 }

@@ -19,6 +19,7 @@
 __device__ __forceinline__ uint32_t sel_for(uint32_t k, uint32_t tbl) {
   return ((tbl & 1u) ? 1u : 0u) | ((4u + k) << 8) | (((tbl >> 1) ? 2u : 0x0cu) << 16) | (0x0cu << 24);
 }
+template <bool KEYXOR = true>
 __device__ __forceinline__ uint32_t aes256_col16(uint32_t st, const RoundKeys& rk, const uint32_t* lds, uint32_t lc) {
   const uint32_t p = threadIdx.x & 15u, a = p & 3u, b = p >> 2;
   const uint32_t kA = (a - b) & 3u, kB = (b - a) & 3u;
@@ -33,11 +34,11 @@ __device__ __forceinline__ uint32_t aes256_col16(uint32_t st, const RoundKeys& r
     if (fromA) {
       x ^= dpp<1 | (0 << 2) | (3 << 4) | (2 << 6)>(x);
       x ^= dpp<2 | (3 << 2) | (0 << 4) | (1 << 6)>(x);
-      st = x ^ rk.w[4 * r + b];
+      st = KEYXOR ? x ^ rk.w[4 * r + b] : x;
     } else {
       x ^= dpp<kRowRor4>(x);
       x ^= dpp<kRowRor8>(x);
-      st = x ^ rk.w[4 * r + a];
+      st = KEYXOR ? x ^ rk.w[4 * r + a] : x;
     }
   }
   uint32_t x = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + __builtin_amdgcn_perm(st, lc, sF)) & fm;
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(64, 1) void k_chain(const uint32_t* __restrict__ ta
   uint32_t kw[15];
   col_round_keys(rk, threadIdx.x & 3u, kw);
   uint32_t x = (MODE >= 3) ? ((threadIdx.x & 3u) + 1u) * 0x9E3779B9u : threadIdx.x * 0x9E3779B9u, y = 0x1234567u + threadIdx.x;
-  const bool on = (MODE == 0 || MODE == 5) ? threadIdx.x == 0 : (MODE == 3 ? threadIdx.x < 8 : (MODE == 6 ? threadIdx.x < 16 : true));
+  const bool on = (MODE == 0 || MODE == 5) ? threadIdx.x == 0 : (MODE == 3 ? threadIdx.x < 8 : ((MODE == 6 || MODE == 8) ? threadIdx.x < 16 : true));
   unsigned long long t0 = 0, t1 = 0;
   if (on) {
     t0 = __builtin_amdgcn_s_memtime();
@@ -77,6 +78,8 @@ __global__ __launch_bounds__(64, 1) void k_chain(const uint32_t* __restrict__ ta
         x = aes256_col(x, kw, lds, lc);
       } else if (MODE == 6 || MODE == 7) {
         x = aes256_col16(x, rk, lds, lc);
+      } else if (MODE == 8) {
+        x = aes256_col16<false>(x, rk, lds, lc);  // rounds 1-13 without the key XOR (not AES: timing only)
       } else {
         uint32_t st[1][4] = {{x, y, x ^ 1u, y ^ 2u}};
         aes256_tt<1>(st, rk, lds, lc);
@@ -126,6 +129,7 @@ int main() {
   bool same = true;
   for (int i = 0; i < 16; ++i) same &= got[i] == ref[i & 3];
   printf("\"aes_col16_matches_col\": %s, ", same ? "true" : "false");
+  printf("\"col16_without_round_key_xor_16lanes_cycles\": %.1f, ", run<8>(dtab, rk, out, cyc, 2000, 1));
   printf("\"aes_col16_64lanes_cycles\": %.1f, \"unit\": \"s_memtime ticks (shader clock)\"}\n",
          run<7>(dtab, rk, out, cyc, 2000, 1));
   return 0;

@@ -640,3 +640,12 @@ def test_host_mid_path_vs_device_and_oracle(dcf, nb, m):
         torch.cuda.synchronize()
         assert np.array_equal(got, dev.cpu().numpy()), b
         assert np.array_equal(got[idx], O.eval_(P, b, ok, s, xs[idx], nthreads=8)), b
+    # the same buffer refilled with other points right away (the kernel must not see the
+    # previous call's x through a cached line)
+    for rep in range(3):
+        xs2 = _rand(rng, (m, nb))
+        got2 = d.eval(False, dcf.Share([s0], k.cws, k.cw_np1), xs2)
+        dev2 = d.eval_device(False, cwb, torch.from_numpy(np.frombuffer(s0, np.uint8).copy()).cuda(),
+                             torch.from_numpy(xs2).cuda())
+        torch.cuda.synchronize()
+        assert np.array_equal(got2, dev2.cpu().numpy()), rep
