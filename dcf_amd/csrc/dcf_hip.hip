@@ -1226,18 +1226,14 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
 #define DCF_SMALL(MODE)                                                                                           \
   hipLaunchKernelGGL(k_eval16_pair<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,                  \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk,  \
-                     (uint4*)ys, p->d_rk0, (MODE == 0 || MODE == 3) ? spf : PrefixTable{nullptr, 0u})
+                     (uint4*)ys, p->d_rk0, MODE == 0 ? spf : PrefixTable{nullptr, 0u})
 #else
 #define DCF_SMALL(MODE)                                                                                           \
   hipLaunchKernelGGL(k_eval16<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s,    \
                      (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk, (uint4*)ys,          \
                      (uint32_t*)nullptr)
 #endif
-#ifndef DCF_PAIR_KEYLDS
-#define DCF_PAIR_KEYLDS 0
-#endif
-    if (num_keys == 1 && DCF_SMALL_PAIR && DCF_PAIR_KEYLDS && 8 * n_bytes <= kPairKeyLevels) DCF_SMALL(3);
-    else if (num_keys == 1) DCF_SMALL(0);
+    if (num_keys == 1) DCF_SMALL(0);
     else if (ppk % 64 == 0) DCF_SMALL(1);
     else DCF_SMALL(2);
 #undef DCF_SMALL

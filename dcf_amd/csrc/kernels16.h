@@ -162,7 +162,6 @@ __device__ __forceinline__ void prefix_row(const PrefixTable& pf, uint32_t idx, 
 // with half the AES work per level: a small batch has too few waves per SIMD to
 // overlap the LDS lookups with the rest (C1: 7 waves per CU with one lane per point).
 constexpr int kQpSwap1 = 1 | (0 << 2) | (3 << 4) | (2 << 6);
-constexpr uint32_t kPairKeyLevels = 256;  // k_eval16_pair<3>: CWs of N <= 32 staged in LDS
 #ifndef DCF_PAIR_GK
 #define DCF_PAIR_GK 1
 #endif
@@ -241,26 +240,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_pair(
     const uint64_t num_keys, const uint64_t points_per_key, uint4* __restrict__ ys,
     const uint4* __restrict__ rkg, const PrefixTable pf) {
   __shared__ uint32_t lds[kLdsWords];
-  // MODE 3: one key of at most kPairKeyLevels levels, its CWs staged in LDS beside the tables:
-  // the per-level cw reads are LDS reads issued ahead of the AES instead of global loads whose
-  // latency the in-order vmcnt exposes after it (C1)
-  __shared__ uint4 kst[MODE == 3 ? 2 * kPairKeyLevels + kPairKeyLevels / 16 : 1];
-  const uint4* ks = cw_s;
-  const uint4* kv = cw_v;
-  const uint8_t* kt = cw_t;
-  if (MODE == 3) {
-    const uint32_t n = 8u * nbytes;
-    uint8_t* t8 = reinterpret_cast<uint8_t*>(kst + 2u * n);
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      kst[i] = cw_s[i];
-      kst[n + i] = cw_v[i];
-      t8[i] = cw_t[i];
-    }
-    ks = kst;
-    kv = kst + n;
-    kt = t8;
-  }
-  lds_fill_tables(lds, tab);  // ends with the barrier
+  lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
   const uint64_t total = num_keys * points_per_key;
   const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 1);
@@ -272,7 +252,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_pair(
     if (MODE == 1) key = __builtin_amdgcn_readfirstlane((uint32_t)(gg / points_per_key));
     if (MODE == 2) key = gg / points_per_key;
     const uint32_t odd = threadIdx.x & 1u;
-    const uint4 y = tt_eval_pair(lds, lc, rk, ks, kv, kt, cw_np1[key], s0s[key], party, xs + gg * nbytes,
+    const uint4 y = tt_eval_pair(lds, lc, rk, cw_s, cw_v, cw_t, cw_np1[key], s0s[key], party, xs + gg * nbytes,
                                  nbytes, num_keys, key, odd, rkg, pf);
     if (live && !odd) ys[g] = y;
   }
