@@ -986,8 +986,8 @@ int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priorit
 #define DCF_EVAL_ROW_MAX 8192   // points up to which auto-mode eval runs k_eval16_row (32 lanes per point)
 #endif
 #ifndef DCF_GEN_ROW_MAX
-#define DCF_GEN_ROW_MAX 1024    // keys up to which gen runs k_gen16_row (one wave per key; r03x: 1024 keys
-#endif                          // 125 vs 142 us col, 4096 keys 167 vs 147)
+#define DCF_GEN_ROW_MAX 2048    // keys up to which gen runs k_gen16_row (one wave per key; pipelined, r03t3:
+#endif                          // 2048 keys 110 vs 148 us col, 4096 keys 149 vs 147, 8192 277 vs 165)
 #ifndef DCF_GEN_COL_MAX
 #define DCF_GEN_COL_MAX 16384   // keys up to which gen runs k_gen16_col (r03a: 4096 keys 232 vs 562 us quads)
 #endif

@@ -1,5 +1,6 @@
 """Per-call time of device-resident single-key evals around DCF_EVAL_ROW_MAX (k_eval16_row vs
-k_eval16_oct): DCF_HIP_LIB=... python scripts/row_threshold.py -> one JSON line {m: us}."""
+k_eval16_oct) and of batched gens around DCF_GEN_ROW_MAX (k_gen16_row vs k_gen16_col):
+DCF_HIP_LIB=... python scripts/row_threshold.py [gen] -> one JSON line {m: us}."""
 import json
 import os
 import sys
@@ -20,6 +21,20 @@ def main():
     cwb = torch.from_numpy(np.frombuffer(dcf_amd.share_to_cwb(k, 16, 16), np.uint8).copy()).cuda()
     s0 = torch.from_numpy(np.frombuffer(k.s0s[0], np.uint8).copy()).cuda()
     out = {}
+    if len(sys.argv) > 1 and sys.argv[1] == "gen":
+        for K in (512, 1024, 2048, 4096, 8192):
+            a, b, c, e = (torch.randint(0, 256, (K, 16), dtype=torch.uint8, device="cuda") for _ in range(4))
+            o = torch.empty(dcf_amd.cwb_bytes(16, 16, K), dtype=torch.uint8, device="cuda")
+            for _ in range(20):
+                d.gen_batch_device(a, b, c, e, dcf_amd.BoundState.LtBeta, o)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(200):
+                d.gen_batch_device(a, b, c, e, dcf_amd.BoundState.LtBeta, o)
+                torch.cuda.synchronize()
+            out[K] = (time.perf_counter() - t0) / 200 * 1e6
+        print(json.dumps({"lib": os.environ.get("DCF_HIP_LIB", "default"), "gen_us": out}), flush=True)
+        return
     for m in (4096, 8192, 12000, 16384, 24576, 32768):
         xs = torch.randint(0, 256, (m, 16), dtype=torch.uint8, device="cuda")
         ys = torch.empty((m, 16), dtype=torch.uint8, device="cuda")

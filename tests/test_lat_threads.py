@@ -69,7 +69,7 @@ def test_oct_eval_vs_oracle(dcf, nb, m):
 
 
 @pytest.mark.parametrize("nb", [1, 2, 16, 32])
-@pytest.mark.parametrize("K", [1, 5, 64, 65, 1024, 1025, 5000])
+@pytest.mark.parametrize("K", [1, 5, 64, 65, 1024, 2048, 2049, 5000])
 def test_col_gen_vs_oracle(dcf, nb, K):
     import torch
     rng = np.random.default_rng(nb * 7919 + K)
