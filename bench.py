@@ -153,12 +153,20 @@ def zero_bits(xs: torch.Tensor, skip_bits: int = 0) -> int:
     return tot
 
 
-def dist_setup(n_gpus: int, backend: str = "nccl"):
+def dist_setup(n_gpus: int, backend: str = "nccl", force: bool = False):
+    """One process per GPU.  A process group comes up for WORLD_SIZE > 1, and also at world
+    size 1 with `force` (--force-dist): then the key broadcast, the per-rank all_gather_object
+    and the timing all-reduce run through the backend (RCCL for nccl) exactly as at N > 1."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world != n_gpus:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    if world > 1 or force:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         # one rank per GPU; with --dist-backend gloo several ranks may share a device (a
         # rehearsal of the multi-rank path on a one-GPU box)
         dev = local % max(1, torch.cuda.device_count())
@@ -169,9 +177,19 @@ def dist_setup(n_gpus: int, backend: str = "nccl"):
             dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
-    if world != n_gpus:
-        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
     return world, rank, local
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def pg() -> bool:
+    """A process group is up (N > 1, or N = 1 with --force-dist)."""
+    return dist.is_initialized()
 
 
 def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int, timing: dict = None):
@@ -182,12 +200,12 @@ def make_key(d: dcf_amd.DcfImpl, n_bytes: int, lam: int, world: int, seed: int, 
     alpha, beta, s0, s1 = rng.bytes(n_bytes), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
     cwb = torch.empty(dcf_amd.cwb_bytes(n_bytes, lam, 1), dtype=torch.uint8, device=dev)
     seeds = torch.empty((2, lam), dtype=torch.uint8, device=dev)
-    if not world > 1 or dist.get_rank() == 0:
+    if not pg() or dist.get_rank() == 0:
         k = d.gen(dcf_amd.CmpFn(alpha, beta), [s0, s1], dcf_amd.BoundState.LtBeta)
         cwb.copy_(torch.from_numpy(np.frombuffer(dcf_amd.share_to_cwb(k, n_bytes, lam), np.uint8).copy()))
         seeds.copy_(torch.from_numpy(np.frombuffer(s0 + s1, np.uint8).reshape(2, lam).copy()))
     torch.cuda.synchronize()
-    if world > 1:
+    if pg():
         dist.barrier()
     t0 = time.perf_counter()
     broadcast_key([cwb, seeds], src=0)
@@ -269,7 +287,7 @@ def timed_loop(step, steps: int, warmup: int, world: int, stream=None, local: di
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if pg():
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -279,7 +297,7 @@ def timed_loop(step, steps: int, warmup: int, world: int, stream=None, local: di
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg():
         dist.barrier()
     torch.cuda.synchronize()
     w = time.perf_counter() - t0
@@ -287,7 +305,7 @@ def timed_loop(step, steps: int, warmup: int, world: int, stream=None, local: di
     if local is not None:
         local.update(wall_s=w, event_s_per_step=k)
     t = torch.tensor([w], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if pg():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item()), k
 
@@ -295,7 +313,7 @@ def timed_loop(step, steps: int, warmup: int, world: int, stream=None, local: di
 def gather_per_rank(world: int, rec: dict):
     """Every rank's measurement record on rank 0 (all_gather_object: small host objects, outside
     the timed region); [rec] at N = 1."""
-    if world == 1:
+    if not pg():
         return [rec]
     out = [None] * world
     dist.all_gather_object(out, rec)
@@ -496,7 +514,7 @@ def run_eval(args, world, rank):
         out["slice_check"] = check
     out["phases"] = {"table_ms": table_ms, "walk_ms": walk_ms, "prefix_levels": depth,
                      "note": "rank 0, one untimed eval with phase events (dcf_prg_set_phase_timing)"}
-    if world > 1:
+    if pg():
         out["per_rank"] = per_rank_summary(per_rank, args.steps)
         out["key_broadcast"] = {"ms": ktime.get("key_broadcast_ms"), "bytes": ktime.get("key_bytes"),
                                 "backend": args.dist_backend, "note": "once, before timing (outside the timed region)"}
@@ -535,7 +553,7 @@ def slice_check(d, cwb, s0, ys, nb, lam, args, world, rank):
     """Multi-rank self-check: every rank's output digest goes to rank 0, which regenerates each
     rank's slice of points, evaluates it itself and compares."""
     digs = [ys_digest(ys)]
-    if world > 1:  # all_gather_object: gloo's all_gather takes host tensors only
+    if pg():  # all_gather_object: gloo's all_gather takes host tensors only
         digs = [None] * world
         dist.all_gather_object(digs, ys_digest(ys))
     if rank != 0:
@@ -642,7 +660,7 @@ def run_c5(args, world, rank):
                         "note": "gen: 4 AES-256 blocks per level per key (k_gen16); eval: blocks the multi-key "
                                 "stream engine encrypts, counted on the device (B every level, A on left levels, "
                                 "minus reused B); peak = T-table LDS bound 87.8 G blocks/s"}}
-    if world > 1:
+    if pg():
         recs = gather_per_rank(world, {"rank": rank, "keys": K, "key_start": kstart, "wall_s": mine["wall_s"],
                                        "kernel_ms": step_s * 1e3, "gen_ms": phase[0] * 1e3,
                                        "eval_ms": (phase[1] + phase[2]) * 1e3})
@@ -720,7 +738,7 @@ def run_fd(args, world, rank):
     for _ in range(args.warmup):
         d.eval_full_domain_device(False, cwb, s0, ys)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg():
         dist.barrier()
     stream = torch.cuda.current_stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -730,12 +748,12 @@ def run_fd(args, world, rank):
         d.eval_full_domain_device(False, cwb, s0, ys)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg():
         dist.barrier()
     wall = time.perf_counter() - t0
     kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
     t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if pg():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
     value = npts * world * args.steps / wall
@@ -897,6 +915,9 @@ def main():
                     help="also time dcf_eval on host buffers (PCIe included; always on for c1)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="bring the process group up at N = 1 too (RCCL key broadcast, per-rank gather, "
+                         "timing all-reduce run as at N > 1)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 re-evaluates every rank's slice and compares output digests")
     args = ap.parse_args()
@@ -918,7 +939,7 @@ def main():
     else:
         args.n_bytes = args.n_bytes or 16
         args.points = args.points or (1 << 28)
-    world, rank, _ = dist_setup(args.gpus, args.dist_backend)
+    world, rank, _ = dist_setup(args.gpus, args.dist_backend, args.force_dist)
     if args.workload == "lat":
         out = run_latency(args, world, rank)
     elif args.workload == "c5":
@@ -932,7 +953,7 @@ def main():
                          "(not the BASELINE.json headline config)")
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg():
         dist.barrier()
         dist.destroy_process_group()
 

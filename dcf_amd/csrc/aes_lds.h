@@ -122,24 +122,11 @@ struct Sel {
       ((T & 1) ? 1u : 0u) | ((4u + K) << 8) | (((T >> 1) ? 2u : 0x0cu) << 16) | (0x0cu << 24);
 };
 
-#ifndef DCF_T1_BITOP3
-// 1: T1 lookups of the middle rounds address through v_bitop3 instead of v_perm.  Same bytes;
-// A/B (ab_t1, same box, 2 runs, M evals/s): C3 541.8 vs 540.8, C2 4124 vs 4113, C5 397.3 vs
-// 395.2, FD 37496 vs 37557, C4 103.4 vs 104.6, C1 195.4 vs 197.7 — noise: the loops sit at the
-// LDS-issue ceiling of the T-table rounds (scripts/micro/aes_rate.hip: 74.6 vs 75.2 G blocks/s).
-#define DCF_T1_BITOP3 0
-#endif
 template <int T, int K>
 __device__ __forceinline__ uint32_t lk(const uint32_t* lds, uint32_t w, uint32_t lc) {
-  uint32_t addr;
-  if (DCF_T1_BITOP3 && T == 1 && K == 1) {
-    // T1 takes state byte 1, which already sits at address bits 8..15: the address is
-    // (w & 0xFF00) | (T1's lane bits), one v_bitop3 (2 cycles per wave64 on gfx950) instead
-    // of a v_perm (4 cycles).  (lc >> 8) & 0xFF is loop-invariant: the compiler hoists it.
-    addr = __builtin_amdgcn_bitop3_b32(w, 0xFF00u, (lc >> 8) & 0xFFu, 0xEA);  // (a & b) | c
-  } else {
-    addr = __builtin_amdgcn_perm(w, lc, Sel<T, K>::v);
-  }
+  // (T1's address through one v_bitop3 instead of the v_perm measured the same: the rounds sit at
+  // the LDS-issue ceiling, AB_LOG ab_t1)
+  const uint32_t addr = __builtin_amdgcn_perm(w, lc, Sel<T, K>::v);
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + addr);
 }
 
@@ -252,104 +239,6 @@ __device__ __forceinline__ void aes_tt_lka(uint32_t (&st)[NB][4], const uint32_t
   }
 }
 
-// NB independent AES-NR encryptions, each under the schedule at byte offset ko[b] of a buffer
-// (round key r at ko[b] + 16 r; lanes may pick different schedules), read through the vector
-// L1 by one buffer_load_dwordx4 per round and block, AHEAD rounds before its use, instead of
-// an LDS read: the LDS serves only the T-table lookups.  kq[b][(r - 1) % AHEAD] holds round
-// key r; the caller has loaded keys 1 .. AHEAD - 1 and XORed key 0 into st.  ko is
-// "redefined" by an empty asm after each round's state, so the compiler cannot hoist the loads
-// (the offset 16 r rides in the instruction).
-template <int NR, int NB, int AHEAD>
-__device__ __forceinline__ void aes_tt_bk(uint32_t (&st)[NB][4], uint32_t (&ko)[NB], __amdgpu_buffer_rsrc_t rs,
-                                          uint4 (&kq)[NB][AHEAD], const uint32_t* lds, uint32_t lc) {
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-#pragma unroll
-  for (int r = 1; r <= NR; ++r) {
-    uint32_t o[NB][4];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int rn = r + AHEAD - 1;  // the round whose key is loaded now
-      if (rn <= NR) {
-        asm volatile("" : "+v"(ko[b]) : "v"(st[b][0]));
-        const v4u k = __builtin_amdgcn_raw_buffer_load_b128(rs, ko[b] + 16u * rn, 0, 0);
-        kq[b][(rn - 1) % AHEAD] = make_uint4(k.x, k.y, k.z, k.w);
-      }
-      const uint4 k = kq[b][(r - 1) % AHEAD];
-      const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (r < NR) {
-          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
-          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
-        } else {  // final round: S(x) sits in byte r of T_{(r+2)&3}
-          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
-          o[b][j] = xor3(__builtin_amdgcn_perm(c, a, 0x0c0c0500u), __builtin_amdgcn_perm(e, d, 0x07020c0cu), kw[j]);
-        }
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
-  }
-}
-
-// NB independent AES-NR encryptions, block b under schedule A (hm[b] = 0) or schedule B
-// (hm[b] = ~0).  Both schedules' round keys come by uniform global loads (one address per
-// wave: a single vector-L1 request, unlike aes_tt_bk's per-lane offsets), AHEAD rounds before
-// their use, and each lane picks its word with one v_bitop3.  qa / qb[(r - 1) % AHEAD] hold
-// round key r; the caller has loaded keys 1 .. AHEAD - 1 and XORed key 0 into st.
-template <int NR, int NB, int AHEAD>
-__device__ __forceinline__ void aes_tt_gk2(uint32_t (&st)[NB][4], const uint32_t (&hm)[NB],
-                                           const uint4* __restrict__ ka, const uint4* __restrict__ kb,
-                                           uint4 (&qa)[AHEAD], uint4 (&qb)[AHEAD], const uint32_t* lds, uint32_t lc) {
-  uint32_t zb = 0u;
-#pragma unroll
-  for (int r = 1; r <= NR; ++r) {
-    // zb: a zero "redefined" after the previous round's state, so the loads stay AHEAD rounds
-    // ahead instead of being hoisted into 2 (NR + 1) live keys
-    asm volatile("" : "+v"(zb) : "v"(st[0][0]), "v"(st[NB - 1][0]));
-    const int rn = r + AHEAD - 1;
-    if (rn <= NR) {
-      qa[(rn - 1) % AHEAD] = ka[rn + zb];
-      qb[(rn - 1) % AHEAD] = kb[rn + zb];
-    }
-    const uint4 a4 = qa[(r - 1) % AHEAD], b4 = qb[(r - 1) % AHEAD];
-    const uint32_t aw[4] = {a4.x, a4.y, a4.z, a4.w}, bw[4] = {b4.x, b4.y, b4.z, b4.w};
-    uint32_t o[NB][4];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t kw = __builtin_amdgcn_bitop3_b32(hm[b], bw[j], aw[j], 0xCA);  // hm ? B : A
-        if (r < NR) {
-          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
-          o[b][j] = xor3(xor3(a, c, d), e, kw);
-        } else {  // final round: S(x) sits in byte r of T_{(r+2)&3}
-          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
-          o[b][j] = xor3(__builtin_amdgcn_perm(c, a, 0x0c0c0500u), __builtin_amdgcn_perm(e, d, 0x07020c0cu), kw);
-        }
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
-  }
-}
-
 // NB independent AES encryptions with NR rounds (10: AES-128, 14: AES-256), each
 // under its own key schedule read from LDS: rk[b] points at NR + 1 uint4 round
 // keys (per lane, so a lane may pick its schedule; lanes reading the same
@@ -428,218 +317,19 @@ __device__ __forceinline__ void aes256_tt_gk(uint32_t (&st)[NB][4], const uint4*
       st[b][0] ^= k.x; st[b][1] ^= k.y; st[b][2] ^= k.z; st[b][3] ^= k.w;
     }
   }
-#ifndef DCF_GK_AHEAD
-#define DCF_GK_AHEAD 3  // rounds between a key's load and its use (r01o A/B on C3: 1 -1.2 %, 2 +2.2 %,
-                        // 3 +3.6 %, 4 +3.1 %, 6 -12 % vs SGPR keys)
-#endif
-  uint4 kq[DCF_GK_AHEAD];
+  // rounds between a key's load and its use (r01o A/B on C3: 1 -1.2 %, 2 +2.2 %, 3 +3.6 %, 4 +3.1 %,
+  // 6 -12 % vs SGPR keys)
+  constexpr int AH = 3;
+  uint4 kq[AH];
 #pragma unroll
-  for (int q = 0; q < DCF_GK_AHEAD - 1; ++q) kq[q] = *reinterpret_cast<const uint4*>(base + 16 * (q + 1));
+  for (int q = 0; q < AH - 1; ++q) kq[q] = *reinterpret_cast<const uint4*>(base + 16 * (q + 1));
 #pragma unroll
   for (int r = 1; r < 15; ++r) {
     asm volatile("" : "+v"(zb) : "v"(st[0][0]), "v"(st[NB - 1][0]));
-    const int rn = r + DCF_GK_AHEAD - 1;  // the round whose key is loaded now
-    if (rn < 15) kq[(rn - 1) % DCF_GK_AHEAD] = *reinterpret_cast<const uint4*>(base + zb + 16 * rn);
-    const uint4 k = kq[(r - 1) % DCF_GK_AHEAD];
+    const int rn = r + AH - 1;  // the round whose key is loaded now
+    if (rn < 15) kq[(rn - 1) % AH] = *reinterpret_cast<const uint4*>(base + zb + 16 * rn);
+    const uint4 k = kq[(r - 1) % AH];
     const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
-    uint32_t o[NB][4];
-    if (r < 14) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
-          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
-        }
-    } else {
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
-          const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
-          const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
-          o[b][j] = xor3(lo, hi, kw[j]);
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
-  }
-}
-
-// AES-256 with round keys read per round by scalar loads (s_load_dwordx4 through the scalar
-// cache) from the device copy of the schedule, AHEAD rounds before use: 4 * AHEAD SGPRs of
-// keys instead of 60, and no vector-memory traffic (the multi-key stream kernel's CW digest
-// loads keep vmcnt to themselves).  The address is base + zs + 16 r with zs a zero that an
-// empty asm redefines after each round's state, so the compiler cannot hoist the loads.
-// Scalar loads count in lgkmcnt with the LDS reads and return out of order, so a key's first
-// use waits lgkmcnt(0): issued AHEAD rounds early it has long landed by then.
-template <int NB, int AHEAD = 2>
-__device__ __forceinline__ void aes256_tt_sk(uint32_t (&st)[NB][4], const uint4* __restrict__ rkg,
-                                             const uint32_t* lds, uint32_t lc) {
-  const char* base = reinterpret_cast<const char*>(rkg);
-  uint4 kq[AHEAD];
-  {
-    const uint4 k = rkg[0];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      st[b][0] ^= k.x; st[b][1] ^= k.y; st[b][2] ^= k.z; st[b][3] ^= k.w;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < AHEAD - 1; ++q) kq[q] = rkg[q + 1];
-#pragma unroll
-  for (int r = 1; r < 15; ++r) {
-    uint32_t zs = 0u;
-    asm volatile("" : "+s"(zs) : "v"(st[0][0]), "v"(st[NB - 1][0]));
-    const int rn = r + AHEAD - 1;  // the round whose key is loaded now
-    if (rn < 15) kq[(rn - 1) % AHEAD] = *reinterpret_cast<const uint4*>(base + zs + 16 * rn);
-    const uint4 k = kq[(r - 1) % AHEAD];
-    const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
-    uint32_t o[NB][4];
-    if (r < 14) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
-          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
-        }
-    } else {
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
-          const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
-          const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
-          o[b][j] = xor3(lo, hi, kw[j]);
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
-  }
-}
-
-// AES-256 with round keys 0..KG-1 from the kernel-argument schedule (SGPRs) and rounds
-// KG..14 from the device copy rkg, each loaded by a uniform global_load_dwordx4 AHEAD
-// rounds before its use.  For kernels whose per-lane loads are issued just before the
-// AES (multi-key stream eval: the CW digest): vmcnt retires in order, so a key load
-// issued in round 1 would make its wait cover those digest loads too (all-global keys:
-// C5 -14 %); by round KG - AHEAD they have landed.  Uses 4 * KG SGPRs of keys instead of
-// 60, which leaves the multi-key stream kernel room for its loop state (no spills).
-template <int NB, int KG, int AHEAD = 3>
-__device__ __forceinline__ void aes256_tt_hk(uint32_t (&st)[NB][4], const RoundKeys& rk,
-                                             const uint4* __restrict__ rkg, const uint32_t* lds, uint32_t lc) {
-  static_assert(KG > AHEAD && KG <= 14, "keys KG..14 are loaded AHEAD rounds early");
-  const char* base = reinterpret_cast<const char*>(rkg);
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) st[b][j] ^= rk.w[j];
-  uint4 kq[15 - KG];
-#pragma unroll
-  for (int r = 1; r < 15; ++r) {
-    // issue the load of round key rn (>= KG) at round rn - AHEAD, after this round's state
-    const int rn = r + AHEAD;
-    if (rn >= KG && rn < 15) {
-      uint32_t zb = 0u;
-      asm volatile("" : "+v"(zb) : "v"(st[0][0]), "v"(st[NB - 1][0]));
-      kq[rn - KG] = *reinterpret_cast<const uint4*>(base + zb + 16 * rn);
-    }
-    uint32_t kw[4];
-    if (r < KG) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) kw[j] = rk.w[4 * r + j];
-    } else {
-      const uint4 k = kq[r - KG];
-      kw[0] = k.x; kw[1] = k.y; kw[2] = k.z; kw[3] = k.w;
-    }
-    uint32_t o[NB][4];
-    if (r < 14) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
-          o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
-        }
-    } else {
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<3, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<0, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<1, 3>(lds, st[b][(j + 3) & 3], lc);
-          const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0500u);
-          const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x07020c0cu);
-          o[b][j] = xor3(lo, hi, kw[j]);
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
-  }
-}
-
-// AES-256 with round keys 0..KS-1 from the kernel-argument schedule (SGPRs) and rounds
-// KS..14 from an LDS copy (rkl, 240 B): one broadcast ds_read_b128 per round shared by the
-// NB blocks, issued after the previous round's state (empty asm on the address) so the
-// compiler keeps one LDS key live, not 15 - 4 * KS SGPRs fewer than aes256_tt with no
-// vector-memory wait (LDS results retire in order, counted apart from the CW loads).
-template <int NB, int KS>
-__device__ __forceinline__ void aes256_tt_sl(uint32_t (&st)[NB][4], const RoundKeys& rk,
-                                             const uint4* rkl, const uint32_t* lds, uint32_t lc) {
-  static_assert(KS >= 0 && KS <= 15, "rounds 0..KS-1 from SGPRs");
-  const char* base = reinterpret_cast<const char*>(rkl);
-  {
-    uint32_t kw[4];
-    if (KS > 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) kw[j] = rk.w[j];
-    } else {
-      const uint4 k = rkl[0];
-      kw[0] = k.x; kw[1] = k.y; kw[2] = k.z; kw[3] = k.w;
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st[b][j] ^= kw[j];
-  }
-#pragma unroll
-  for (int r = 1; r < 15; ++r) {
-    uint32_t kw[4];
-    if (r < KS) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) kw[j] = rk.w[4 * r + j];
-    } else {
-      uint32_t zb = 0u;
-      asm volatile("" : "+v"(zb) : "v"(st[0][0]), "v"(st[NB - 1][0]));
-      const uint4 k = *reinterpret_cast<const uint4*>(base + zb + 16 * r);
-      kw[0] = k.x; kw[1] = k.y; kw[2] = k.z; kw[3] = k.w;
-    }
     uint32_t o[NB][4];
     if (r < 14) {
 #pragma unroll
@@ -679,85 +369,13 @@ __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* co
   aes_tt_lk<10, NB>(st, rk, lds, lc);
 }
 
-// ------------------------------------------------------------------------
-// Two-table variant (64 KiB of LDS instead of 128: room for two 640-thread
-// workgroups per CU).  Only T0 and T2 are stored, 32 replicas each, at
-//   addr(T, b, lane) = b * 256 + (T >> 1) * 128 + (lane & 31) * 4   (T in {0, 2});
-// T1 = rotl8(T0) and T3 = rotl8(T2), and rotation distributes over XOR, so a
-// column is T0[a] ^ T2[d] ^ rotl8(T0[c] ^ T2[e]) ^ rk: 4 lookups, 4 VALU.
-// ------------------------------------------------------------------------
-constexpr int kLdsWords2 = 16384;  // 64 KiB
-
-__device__ __forceinline__ void lds_fill_tables2(uint32_t* lds, const uint32_t* __restrict__ tab) {
-  for (int idx = threadIdx.x; idx < kLdsWords2; idx += blockDim.x) {
-    const int b = idx >> 6, half = (idx >> 5) & 1;
-    lds[idx] = tab[(2 * half) * 256 + b];
-  }
-  __syncthreads();
-}
-
-// Lookup of T0 (H = 0) or T2 (H = 1) at state byte K of w.
-template <int H, int K>
-__device__ __forceinline__ uint32_t lk2(const uint32_t* lds, uint32_t w, uint32_t lc) {
-  constexpr uint32_t sel = (H ? 1u : 0u) | ((4u + K) << 8) | (0x0cu << 16) | (0x0cu << 24);
-  const uint32_t addr = __builtin_amdgcn_perm(w, lc, sel);
-  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + addr);
-}
-
-__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
-
-template <int NB>
-__device__ __forceinline__ void aes256_tt2(uint32_t (&st)[NB][4], const RoundKeys& rk, const uint32_t* lds,
-                                           uint32_t lc) {
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) st[b][j] ^= rk.w[j];
-#pragma unroll
-  for (int r = 1; r < 14; ++r) {
-    uint32_t o[NB][4];
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t a = lk2<0, 0>(lds, st[b][j], lc);            // T0[byte 0 of col j]
-        const uint32_t c = lk2<0, 1>(lds, st[b][(j + 1) & 3], lc);  // T1 = rotl8(T0)
-        const uint32_t d = lk2<1, 2>(lds, st[b][(j + 2) & 3], lc);  // T2
-        const uint32_t e = lk2<1, 3>(lds, st[b][(j + 3) & 3], lc);  // T3 = rotl8(T2)
-        o[b][j] = xor3(a, d, rotl8(c ^ e)) ^ rk.w[4 * r + j];
-      }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
-  }
-  // Final round: S(x) is byte 1 of T0[x].
-  uint32_t o[NB][4];
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t a = lk2<0, 0>(lds, st[b][j], lc);
-      const uint32_t c = lk2<0, 1>(lds, st[b][(j + 1) & 3], lc);
-      const uint32_t d = lk2<0, 2>(lds, st[b][(j + 2) & 3], lc);
-      const uint32_t e = lk2<0, 3>(lds, st[b][(j + 3) & 3], lc);
-      const uint32_t lo = __builtin_amdgcn_perm(c, a, 0x0c0c0501u);  // byte0 = S(a), byte1 = S(c)
-      const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x05010c0cu);  // byte2 = S(d), byte3 = S(e)
-      o[b][j] = xor3(lo, hi, rk.w[56 + j]);
-    }
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) st[b][j] = o[b][j];
-}
-
 // In-kernel clock probe (diagnostic builds only, -DDCF_CLOCK_STAMPS; MI355X_MICROARCH.md "DVFS
 // give-back" item 6): lane 0 of workgroup w stamps the shader-clock counter (s_memtime) and the
 // 100 MHz real-time counter (s_memrealtime) when its work starts and ends; the engine clock is
 // the ratio of the deltas x 100 MHz.  The stamps go to a buffer of their own by plain vector
 // stores (dcf_debug_clock_stamps reads them back); no output is computed from them.
 #ifdef DCF_CLOCK_STAMPS
-constexpr uint32_t kClkSlots = 4, kClkGroups = 4096;
+constexpr uint32_t kClkSlots = 6, kClkGroups = 4096;
 __device__ unsigned long long g_clk_stamps[kClkSlots * kClkGroups * 4];
 __device__ __forceinline__ void clk_stamp(uint32_t slot, uint32_t phase) {
   const uint32_t wg = blockIdx.x + gridDim.x * blockIdx.y;

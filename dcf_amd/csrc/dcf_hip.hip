@@ -176,15 +176,29 @@ struct dcf_prg {
 
 namespace {
 
+// The prg's settings as one call sees them: read once, when the call leases its workspace (the
+// setters may race a call; no decision inside a call reads a setting twice).
+struct Cfg {
+  int mode, prefix_levels, hyb_tt, hyb_mem, shy_prio;
+  uint32_t shy_mask;
+  size_t prefix_cap;
+  bool timing;
+};
+Cfg snapshot(const dcf_prg* p) {
+  return Cfg{p->eval_mode.load(), p->prefix_levels.load(), p->hybrid_tt_waves.load(), p->hybrid_mem.load(),
+             p->shy_prio.load(), p->shy_mask.load(), p->prefix_cap.load(), p->timing.load() != 0};
+}
+
 // A workspace leased for one call.  `st` is the stream the call's device work is queued on
 // (for host entry points: the workspace's own compute stream, set by host_lease()).
 struct Lease {
   dcf_prg* p;
+  const Cfg c;  // the call's settings
   Workspace* w = nullptr;
   hipStream_t st = nullptr;
   bool ordered = false;
   bool drained = false;  // a host call synchronized its streams: nothing left to order after
-  Lease(dcf_prg* prg) : p(prg) {
+  Lease(dcf_prg* prg) : p(prg), c(snapshot(prg)) {
     {
       std::lock_guard<std::mutex> g(p->pool_mu);
       if (!p->free_ws.empty()) {
@@ -260,8 +274,8 @@ int ensure_ctr(Workspace* w) {
 }
 
 // Phase timing (dcf_prg_set_phase_timing): event i of the lease's workspace on its stream.
-void phase_mark(dcf_prg* p, Lease& L, int i) {
-  if (!p->timing.load(std::memory_order_relaxed)) return;
+void phase_mark(dcf_prg*, Lease& L, int i) {
+  if (!L.c.timing) return;
   Workspace* w = L.w;
   if (!w->tev[i] && hipEventCreate(&w->tev[i]) != hipSuccess) {
     (void)hipGetLastError();
@@ -276,27 +290,13 @@ void phase_mark(dcf_prg* p, Lease& L, int i) {
 // subtrees under level S, each expanded by one workgroup.
 uint32_t prefix_split(uint32_t levels) { return levels > 18u ? 8u : (levels > 10u ? levels - 10u : 0u); }
 
-// Depth-first tail of k_prefix_build16: the last H levels, once the workgroup's level holds
-// at least one node per thread (2^10 = kBlock); DCF_PFX_DFS caps H (0: level by level only).
-#ifndef DCF_PFX_DFS
-#define DCF_PFX_DFS 4
-#endif
-// Full-domain eval: the last DCF_FD_TAIL levels in registers, depth-first (DCF_FD_DFS = 1,
-// k_fd_dfs16) or breadth-first (k_fd_tail16, 2^D nodes per lane: D <= 3).
-#ifndef DCF_FD_DFS
-#define DCF_FD_DFS 1
-#endif
-#ifndef DCF_FD_BUILD
-#define DCF_FD_BUILD 1  // full domain: the levels above the depth-first tail by one k_prefix_build16 launch
-#endif
-#ifndef DCF_FD_TAIL
-#define DCF_FD_TAIL (DCF_FD_DFS ? 4 : 3)  // depth-first 5: 128 VGPRs + scratch spills
-#endif
-#ifndef DCF_STREAM_NBC
-#define DCF_STREAM_NBC 1  // single-key stream eval instances with the x width fixed (N = 16, N = 4)
-#endif
+// Depth-first tail of k_prefix_build16: the last H <= kPfxDfsMax levels, once the workgroup's
+// level holds at least one node per thread (2^10 = kBlock).
+// Full-domain eval: the last kFdTail levels in registers, depth-first (k_fd_dfs16; 5 levels:
+// 128 VGPRs + scratch spills), the levels above by one k_prefix_build16 launch.
+constexpr uint32_t kFdTail = 4;
 uint32_t prefix_dfs_levels(uint32_t levels, uint32_t S) {
-  const uint32_t cap = std::min<uint32_t>(DCF_PFX_DFS, kPfxDfsMax);
+  const uint32_t cap = kPfxDfsMax;
   return levels >= S + 10u + 1u ? std::min<uint32_t>(cap, levels - S - 10u) : 0u;
 }
 
@@ -322,17 +322,17 @@ size_t prefix_table_bytes(const dcf_prg* p, uint32_t d) {
 }
 
 // Auto depth under the dcf_prg_set_prefix_max_bytes cap: shallower until it fits (none below 8).
-uint32_t capped_depth(const dcf_prg* p, uint32_t d) {
-  if (!p->prefix_cap) return d;
-  while (d >= 8u && prefix_table_bytes(p, d) > p->prefix_cap) --d;
+uint32_t capped_depth(const dcf_prg* p, const Cfg& c, uint32_t d) {
+  if (!c.prefix_cap) return d;
+  while (d >= 8u && prefix_table_bytes(p, d) > c.prefix_cap) --d;
   return d >= 8u ? d : 0u;
 }
 
-uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
-  if (p->lambda != 16 || num_keys != 1 || p->prefix_levels == 0) return 0;
+uint32_t prefix_depth(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t num_keys, uint64_t total) {
+  if (p->lambda != 16 || num_keys != 1 || c.prefix_levels == 0) return 0;
   uint32_t d;
-  if (p->prefix_levels > 0) {
-    d = std::min((uint32_t)p->prefix_levels, kPrefixMaxForced);
+  if (c.prefix_levels > 0) {
+    d = std::min((uint32_t)c.prefix_levels, kPrefixMaxForced);
   } else {
     // Hirose (one-launch build, k_prefix_build16): D = log2(total), r02g sweep C2 (2^24
     // points) D = 22/23/24/25 -> 3.97/4.08/4.13/3.93 G evals/s; MMO (level kernels): log2 - 1
@@ -340,49 +340,36 @@ uint32_t prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint6
     d = p->kind == 0 ? lg : (lg > 1u ? lg - 1u : 0u);
     if (d < 8u) return 0;
     d = std::min(d, kPrefixMax);
-    d = capped_depth(p, std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1)));
+    d = capped_depth(p, c, std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1)));
   }
   return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
 }
 
 // Shared-prefix depth for the small-batch pair path (k_eval16_pair, auto mode, fewer points than
-// two per lane of the GPU): a C1-size batch walks its 8N levels back to back, so the table's
-// one-launch build (a few microseconds) is paid once against D levels saved on every point.
-// Auto (off by default, see below): log2(total) - DCF_SMALL_PFX_SUB from 2^DCF_SMALL_PFX_MIN
-// points; forced depths (dcf_prg_set_prefix_levels) always apply.
-#ifndef DCF_SMALL_PFX_SUB
-#define DCF_SMALL_PFX_SUB 1
-#endif
-#ifndef DCF_SMALL_PFX_MIN
-#define DCF_SMALL_PFX_MIN -1  // < 0: never in auto mode.  C1 A/B (same box, 300 steps, M evals/s): no table
-                              // 226.3-226.4, D = 14 / 15 / 16: 221.1-221.5 / 221.2-221.5 / 221.8-222.1 — the
-                              // build's D sequential levels on few workgroups cost what the walk saves
-#endif
-uint32_t small_prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t total) {
-  if (p->lambda != 16 || p->kind != 0 || p->prefix_levels == 0) return 0;
-  if (p->prefix_levels > 0) return std::min<uint32_t>(std::min((uint32_t)p->prefix_levels, kPrefixMaxForced),
-                                                      (uint32_t)(8 * n_bytes - 1));
-  if (DCF_SMALL_PFX_MIN < 0 || total < (1ull << (DCF_SMALL_PFX_MIN < 0 ? 0 : DCF_SMALL_PFX_MIN))) return 0;
-  const uint32_t lg = 63u - (uint32_t)__builtin_clzll(total | 1u);
-  if (lg < 8u + DCF_SMALL_PFX_SUB) return 0;
-  return capped_depth(p, std::min<uint32_t>(lg - DCF_SMALL_PFX_SUB, (uint32_t)(8 * n_bytes - 1)));
+// two per lane of the GPU): only a forced depth (dcf_prg_set_prefix_levels).  In auto mode a
+// C1-size batch walks without a table: C1 A/B (same box, 300 steps, M evals/s) no table
+// 226.3-226.4, D = 14 / 15 / 16 (log2(points) - 1..3) 221.1-221.5 / 221.2-221.5 / 221.8-222.1 —
+// the build's D sequential levels on few workgroups cost what the walk saves.
+uint32_t small_prefix_depth(const dcf_prg* p, const Cfg& c, size_t n_bytes) {
+  if (p->lambda != 16 || p->kind != 0 || c.prefix_levels <= 0) return 0;
+  return std::min<uint32_t>(std::min((uint32_t)c.prefix_levels, kPrefixMaxForced), (uint32_t)(8 * n_bytes - 1));
 }
 
 // Shared-prefix depth for the LAMBDA >= 32 stream head over m points of one key
 // (kernels_wide_stream.h WidePrefix): 80 B per node, 4 AES blocks per parent.
 // Auto: log2(m) - 1, at most 22 (two 336 MB node buffers at 2^22), none below 8.
 constexpr uint32_t kWidePrefixMax = 22;
-uint32_t wide_prefix_depth(const dcf_prg* p, size_t n_bytes, uint64_t m) {
-  if (p->lambda <= 16 || p->kind != 0 || p->prefix_levels == 0 || p->eval_mode == DCF_EVAL_TTABLE || m == 0) return 0;
+uint32_t wide_prefix_depth(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t m) {
+  if (p->lambda <= 16 || p->kind != 0 || c.prefix_levels == 0 || c.mode == DCF_EVAL_TTABLE || m == 0) return 0;
   uint32_t d;
-  if (p->prefix_levels > 0) {
-    d = std::min((uint32_t)p->prefix_levels, 30u);
+  if (c.prefix_levels > 0) {
+    d = std::min((uint32_t)c.prefix_levels, 30u);
   } else {
     const uint32_t lg = 63u - (uint32_t)__builtin_clzll(m | 1u);
     d = lg > 1u ? lg - 1u : 0u;
     if (d < 8u) return 0;
     d = std::min(d, kWidePrefixMax);
-    d = capped_depth(p, std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1)));
+    d = capped_depth(p, c, std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1)));
   }
   return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
 }
@@ -449,7 +436,7 @@ int build_prefix(dcf_prg* p, Workspace* w, size_t n_bytes, int party, const uint
     const uint32_t H = prefix_dfs_levels(levels, S);
     hipLaunchKernelGGL(k_prefix_build16, dim3(1u << S), dim3(kBlock), 0, st, p->d_tab, p->rk[0], cws, cwv, cwt,
                        (const uint4*)s0, (uint32_t)party, S, levels, H, ba, ba + ((size_t)1 << S) * region,
-                       (uint64_t)region, R, (uint4*)w->d_pfx, DCF_PFX_GK ? p->d_rk0 : nullptr);
+                       (uint64_t)region, R, (uint4*)w->d_pfx, p->d_rk0);
     HIP_TRY(hipGetLastError());
     *out = PrefixTable{(const uint4*)w->d_pfx, levels};
     return DCF_OK;
@@ -490,43 +477,34 @@ int build_prefix(dcf_prg* p, Workspace* w, size_t n_bytes, int party, const uint
 
 // build_prefix at depth d; in auto mode (prefix_levels < 0) an allocation failure retries
 // two levels shallower, down to 8, and then evaluates without a table (same output bytes).
-int try_prefix(dcf_prg* p, Workspace* w, size_t n_bytes, int party, const uint4* cws, const uint4* cwv,
+int try_prefix(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, int party, const uint4* cws, const uint4* cwv,
                const uint8_t* cwt, const uint4* np1, const uint8_t* s0, uint32_t d, PrefixTable* out, hipStream_t st) {
   *out = PrefixTable{nullptr, 0u};
   while (d) {
     const int rc = build_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0, d, out, st);
     if (rc != kPrefixNoMem) return rc;
-    if (p->prefix_levels >= 0) return fail(DCF_ERR_HIP, t_err);  // a forced depth must fit
+    if (c.prefix_levels >= 0) return fail(DCF_ERR_HIP, t_err);  // a forced depth must fit
     d = d >= 10u ? d - 2u : 0u;
   }
   *out = PrefixTable{nullptr, 0u};
   return DCF_OK;
 }
 
-#ifndef DCF_TAIL_ROUNDS
-#define DCF_TAIL_ROUNDS 0  // r02i A/B on C4: 0 (4096-point ranges) 41.1-41.3 ms, 1 42.2-42.3, 2 41.9-42.1, 4 41.7-41.8
-#endif
 template <int TW, int NCH = 0>
 int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
                 uint32_t lam, uint64_t K, uint64_t key, const uint32_t* tvec, uint64_t cnt, uint8_t* ys,
-                hipStream_t st, int cus) {
+                hipStream_t st) {
   const uint32_t nch = (nlev + 1 + 3) / 4;
   const size_t lds = (size_t)nch * 16 * TW;
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail<TW, NCH>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Points per workgroup: each workgroup builds its tile's tables once, then streams its
-  // points; DCF_TAIL_ROUNDS > 0 sizes the ranges so the grid is that many workgroups per
-  // CU (fewer table builds and workgroup drains), 0 = fixed kTailPts-point ranges.
+  // kTailPts points (r02i A/B on C4: 41.1-41.3 ms vs 41.7-42.3 with ranges sized to 1, 2 or 4
+  // workgroups per CU).
   const uint64_t tiles = (lam + TW - 1) / TW;
-  uint64_t per = kTailPts;
-  if (DCF_TAIL_ROUNDS > 0) {
-    const uint64_t slots = (uint64_t)DCF_TAIL_ROUNDS * (uint64_t)cus;
-    const uint64_t ranges = std::max<uint64_t>(1, slots / tiles);
-    per = std::max<uint64_t>(kTailPts, (((cnt + ranges - 1) / ranges) + 1023) & ~(uint64_t)1023);
-  }
-  const dim3 grid((unsigned)tiles, (unsigned)((cnt + per - 1) / per));
+  const dim3 grid((unsigned)tiles, (unsigned)((cnt + kTailPts - 1) / kTailPts));
   hipLaunchKernelGGL((k_eval_wide_tail<TW, NCH>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key, tvec,
-                     cnt, (uint32_t)per, ys);
+                     cnt, kTailPts, ys);
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }
@@ -544,21 +522,13 @@ int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, con
   const size_t lds = L::lds_bytes();
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-#ifndef DCF_TAIL2_PTS
-#define DCF_TAIL2_PTS 32768  // at least this many points per workgroup (one table build each; C4 A/B: 4096 37.8-38.0 ms, 8192 37.0-37.4, 16384 36.9-37.0, 32768 36.7-37.0, 65536 36.4-36.8)
-#endif
+  // One workgroup per CU: the batch split into cus / tiles ranges, so the tiles of a range build
+  // their tables once and walk its points together (the rows being written at any time stay
+  // few), at least 32768 points per workgroup (C4 A/B: 34.36-34.38 ms vs 34.78-35.01 with
+  // 32768-point ranges; 4096-point ranges 37.8-38.0).
   const uint64_t tiles = (lam + 127) / 128;
-  uint64_t per = DCF_TAIL2_PTS;
-#ifndef DCF_TAIL2_ONE_ROUND
-#define DCF_TAIL2_ONE_ROUND 1  // C4 A/B (same box, ms): 34.36-34.38 vs 34.78-35.01 with 32768-point ranges
-#endif
-  // One workgroup per CU: the batch split into cus / tiles ranges, so the tiles of a range
-  // build their tables once and walk its points together (the rows being written at any time
-  // stay few) instead of 128 workgroups per CU each building tables for 32768 points.
-  if (DCF_TAIL2_ONE_ROUND) {
-    const uint64_t ranges = std::max<uint64_t>(1, (uint64_t)cus / tiles);
-    per = std::max<uint64_t>(per, (((cnt + ranges - 1) / ranges) + 255) & ~(uint64_t)255);
-  }
+  const uint64_t ranges = std::max<uint64_t>(1, (uint64_t)cus / tiles);
+  const uint64_t per = std::max<uint64_t>(32768, (((cnt + ranges - 1) / ranges) + 255) & ~(uint64_t)255);
   const dim3 grid((unsigned)tiles, (unsigned)((cnt + per - 1) / per));
   hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key,
                      tvec, cnt, (uint32_t)per, ys);
@@ -566,16 +536,13 @@ int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, con
   return DCF_OK;
 }
 
-#ifndef DCF_TAIL2
-#define DCF_TAIL2 1  // 0: the 4-bit 256-byte-tile tail for every N
-#endif
 // The tail for n = nlev levels: the paired-slot tail when one of its instances covers the
 // n + 1 rows with fewer LDS reads than the 4-bit tail's ceil((n + 1) / 4), else the 4-bit one.
 int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
              uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
              int cus) {
   const uint32_t nrows = nlev + 1, nch = (nrows + 3) / 4;
-  if (DCF_TAIL2 && lam % 128 == 0) {
+  if (lam % 128 == 0) {
 #define DCF_T2(A, B)                                                                            \
   if (nrows <= Tail2Layout<A, B>::rows() && 2u * (A + B) < nch)                                 \
     return launch_tail2<A, B>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus);
@@ -586,14 +553,14 @@ int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const u
     DCF_T2(5, 7)   // N = 12..16: 97..129 rows, 24 reads (25..33)
 #undef DCF_T2
   }
-  return (nch == 33) ? launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus)
-       : (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus)
-                     : launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus);
+  return (nch == 33) ? launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st)
+       : (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st)
+                     : launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
 }
 
 // Dcf::eval at LAMBDA >= 32 for key `key` of a K-key CWB (see kernels_wide.h).
 // The caller (eval_launch) has zeroed the workspace's block count once for the whole call.
-int eval_wide(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
+int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
               const uint8_t* s0, const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nlev = (uint32_t)(8 * n_bytes);
   if (n_bytes > 31) return fail(DCF_ERR_UNSUPPORTED, "LAMBDA >= 32 eval supports N <= 31");
@@ -607,7 +574,7 @@ int eval_wide(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key
   if (rc) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
   WidePrefix wpf{nullptr, 0u};
-  const int mode = p->eval_mode;
+  const int mode = c.mode;
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = (m - off < chunk) ? m - off : chunk;
     const dim3 grid((unsigned)grid_for(cnt, p->cus));
@@ -622,7 +589,7 @@ int eval_wide(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key
         hipLaunchKernelGGL(k_cw_digest, dim3((4 * nlev + 255) / 256), dim3(256), 0, st, cws, cwv, cwt, nlev, lam, K,
                            key, (uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64);
         HIP_TRY(hipGetLastError());
-        const uint32_t d = wide_prefix_depth(p, n_bytes, m);
+        const uint32_t d = wide_prefix_depth(p, c, n_bytes, m);
         if (d) {
           rc = build_wide_prefix(p, w, nlev, party, s0, d, &wpf, st);
           if (rc) return rc;
@@ -632,14 +599,9 @@ int eval_wide(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key
       const uint64_t units = (cnt + kWideUnit - 1) / kWideUnit;
       uint64_t blocks = (units + 15) / 16;
       if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
-#ifndef DCF_WHS_NS
-#define DCF_WHS_NS 1  // points per lane
-#endif
-#ifndef DCF_WHS_WG
-#define DCF_WHS_WG kBlock  // threads per workgroup (one workgroup per CU: the T-tables fill the LDS)
-#endif
+      // one point per lane, one 1024-thread workgroup per CU (the T-tables fill the LDS)
 #define DCF_WHS(MH, XR)                                                                                        \
-  hipLaunchKernelGGL((k_eval_wide_head_stream<DCF_WHS_NS, MH, XR, DCF_WHS_WG>), dim3((unsigned)blocks), dim3(DCF_WHS_WG), 0, st, p->d_tab,     \
+  hipLaunchKernelGGL((k_eval_wide_head_stream<1, MH, XR, kBlock>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab,     \
                      p->d_rk2, (const uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
                      lam, K, key, cnt, w->d_ctr, ys + off * lam, tvec, wpf)
       const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16;
@@ -881,14 +843,14 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   const uint64_t total = (uint64_t)num_keys * points_per_key;
   // the paths eval_launch takes without a table: small batches (MMO: at auto depth; Hirose: in
   // auto mode), Hirose engines other than the stream engine (MMO ignores the engine setting)
+  const Cfg c = snapshot(p);
   const bool small = total < (uint64_t)p->cus * kBlock * 2;
   if (p->kind == 1 && p->lambda > 16) return 0;  // MMO at LAMBDA >= 32: no shared prefix (head/tail per block)
-  if (p->kind == 1) return small && p->prefix_levels < 0 ? 0 : (int)prefix_depth(p, n_bytes, num_keys, total);
-  if (p->lambda > 16) return n_bytes > 31 ? 0 : (int)wide_prefix_depth(p, n_bytes, points_per_key);
-  if (p->eval_mode == DCF_EVAL_AUTO && small) return num_keys == 1 ? (int)small_prefix_depth(p, n_bytes, total) : 0;
-  if (p->eval_mode != DCF_EVAL_AUTO && p->eval_mode != DCF_EVAL_STREAM && p->eval_mode != DCF_EVAL_STREAM_HYBRID)
-    return 0;
-  return (int)prefix_depth(p, n_bytes, num_keys, total);
+  if (p->kind == 1) return small && c.prefix_levels < 0 ? 0 : (int)prefix_depth(p, c, n_bytes, num_keys, total);
+  if (p->lambda > 16) return n_bytes > 31 ? 0 : (int)wide_prefix_depth(p, c, n_bytes, points_per_key);
+  if (c.mode == DCF_EVAL_AUTO && small) return num_keys == 1 ? (int)small_prefix_depth(p, c, n_bytes) : 0;
+  if (c.mode != DCF_EVAL_AUTO && c.mode != DCF_EVAL_STREAM && c.mode != DCF_EVAL_STREAM_HYBRID) return 0;
+  return (int)prefix_depth(p, c, n_bytes, num_keys, total);
 }
 
 int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves, int slab_variant) {
@@ -978,31 +940,25 @@ int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priorit
 }
 
 // Tiny batches run the latency kernels of kernels_lat.h (one AES column per lane).  Thresholds:
-// scripts/lat_sweep.sh (DESIGN.md §4 "Latency kernels").
-#ifndef DCF_EVAL_OCT_MAX
-#define DCF_EVAL_OCT_MAX 32768  // points (one key) up to which auto-mode eval runs k_eval16_oct
-#endif                          // (r03a sweep, us per device call: 32768 oct 187 vs pair 273; 100k 623 vs 485)
-#ifndef DCF_EVAL_ROW_MAX
-#define DCF_EVAL_ROW_MAX 8192   // points up to which auto-mode eval runs k_eval16_row (32 lanes per point)
-#endif
-#ifndef DCF_GEN_ROW_MAX
-#define DCF_GEN_ROW_MAX 2048    // keys up to which gen runs k_gen16_row (one wave per key; pipelined, r03t3:
-#endif                          // 2048 keys 110 vs 148 us col, 4096 keys 149 vs 147, 8192 277 vs 165)
-#ifndef DCF_GEN_COL_MAX
-#define DCF_GEN_COL_MAX 16384   // keys up to which gen runs k_gen16_col (r03a: 4096 keys 232 vs 562 us quads)
-#endif
+// scripts/lat_sweep.py / row_threshold.py (DESIGN.md §4 "Latency kernels", profiles/AB_LOG.md).
+constexpr uint64_t kEvalOctMax = 32768;  // points (one key) up to which auto-mode eval runs k_eval16_oct
+                                         // (r03a, us per device call: 32768 oct 187 vs pair 273; 100k 623 vs 485)
+constexpr uint64_t kEvalRowMax = 8192;   // points up to which auto-mode eval runs k_eval16_row (32 lanes per point)
+constexpr uint64_t kGenRowMax = 2048;    // keys up to which gen runs k_gen16_row (one wave per key; pipelined, r03t3:
+                                         // 2048 keys 110 vs 148 us col, 4096 keys 149 vs 147, 8192 277 vs 165)
+constexpr uint64_t kGenColMax = 16384;   // keys up to which gen runs k_gen16_col (r03a: 4096 keys 232 vs 562 us quads)
 // Items per workgroup of the latency kernels: a small batch spread over the CUs (one wave per
 // CU while it lasts), at most `cap` (a full 1024-thread workgroup).
 static uint32_t per_wg(uint64_t items, int cus, uint32_t cap) {
   const uint64_t per = (items + (uint64_t)cus - 1) / (uint64_t)cus;
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, per));
 }
-static bool oct_eval(const dcf_prg* p, size_t n_bytes, uint64_t num_keys, uint64_t total) {
-  return p->kind == 0 && p->lambda == 16 && num_keys == 1 && total <= (uint64_t)DCF_EVAL_OCT_MAX &&
-         8 * n_bytes <= kColMaxLevels && p->prefix_levels <= 0 && p->eval_mode == DCF_EVAL_AUTO;
+static bool oct_eval(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t num_keys, uint64_t total) {
+  return p->kind == 0 && p->lambda == 16 && num_keys == 1 && total <= kEvalOctMax && 8 * n_bytes <= kColMaxLevels &&
+         c.prefix_levels <= 0 && c.mode == DCF_EVAL_AUTO;
 }
 static bool col_gen(const dcf_prg* p, size_t n_bytes, uint64_t num_keys) {
-  return p->kind == 0 && p->lambda == 16 && num_keys <= (uint64_t)DCF_GEN_COL_MAX && 8 * n_bytes <= kColMaxLevels;
+  return p->kind == 0 && p->lambda == 16 && num_keys <= kGenColMax && 8 * n_bytes <= kColMaxLevels;
 }
 
 // Per-wave scratch slabs (bitsliced v) for every 16-wave workgroup of the hybrid kernels.
@@ -1047,7 +1003,7 @@ static int gen_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, con
     }
     return DCF_OK;
   }
-  if (col_gen(p, n_bytes, num_keys) && num_keys <= (uint64_t)DCF_GEN_ROW_MAX) {
+  if (col_gen(p, n_bytes, num_keys) && num_keys <= kGenRowMax) {
     // The smallest batches: one wave per key, one table lookup per lane and AES round
     // (k_gen16_row: a lone key's level is one 16-lane AES chain).
     const uint32_t kpw = per_wg(num_keys, p->cus, kBlock / 64);
@@ -1071,10 +1027,7 @@ static int gen_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, con
   // Lanes per key: a quad while the batch leaves lanes idle (a key's 8N levels take a quarter of
   // the AES latency: single gen 826 -> 266 us), one lane per key for large batches (2^20 keys:
   // 7.5-7.6 ms with one lane, 8.0 with quads — the four lanes repeat the level update).
-#ifndef DCF_GEN_QUAD_MAX
-#define DCF_GEN_QUAD_MAX ((uint64_t)p->cus * kBlock / 2)  // keys
-#endif
-  const bool quad = (uint64_t)num_keys <= DCF_GEN_QUAD_MAX;
+  const bool quad = (uint64_t)num_keys <= (uint64_t)p->cus * kBlock / 2;
   const uint64_t items = (uint64_t)num_keys * (quad ? 4u : 1u);
   uint32_t* ctr = nullptr;
   if (items >= (uint64_t)p->cus * kBlock * 2 && (items + 63) / 64 <= 0xFFFFFFFFull) {
@@ -1116,8 +1069,9 @@ static int eval_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, si
                        const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys) {
   if (int rc = ensure_ctr(L.w)) return rc;
   // the block count (dcf_prg_last_eval_blocks) covers the whole call: zeroed once here (the
-  // latency kernel zeroes it itself: one command less on a ~100 us call)
-  if (!(p->eval_mode == DCF_EVAL_AUTO && oct_eval(p, n_bytes, num_keys, (uint64_t)num_keys * ppk)))
+  // latency kernels zero it themselves: one command less on a ~100 us call).  The decision and
+  // eval_body's engine choice read the same settings snapshot (L.c).
+  if (!oct_eval(p, L.c, n_bytes, num_keys, (uint64_t)num_keys * ppk))
     HIP_TRY(hipMemsetAsync(L.w->d_ctr, 0, kCtrBytes, L.st));
   L.w->last_prefix = 0;
   phase_mark(p, L, 0);
@@ -1127,9 +1081,17 @@ static int eval_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, si
   return rc;
 }
 
+// Multi-key stream eval: keys per launch.  The kernel's work distribution, point and digest-row
+// indices are 32-bit (kernels_stream.h StreamLane): a launch covers < 2^31 points, and its digest
+// rows key * 8N + level index uint4 pairs (2 * row < 2^31), so at most 2^30 / 8N keys.
+static uint64_t mk_keys_per_launch(size_t n_bytes, uint64_t ppk) {
+  return std::max<uint64_t>(1, std::min<uint64_t>({1ull << 24, (1ull << 31) / ppk, (1ull << 30) / (8 * n_bytes)}));
+}
+
 static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party, const uint8_t* cwb,
                      const uint8_t* s0s, const uint8_t* xs, uint8_t* ys) {
   Workspace* w = L.w;
+  const Cfg& c = L.c;
   hipStream_t st = L.st;
   const uint64_t total = (uint64_t)num_keys * ppk;
   const size_t n = 8 * n_bytes, lam = p->lambda;
@@ -1138,8 +1100,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     for (uint64_t k = 0; k < num_keys; ++k) {
       int rc = p->kind == 1 ? eval_mmo_wide(p, w, n_bytes, num_keys, k, party, cwb, s0s + k * lam,
                                             xs + k * ppk * n_bytes, ppk, ys + k * ppk * lam, st)
-                            : eval_wide(p, w, n_bytes, num_keys, k, party, cwb, s0s + k * lam, xs + k * ppk * n_bytes,
-                                        ppk, ys + k * ppk * lam, st);
+                            : eval_wide(p, c, w, n_bytes, num_keys, k, party, cwb, s0s + k * lam,
+                                        xs + k * ppk * n_bytes, ppk, ys + k * ppk * lam, st);
       if (rc) return rc;
     }
     return DCF_OK;
@@ -1156,10 +1118,10 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
                      (uint4*)ys, pf)
     PrefixTable pf{nullptr, 0u};
     // auto depth: none for small batches (latency-bound: the table's D launches cost what it saves)
-    if (num_keys == 1 && (p->prefix_levels > 0 || total >= (uint64_t)p->cus * kBlock * 2)) {
-      const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
+    if (num_keys == 1 && (c.prefix_levels > 0 || total >= (uint64_t)p->cus * kBlock * 2)) {
+      const uint32_t d = prefix_depth(p, c, n_bytes, num_keys, total);
       if (d) {
-        int rc = try_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+        int rc = try_prefix(p, c, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
         if (rc) return rc;
         w->last_prefix = pf.levels;
       }
@@ -1173,8 +1135,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     return DCF_OK;
   }
   const bool bs_ok = (num_keys == 1 && n_bytes <= 16);
-  int mode = p->eval_mode;
-  if (mode == DCF_EVAL_AUTO && oct_eval(p, n_bytes, num_keys, total) && total <= (uint64_t)DCF_EVAL_ROW_MAX) {
+  int mode = c.mode;
+  if (oct_eval(p, c, n_bytes, num_keys, total) && total <= kEvalRowMax) {
     // The smallest batches: 32 lanes per point, one table lookup per lane and AES round
     // (k_eval16_row: a lone point's level is one 16-lane AES chain).
     phase_mark(p, L, 1);
@@ -1184,7 +1146,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     HIP_TRY(hipGetLastError());
     return DCF_OK;
   }
-  if (mode == DCF_EVAL_AUTO && oct_eval(p, n_bytes, num_keys, total)) {
+  if (oct_eval(p, c, n_bytes, num_keys, total)) {
     // Tiny batches (a single point through the C ABI: benches/dcf.rs bench_eval) are latency-
     // bound: 8 lanes per point, one AES column each, A and B side by side (k_eval16_oct).
     phase_mark(p, L, 1);
@@ -1194,45 +1156,31 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     HIP_TRY(hipGetLastError());
     return DCF_OK;
   }
-  // Auto: one key -> the stream engine (T-table, right steps encrypt B only; C3: 407 M
-  // evals/s vs 353 M hybrid, 332 M T-table).  Many keys -> lockstep T-table, whose waves
-  // share one key's CWs through scalar loads (C5: 264 M vs 206 M evals/s with streams,
-  // whose lanes sit on different levels and miss L1 on the level-major CW layout).
-  // Small batches (fewer points than two per lane of the GPU) are latency-bound: one
-  // point's 8N levels run back to back, so the lockstep walk (A and B of a level in
-  // one AES pass: 8N passes) beats the stream engine (~12N passes), and the points are
-  // spread over every CU with workgroups just big enough (C1, 100k points: 3.2 -> see
-  // DESIGN.md).
+  // Auto: small batches (fewer points than two per lane of the GPU) are latency-bound: one
+  // point's 8N levels run back to back, so the lockstep walk (A and B of a level in one AES
+  // pass: 8N passes) beats the stream engine (~12N passes); it runs on a lane pair per point
+  // (k_eval16_pair: the even lane encrypts A, the odd lane B), spread over every CU with
+  // workgroups just big enough (C1).  Larger batches: the stream engine, single key or many
+  // (C3: 407 M evals/s vs 353 M hybrid, 332 M lockstep T-table; C5 with the key-major digest).
   if (mode == DCF_EVAL_AUTO && total < (uint64_t)p->cus * kBlock * 2) {
-#ifndef DCF_SMALL_PAIR
-#define DCF_SMALL_PAIR 1
-#endif
     PrefixTable spf{nullptr, 0u};
-    if (DCF_SMALL_PAIR && num_keys == 1) {
-      const uint32_t d = small_prefix_depth(p, n_bytes, total);
+    if (num_keys == 1) {
+      const uint32_t d = small_prefix_depth(p, c, n_bytes);
       if (d) {
-        int rc = try_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &spf, st);
+        int rc = try_prefix(p, c, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &spf, st);
         if (rc) return rc;
         w->last_prefix = spf.levels;
       }
     }
     phase_mark(p, L, 1);
-    const uint64_t lanes_per_point = DCF_SMALL_PAIR ? 2 : 1;
-    uint64_t threads = (total * lanes_per_point + p->cus - 1) / p->cus;
+    uint64_t threads = (total * 2 + p->cus - 1) / p->cus;
     threads = ((threads + 63) / 64) * 64;
     if (threads > (uint64_t)kBlock) threads = kBlock;
-    const dim3 g2((unsigned)((total * lanes_per_point + threads - 1) / threads)), b2((unsigned)threads);
-#if DCF_SMALL_PAIR
+    const dim3 g2((unsigned)((total * 2 + threads - 1) / threads)), b2((unsigned)threads);
 #define DCF_SMALL(MODE)                                                                                           \
   hipLaunchKernelGGL(k_eval16_pair<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,                  \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk,  \
                      (uint4*)ys, p->d_rk0, MODE == 0 ? spf : PrefixTable{nullptr, 0u})
-#else
-#define DCF_SMALL(MODE)                                                                                           \
-  hipLaunchKernelGGL(k_eval16<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1, (const uint4*)s0s,    \
-                     (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk, (uint4*)ys,          \
-                     (uint32_t*)nullptr)
-#endif
     if (num_keys == 1) DCF_SMALL(0);
     else if (ppk % 64 == 0) DCF_SMALL(1);
     else DCF_SMALL(2);
@@ -1249,9 +1197,9 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
   const bool tt_single = (mode == DCF_EVAL_TTABLE && bs_ok);
   if (mode == DCF_EVAL_HYBRID || tt_single) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "hybrid eval: single key, N <= 16");
-    const bool mem = tt_single || p->hybrid_mem != 0;
+    const bool mem = tt_single || c.hyb_mem != 0;
     const int waves = mem ? 16 : kHybridWaves;
-    int ntt = tt_single ? 16 : p->hybrid_tt_waves.load();
+    int ntt = tt_single ? 16 : c.hyb_tt;
     if (mem && ntt < 1) ntt = 1;  // 15 LDS x-slots for bitsliced waves
     if (ntt > waves) ntt = waves;
     const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
@@ -1283,9 +1231,9 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     int rc = ensure_slabs(p, w, st);
     if (rc) return rc;
     PrefixTable pf{nullptr, 0u};
-    const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
+    const uint32_t d = prefix_depth(p, c, n_bytes, num_keys, total);
     if (d) {
-      rc = try_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+      rc = try_prefix(p, c, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
       if (rc) return rc;
       w->last_prefix = pf.levels;
     }
@@ -1294,12 +1242,9 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
     hipLaunchKernelGGL(k_eval16_shybrid, dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
                        (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, w->d_ctr,
-                       (uint4*)ys, pf, (uint32_t)p->shy_mask, (uint32_t)p->shy_prio, reinterpret_cast<uint4*>(w->d_slabs),
-                       p->d_km);
+                       (uint4*)ys, pf, c.shy_mask, (uint32_t)c.shy_prio, reinterpret_cast<uint4*>(w->d_slabs), p->d_km);
   } else if (mode == DCF_EVAL_STREAM) {
-#ifndef DCF_STREAM_NS
-#define DCF_STREAM_NS 2  // streams per lane
-#endif
+    constexpr int NS = 2;  // streams per lane
     const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16, multi = num_keys > 1;
     if (multi && ppk >= (1ull << 31)) return fail(DCF_ERR_UNSUPPORTED, "multi-key stream eval: 2^31 points per key or more");
     const uint4* scs = cws;
@@ -1313,8 +1258,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       sct = w->d_kdig + (size_t)num_keys * n * 32;
     }
     PrefixTable pf{nullptr, 0u};
-    if (multi && DCF_MK_PFX && p->prefix_levels != 0 && n > kMkPfxLevels && ppk >= 32 &&
-        num_keys <= (1ull << (31 - kMkPfxLevels))) {
+    if (multi && c.prefix_levels != 0 && n > kMkPfxLevels && ppk >= 32 && num_keys <= (1ull << (31 - kMkPfxLevels))) {
+      // per-key top trees (k_mk_prefix16: 32 rows per key); no room -> walk from the root (same bytes)
       const size_t need = (size_t)num_keys * (32u << kMkPfxLevels);
       if (w->pfx_bytes < need) {
         if (w->d_pfx) {
@@ -1324,7 +1269,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
           w->pfx_bytes = 0;
         }
         if (hipMalloc(&w->d_pfx, need) != hipSuccess) {
-          (void)hipGetLastError();  // no room: walk from the root (same output bytes)
+          (void)hipGetLastError();
         } else {
           w->pfx_bytes = need;
         }
@@ -1340,81 +1285,60 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       }
     }
     if (!multi) {
-      const uint32_t d = prefix_depth(p, n_bytes, num_keys, total);
+      const uint32_t d = prefix_depth(p, c, n_bytes, num_keys, total);
       if (d) {
-        int rc = try_prefix(p, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
+        int rc = try_prefix(p, c, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
         if (rc) return rc;
         w->last_prefix = pf.levels;
       }
-      if (DCF_STREAM_D48) {  // single key: 48-byte CW rows + a zero row (kernels_stream.h k_cw_rows48)
-        if (int rc = grow(&w->d_rows, &w->rows_bytes, (n + 1) * 48, st)) return rc;
-        hipLaunchKernelGGL(k_cw_rows48, dim3(1), dim3(256), 0, st, cws, cwv, cwt, (uint32_t)n, (uint4*)w->d_rows);
-        HIP_TRY(hipGetLastError());
-        scs = (const uint4*)w->d_rows;
-      }
     }
     phase_mark(p, L, 1);
-    const bool pfx = DCF_STREAM_PFXT && pf.levels != 0;
-    // One launch covers < 2^31 points and (multi-key) < 2^24 keys: the kernel's work
-    // distribution, point and digest-row indices are 32-bit (kernels_stream.h StreamLane).
-    // Larger batches run as several launches over consecutive points / whole keys, sharing
-    // the table, digest and CW rows built above.
-    const uint64_t kpl = multi ? std::max<uint64_t>(1, std::min<uint64_t>(1ull << 24, (1ull << 31) / ppk)) : 1;
+    // One launch covers < 2^31 points (multi-key: mk_keys_per_launch whole keys).  Larger
+    // batches run as several launches over consecutive points / whole keys, sharing the table
+    // and digest built above.
+    const uint64_t kpl = multi ? mk_keys_per_launch(n_bytes, ppk) : 1;
     const uint64_t ppl = multi ? kpl * ppk : (1ull << 31);  // points per launch
     for (uint64_t c0 = 0; c0 < total; c0 += ppl) {
-    const uint64_t cnt = std::min<uint64_t>(ppl, total - c0), k0 = multi ? c0 / ppk : 0, kc = multi ? cnt / ppk : 1;
-    // the table build counted its work units on the counter: each walk's counter starts at 0
-    // (the block count beside it keeps the per-key top trees' blocks)
-    HIP_TRY(hipMemsetAsync(w->d_ctr, 0, 8, st));
-    const uint64_t units = (cnt + kStreamUnit - 1) / kStreamUnit;
-    uint64_t blocks = (units + 15) / 16;
-    if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
-    const uint4* lcs = multi ? scs + k0 * 2 * n : scs;
-    const uint8_t* lct = multi ? sct + k0 * n : sct;
-    const uint4* lnp1 = np1 + k0;
-    const uint8_t* lxs = xs + c0 * n_bytes;
-    uint8_t* lys = ys + c0 * lam;
-    const uint8_t* ls0 = s0s + k0 * lam;
-    const PrefixTable lpf = (multi && pf.levels) ? PrefixTable{pf.sv + 2 * (k0 << pf.levels), pf.levels} : pf;
-#define DCF_STREAM_KN(XR, MK, PF, D4, NBC)                                                                    \
-  hipLaunchKernelGGL((k_eval16_stream<DCF_STREAM_NS, XR, MK, kBlock, false, PF, D4, NBC>), dim3((unsigned)blocks), block, 0, st, \
-                     p->d_tab, p->rk[0], lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes, \
-                     (uint64_t)kc, (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0)
-#define DCF_STREAM_K(XR, MK, PF, D4) DCF_STREAM_KN(XR, MK, PF, D4, 0)
-    // single key, x in registers: N = 16 (C1 / C3) and N = 4 (C2) with the x width fixed at
-    // compile time (a point's start loads x without width branches: C2 starts a point every
-    // ~13 AES slots)
-#ifndef DCF_MK_PFXT
-#define DCF_MK_PFXT 1  // multi-key: a kernel instance for "per-key top trees present" (no root-seed start path:
-                       // 48 -> 33 SGPR spills; C5 r03c A/B, same box, 2 runs: 414.6 / 413.7 vs 408.5 / 408.1 M evals/s)
-#endif
-#define DCF_STREAM(XR, MK)                                                                                    \
-  do {                                                                                                        \
-    if (MK && DCF_MK_PFXT && lpf.levels) DCF_STREAM_K(XR, MK, true, false);                                   \
-    else if (MK) DCF_STREAM_K(XR, MK, false, false);                                                          \
-    else if (pfx) DCF_STREAM_K(XR, false, true, DCF_STREAM_D48 != 0);                                          \
-    else if (XR && DCF_STREAM_NBC && n_bytes == 16) DCF_STREAM_KN(XR, false, false, DCF_STREAM_D48 != 0, 16);    \
-    else if (XR && DCF_STREAM_NBC && n_bytes == 4) DCF_STREAM_KN(XR, false, false, DCF_STREAM_D48 != 0, 4);      \
-    else DCF_STREAM_K(XR, false, false, DCF_STREAM_D48 != 0);                                                  \
-  } while (0)
-#ifdef DCF_STREAM_TT2
-    if (xreg && !multi) {
-      uint64_t b2 = (units + 9) / 10;
-      if (b2 > 2 * (uint64_t)p->cus) b2 = 2 * (uint64_t)p->cus;
-      hipLaunchKernelGGL((k_eval16_stream<2, true, false, 640, true>), dim3((unsigned)b2), dim3(640), 0, st, p->d_tab,
-                         p->rk[0], lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes,
-                         (uint64_t)kc, (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0);
-    } else
-#endif
-    if (xreg && multi) DCF_STREAM(true, true);
-    else if (xreg) DCF_STREAM(true, false);
-    else if (multi) DCF_STREAM(false, true);
-    else DCF_STREAM(false, false);
-    HIP_TRY(hipGetLastError());
-    }  // launches
+      const uint64_t cnt = std::min<uint64_t>(ppl, total - c0), k0 = multi ? c0 / ppk : 0, kc = multi ? cnt / ppk : 1;
+      // the table build counted its work units on the counter: each walk's counter starts at 0
+      // (the block count beside it keeps the per-key top trees' blocks)
+      HIP_TRY(hipMemsetAsync(w->d_ctr, 0, 8, st));
+      const uint64_t units = (cnt + kStreamUnit - 1) / kStreamUnit;
+      uint64_t blocks = (units + 15) / 16;
+      if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
+      const uint4* lcs = multi ? scs + k0 * 2 * n : scs;
+      const uint8_t* lct = multi ? sct + k0 * n : sct;
+      const uint4* lnp1 = np1 + k0;
+      const uint8_t* lxs = xs + c0 * n_bytes;
+      uint8_t* lys = ys + c0 * lam;
+      const uint8_t* ls0 = s0s + k0 * lam;
+      const PrefixTable lpf = (multi && pf.levels) ? PrefixTable{pf.sv + 2 * (k0 << pf.levels), pf.levels} : pf;
+#define DCF_STREAM(XR, MK, PF, NBC)                                                                             \
+  hipLaunchKernelGGL((k_eval16_stream<NS, XR, MK, PF, NBC>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], \
+                     lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes, (uint64_t)kc, \
+                     (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0)
+      // multi-key: an instance for "per-key top trees present" (no root-seed start path: 48 -> 33
+      // SGPR spills; C5 r03c A/B 414.6 / 413.7 vs 408.5 / 408.1 M evals/s).  Single key, x in
+      // registers: N = 16 (C1 / C3) and N = 4 (C2) with the x width fixed at compile time (a
+      // point's start loads x without width branches: C2 starts a point every ~13 AES slots).
+      if (multi && lpf.levels) {
+        if (xreg) DCF_STREAM(true, true, true, 0);
+        else DCF_STREAM(false, true, true, 0);
+      } else if (multi) {
+        if (xreg) DCF_STREAM(true, true, false, 0);
+        else DCF_STREAM(false, true, false, 0);
+      } else if (xreg && n_bytes == 16) {
+        DCF_STREAM(true, false, false, 16);
+      } else if (xreg && n_bytes == 4) {
+        DCF_STREAM(true, false, false, 4);
+      } else if (xreg) {
+        DCF_STREAM(true, false, false, 0);
+      } else {
+        DCF_STREAM(false, false, false, 0);
+      }
 #undef DCF_STREAM
-#undef DCF_STREAM_K
-#undef DCF_STREAM_KN
+      HIP_TRY(hipGetLastError());
+    }
   } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
     phase_mark(p, L, 1);
@@ -1486,9 +1410,6 @@ constexpr size_t kHostChunkBytes = 128ull << 20;
 // device-mapped buffer that the kernel reads and writes itself — one launch, no copy commands.
 constexpr size_t kTinyBytes = 1ull << 20;
 constexpr size_t kHostMidBytes = 64ull << 20;  // x + y of a mid-size host eval through the mapped buffer
-#ifndef DCF_HOST_MID
-#define DCF_HOST_MID 1
-#endif
 
 static int ensure_host_path(Workspace* w) {
   if (w->hs[0]) return DCF_OK;
@@ -1530,18 +1451,16 @@ static int ensure_tiny(Workspace* w, uint8_t** dptr) {
 }
 
 // The mid-size host buffer: mapped into the device's address space, coarse-grained (the GPU may
-// cache it; the host reads the outputs only after the stream has passed the kernel).  Grown on
-// demand and kept.  Returns its device address.
-#ifndef DCF_HOST_MID_COHERENT
-#define DCF_HOST_MID_COHERENT 0  // 1: fine-grained.  r03y2 C1 host path (3 runs): 143-148 vs 141-146 M evals/s,
-#endif                           // noise; buffer reuse with new x is tested for the default
+// cache it; the host reads the outputs only after the stream has passed the kernel; fine-grained
+// measured the same, r03y2 C1 host path 143-148 vs 141-146 M evals/s).  Grown on demand and kept.
+// Returns its device address.
 static int ensure_mid(Workspace* w, size_t bytes, uint8_t** dptr) {
   if (w->mid_bytes < bytes) {
     if (w->h_mid) HIP_TRY(hipHostFree(w->h_mid));
     w->h_mid = nullptr;
     w->mid_bytes = 0;
     HIP_TRY(hipHostMalloc((void**)&w->h_mid, bytes,
-                          hipHostMallocMapped | (DCF_HOST_MID_COHERENT ? hipHostMallocCoherent : hipHostMallocNonCoherent)));
+                          hipHostMallocMapped | hipHostMallocNonCoherent));
     w->mid_bytes = bytes;
   }
   HIP_TRY(hipHostGetDevicePointer((void**)dptr, w->h_mid, 0));
@@ -1587,7 +1506,7 @@ static int host_eval(dcf_prg* p, Lease& L, size_t nb, int party, const uint8_t* 
   Workspace* w = L.w;
   const size_t lam = p->lambda;
   const size_t ko = 0, so0 = align256(cwb_len), xo = so0 + 256, yo = xo + align256(m * nb);
-  if (oct_eval(p, nb, 1, m) && yo + m * lam <= kTinyBytes) {
+  if (oct_eval(p, L.c, nb, 1, m) && yo + m * lam <= kTinyBytes) {
     uint8_t* d = nullptr;
     if (int rc = ensure_tiny(w, &d)) return rc;
     uint8_t* h = w->h_tiny;
@@ -1604,7 +1523,7 @@ static int host_eval(dcf_prg* p, Lease& L, size_t nb, int party, const uint8_t* 
   // launch, one stream sync and one host copy out — no staging DMAs or chunk events (a C1-size
   // call is one chunk, its copies cannot overlap its kernel anyway).  The key goes to device
   // memory first: the walk reads a correction word per level.
-  if (DCF_HOST_MID && lam == 16 && p->eval_mode == DCF_EVAL_AUTO && m < (uint64_t)p->cus * kBlock * 2 &&
+  if (lam == 16 && L.c.mode == DCF_EVAL_AUTO && m < (uint64_t)p->cus * kBlock * 2 &&
       m * (nb + lam) <= kHostMidBytes) {
     const size_t kb = align256(cwb_len) + align256(lam);
     const size_t mx = align256(m * nb), need = kb + mx + m * lam;
@@ -1846,9 +1765,8 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
     return DCF_OK;
   }
   // Two ping-pong node buffers: s (16 B), v (16 B), t (1 B) per node.  With the
-  // Hirose PRG the last kFdTail levels run in registers (k_fd_tail16), so the widest
+  // Hirose PRG the last kFdTail levels run in registers (k_fd_dfs16), so the widest
   // node level in HBM is 2^(n - kFdTail).
-  constexpr uint32_t kFdTail = DCF_FD_TAIL;
   const bool fused = p->kind == 0 && nlev > kFdTail;
   const size_t n = 8 * n_bytes;
   const uint4* cws = (const uint4*)cwb;
@@ -1861,7 +1779,7 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   // instead of one breadth-first level launch per level with 33-byte SoA nodes through HBM;
   // the tail then starts from the rows.  Falls back to the level kernels if the table and its
   // build buffers (~65 B per node of level lev_end) cannot be allocated.
-  if (DCF_FD_BUILD && fused && DCF_FD_DFS && lev_end >= 12) {
+  if (fused && lev_end >= 12) {
     PrefixTable pf{nullptr, 0u};
     const int brc = build_prefix(p, L.w, n_bytes, party, cws, cwv, cwt, np1, s0, lev_end, &pf, st);
     if (brc != DCF_OK && brc != kPrefixNoMem) return brc;
@@ -1910,13 +1828,8 @@ int dcf_eval_full_domain_device(dcf_prg* p, size_t n_bytes, int party, const uin
   }
   if (fused) {
     const uint64_t nodes = 1ull << lev_end;
-    if (DCF_FD_DFS)  // depth-first in registers (k_fd_dfs16)
-      hipLaunchKernelGGL(k_fd_dfs16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
-                         p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63);
-    else
-      hipLaunchKernelGGL(k_fd_tail16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
-                         p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63,
-                         DCF_FD_GK ? p->d_rk0 : nullptr);
+    hipLaunchKernelGGL(k_fd_dfs16<kFdTail>, dim3((unsigned)grid_for(nodes, p->cus)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], cws, cwv, cwt, np1, lev_end, nodes, s_a, v_a, t_a, (uint4*)ys, ctrs + 63);
     HIP_TRY(hipGetLastError());
   }
   return DCF_OK;
@@ -2069,7 +1982,8 @@ int dcf_eval_multi_gpu_device(dcf_prg* const* prgs, size_t G, size_t n_bytes, in
 
 #ifdef DCF_CLOCK_STAMPS
 // Diagnostic builds only (not in include/dcf_hip.h): the in-kernel clock stamps of slot `slot`
-// (0 = k_eval_wide_tail2, 1 = k_eval_wide_head_stream, 2 = k_eval16_stream, 3 = k_eval16_oct) of the last launch:
+// (0 = k_eval_wide_tail2 main loop, 1 = k_eval_wide_head_stream walk, 2 = k_eval16_stream, 3 = k_eval16_oct,
+// 4 = k_eval_wide_tail2 entry (phase 0 only), 5 = k_eval_wide_head_stream entry (phase 0 only)) of the last launch:
 // per workgroup {memtime, realtime} at start and end, kClkGroups x 4 u64.
 int dcf_debug_clock_stamps(int device, int slot, unsigned long long* out, size_t n) {
   if (!out || slot < 0 || slot >= (int)kClkSlots || n < (size_t)kClkGroups * 4) return fail(DCF_ERR_ARG, "bad argument");

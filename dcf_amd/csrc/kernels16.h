@@ -162,9 +162,6 @@ __device__ __forceinline__ void prefix_row(const PrefixTable& pf, uint32_t idx, 
 // with half the AES work per level: a small batch has too few waves per SIMD to
 // overlap the LDS lookups with the rest (C1: 7 waves per CU with one lane per point).
 constexpr int kQpSwap1 = 1 | (0 << 2) | (3 << 4) | (2 << 6);
-#ifndef DCF_PAIR_GK
-#define DCF_PAIR_GK 1
-#endif
 
 __device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, const RoundKeys& rk,
                                               const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
@@ -194,10 +191,7 @@ __device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, 
       uint32_t st[1][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[0][j] = s[j] ^ inv;
-      if (DCF_PAIR_GK)
-        aes256_tt_gk<1>(st, rkg, lds, lc);  // round keys per round from global memory
-      else
-        aes256_tt<1>(st, rk, lds, lc);
+      aes256_tt_gk<1>(st, rkg, lds, lc);  // round keys per round from global memory (SGPR keys spill)
       uint32_t A[4], B[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -488,104 +482,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
   }
 }
 
-// Last D levels of the full-domain expansion in registers: one lane per node at
-// level nlev - D expands its 2^D leaves (2^D - 1 PRG calls) and writes their y
-// contiguously (2^D x 16 B), so the two largest node levels never go to HBM.
-#ifndef DCF_FD_GK
-#define DCF_FD_GK 0  // 1: aes256_tt_gk round keys (r01o A/B on FD N=4: 138.5 vs 119.7 ms, -13 %)
-#endif
-template <int D>
-__global__ __launch_bounds__(kBlock, 1) void k_fd_tail16(
-    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
-    const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
-    const uint32_t lev0, const uint64_t nnodes, const uint4* __restrict__ s_in, const uint4* __restrict__ v_in,
-    const uint8_t* __restrict__ t_in, uint4* __restrict__ ys, uint32_t* __restrict__ ctr,
-    const uint4* __restrict__ rkg) {
-  __shared__ uint32_t lds[kLdsWords];
-  lds_fill_tables(lds, tab);
-  const uint32_t lc = lane_const();
-  const uint4 np = cw_np1[0];
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint32_t unit = fd_unit(nnodes);
-  for (uint64_t base = next_unit_base_n(ctr, ~0ull, unit); base < nnodes;
-       base = next_unit_base_n(ctr, base, unit)) {
-    const uint64_t j = base + (threadIdx.x & 63u);
-    const bool live = j < nnodes;
-    const uint64_t jj = live ? j : nnodes - 1;
-    // nodes of the current level: ns/nv (4 words each), nt; level d has 2^d nodes
-    uint32_t ns[1 << (D - 1)][4], nv[1 << (D - 1)][4], nt[1 << (D - 1)];
-    {
-      const uint4 sv = s_in[jj], vv = v_in[jj];
-      ns[0][0] = sv.x; ns[0][1] = sv.y; ns[0][2] = sv.z; ns[0][3] = sv.w;
-      nv[0][0] = vv.x; nv[0][1] = vv.y; nv[0][2] = vv.z; nv[0][3] = vv.w;
-      nt[0] = t_in[jj];
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const uint32_t lev = lev0 + d;
-      const uint4 cs = cw_s[lev], cv = cw_v[lev];
-      const uint32_t ct = cw_t[lev];
-      const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
-      uint32_t cs2[1 << (D - 1)][4], cv2[1 << (D - 1)][4], ct2[1 << (D - 1)];  // next level (d < D - 1)
-#pragma unroll
-      for (int i = (1 << d) - 1; i >= 0; --i) {  // descending: children 2i, 2i+1 overwrite nothing unread
-        uint32_t st[2][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          st[0][k] = ns[i][k];
-          st[1][k] = ~ns[i][k];
-        }
-        // A, B: both children (lib.rs:176-189 with x bit 0 / 1)
-        if (DCF_FD_GK)
-          aes256_tt_gk<2>(st, rkg, lds, lc);  // round keys per round from global memory (no SGPR spills)
-        else
-          aes256_tt<2>(st, rk, lds, lc);
-        const uint32_t tm = 0u - nt[i];
-        uint32_t sl[4], vl[4], sr[4], vr[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t msk = (k == 3) ? kMaskLast : 0xFFFFFFFFu;
-          sl[k] = ((st[0][k] ^ ns[i][k]) & msk) ^ (tm & csw[k]);
-          sr[k] = (ns[i][k] & msk) ^ (tm & csw[k]);
-          vl[k] = nv[i][k] ^ ((st[1][k] ^ ~ns[i][k]) & msk) ^ (tm & cvw[k]);
-          vr[k] = nv[i][k] ^ ((~ns[i][k]) & msk) ^ (tm & cvw[k]);
-        }
-        const uint32_t tl = ((st[0][0] ^ ns[i][0]) & 1u) ^ (nt[i] & ct & 1u);
-        const uint32_t tr = ((st[1][0] ^ ~ns[i][0]) & 1u) ^ (nt[i] & (ct >> 1) & 1u);
-        if (d == D - 1) {  // leaves: y = v ^ s ^ t * cw_np1 (lib.rs:192)
-          if (live) {
-            const uint32_t ml = 0u - tl, mr = 0u - tr;
-            uint4* y = ys + (jj << D) + 2 * i;
-            y[0] = make_uint4(vl[0] ^ sl[0] ^ (ml & np.x), vl[1] ^ sl[1] ^ (ml & np.y), vl[2] ^ sl[2] ^ (ml & np.z),
-                              vl[3] ^ sl[3] ^ (ml & np.w));
-            y[1] = make_uint4(vr[0] ^ sr[0] ^ (mr & np.x), vr[1] ^ sr[1] ^ (mr & np.y), vr[2] ^ sr[2] ^ (mr & np.z),
-                              vr[3] ^ sr[3] ^ (mr & np.w));
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            cs2[2 * i][k] = sl[k]; cv2[2 * i][k] = vl[k];
-            cs2[2 * i + 1][k] = sr[k]; cv2[2 * i + 1][k] = vr[k];
-          }
-          ct2[2 * i] = tl;
-          ct2[2 * i + 1] = tr;
-        }
-      }
-      if (d < D - 1) {
-#pragma unroll
-        for (int i = 0; i < (2 << d); ++i) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            ns[i][k] = cs2[i][k];
-            nv[i][k] = cv2[i][k];
-          }
-          nt[i] = ct2[i];
-        }
-      }
-    }
-  }
-}
-
 // Pack the prefix level's (s, v, t) arrays into PrefixTable rows.
 __global__ void k_prefix_pack(const uint4* __restrict__ s, const uint4* __restrict__ v,
                               const uint8_t* __restrict__ t, const uint64_t n, uint4* __restrict__ sv) {
@@ -635,13 +531,9 @@ __device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, co
 // (key k, node j of level D - 3) walks root -> j (D - 3 PRG calls), then expands j's subtree
 // depth-first to its 8 leaves (7 calls): D = 5: 36 PRG calls per key instead of 64 x 5 walks.
 // Same node values as the lockstep / stream walks (fd_children: lib.rs:176-189).
-#ifndef DCF_MK_PFX
-#define DCF_MK_PFX 1  // multi-key stream eval: per-key top trees (dcf_hip.hip, >= 32 points per key)
-#endif
-#ifndef DCF_MK_PFX_LEVELS
-#define DCF_MK_PFX_LEVELS 5  // C5 A/B (same box, M evals/s): 6 400.5-400.8, 5 402.0-402.6, 4 401.2-401.7
-#endif
-constexpr uint32_t kMkPfxLevels = DCF_MK_PFX_LEVELS;  // 4..6
+// Multi-key stream eval (>= 32 points per key): per-key top trees of kMkPfxLevels levels.
+// C5 A/B (same box, M evals/s): 6 levels 400.5-400.8, 5 402.0-402.6, 4 401.2-401.7.
+constexpr uint32_t kMkPfxLevels = 5;  // 4..6
 constexpr uint32_t kMkPfxRoot = kMkPfxLevels - 3u;     // levels walked from the root per thread
 template <bool GKB = true>
 __global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
@@ -718,9 +610,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
 // table directly (no pack pass).  Same bytes as the level kernels + k_prefix_pack.
 // H > 0: the level-by-level part stops at level D - H (one node or more per thread) and
 // each thread expands its nodes' last H levels depth-first (see the tail below).
-#ifndef DCF_PFX_GK
-#define DCF_PFX_GK 1  // table build: AES round keys per round from the device copy (no SGPR spills)
-#endif
+// Round keys per round from the device copy (aes256_tt_gk: SGPR keys spill here).
 constexpr uint32_t kPfxDfsMax = 4;  // H <= 4: a 3-slot stack of 9-word nodes (27 VGPRs; 5 slots spill to scratch)
 __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
@@ -728,7 +618,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     const uint32_t party, const uint32_t S, const uint32_t D, const uint32_t H, uint8_t* __restrict__ buf_a,
     uint8_t* __restrict__ buf_b, const uint64_t region_bytes, const uint32_t region_nodes,
     uint4* __restrict__ table, const uint4* __restrict__ rkg) {
-  constexpr bool GKB = DCF_PFX_GK != 0;
+  constexpr bool GKB = true;
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint4 root_s, root_v;
   __shared__ uint32_t root_t;

@@ -38,32 +38,20 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
 
 // Column j of AES-256(in) for the lane quad holding the block's four columns (lane j of the
 // quad holds column j); kw[r] = word j of round key r.
-#ifndef DCF_COL_LATE_DPP
-#define DCF_COL_LATE_DPP 1  // rounds 1-13: look up the lane's own four bytes, rotate the results
-#endif
 __device__ __forceinline__ uint32_t aes256_col(uint32_t st, const uint32_t (&kw)[15], const uint32_t* lds,
                                                uint32_t lc) {
   st ^= kw[0];
 #pragma unroll
   for (int r = 1; r < 14; ++r) {
-    if (DCF_COL_LATE_DPP) {
-      // out_j = T0[s_j.b0] ^ T1[s_{j+1}.b1] ^ T2[s_{j+2}.b2] ^ T3[s_{j+3}.b3]: lane j looks up all
-      // four bytes of ITS word (T1[s_j.b1] is lane j-1's term, ...) and the quad rotations move
-      // the results instead of the inputs — the lookups start right after the previous round's
-      // XOR (no DPP hazard wait, no moves in front of them) and the moves fold into the XORs.
-      const uint32_t a = lk<0, 0>(lds, st, lc);
-      const uint32_t c = lk<1, 1>(lds, st, lc);
-      const uint32_t d = lk<2, 2>(lds, st, lc);
-      const uint32_t e = lk<3, 3>(lds, st, lc);
-      st = (a ^ kw[r]) ^ dpp<kQpRot1>(c) ^ dpp<kQpRot2>(d) ^ dpp<kQpRot3>(e);
-    } else {
-      const uint32_t w1 = dpp<kQpRot1>(st), w2 = dpp<kQpRot2>(st), w3 = dpp<kQpRot3>(st);
-      const uint32_t a = lk<0, 0>(lds, st, lc);
-      const uint32_t c = lk<1, 1>(lds, w1, lc);
-      const uint32_t d = lk<2, 2>(lds, w2, lc);
-      const uint32_t e = lk<3, 3>(lds, w3, lc);
-      st = xor3(xor3(a, c, d), e, kw[r]);
-    }
+    // out_j = T0[s_j.b0] ^ T1[s_{j+1}.b1] ^ T2[s_{j+2}.b2] ^ T3[s_{j+3}.b3]: lane j looks up all
+    // four bytes of ITS word (T1[s_j.b1] is lane j-1's term, ...) and the quad rotations move
+    // the results instead of the inputs — the lookups start right after the previous round's
+    // XOR (no DPP hazard wait, no moves in front of them) and the moves fold into the XORs.
+    const uint32_t a = lk<0, 0>(lds, st, lc);
+    const uint32_t c = lk<1, 1>(lds, st, lc);
+    const uint32_t d = lk<2, 2>(lds, st, lc);
+    const uint32_t e = lk<3, 3>(lds, st, lc);
+    st = (a ^ kw[r]) ^ dpp<kQpRot1>(c) ^ dpp<kQpRot2>(d) ^ dpp<kQpRot3>(e);
   }
   // final round: SubBytes + ShiftRows + AddRoundKey (S(x) sits in byte r of T_{(r+2)&3})
   const uint32_t w1 = dpp<kQpRot1>(st), w2 = dpp<kQpRot2>(st), w3 = dpp<kQpRot3>(st);
@@ -230,7 +218,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_oct(
 // each row the other's block (gfx950: odd rows of the first operand trade places with even
 // rows of the second, so with x in both, the results hold row 0's and row 1's x in every
 // lane); every lane then runs the level update for its column (p & 3), t comes from column 0.
-// The tiny-batch kernel (auto mode, up to DCF_EVAL_ROW_MAX points): a lone point's level costs
+// The tiny-batch kernel (auto mode, up to kEvalRowMax points): a lone point's level costs
 // one 16-lane AES chain instead of aes256_col's.  `ppw` points per workgroup (<= 32), spread
 // over the CUs like k_eval16_oct.  cwb / s0 / xs / ys may be host-mapped.
 __global__ __launch_bounds__(kBlock, 1) void k_eval16_row(
@@ -390,7 +378,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16_col(
 // of the level (A0, B0, A1, B1: prg.rs:42-73 on both parties' seeds, lib.rs:103-104) with
 // aes256_col16; v_permlane16_swap then v_permlane32_swap put column p&3 of all four blocks in
 // every lane, which runs k_gen16_col's level update (lib.rs:105-152) for its column.  The
-// tiny-batch gen (up to DCF_GEN_ROW_MAX keys), `kpw` keys per workgroup (<= 16).  Inputs and
+// tiny-batch gen (up to kGenRowMax keys), `kpw` keys per workgroup (<= 16).  Inputs and
 // the CWB output may be host-mapped.
 __global__ __launch_bounds__(kBlock, 1) void k_gen16_row(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ alpha,

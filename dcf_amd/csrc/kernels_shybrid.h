@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_shybrid(
   const uint32_t wave = threadIdx.x >> 6;
   if ((tt_mask >> wave) & 1u) {
     if (prio & 1u) __builtin_amdgcn_s_setprio(2);
-    stream_run<2, true, false, false, kWavePoints>(lds, nullptr, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, 1,
+    stream_run<2, true, false, kWavePoints, false>(lds, nullptr, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, 1,
                                                    total, total, ctr, ys, pf);
     return;
   }

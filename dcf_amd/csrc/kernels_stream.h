@@ -32,71 +32,11 @@
 
 namespace {
 
-#ifndef DCF_STREAM_UNIT
-#define DCF_STREAM_UNIT 256
-#endif
-constexpr uint32_t kStreamUnit = DCF_STREAM_UNIT;  // points per refill of a wave
-#ifndef DCF_LDS_KEYS
-#define DCF_LDS_KEYS 0  // 1: stream engine round keys from LDS (no SGPR spills, but 28 more LDS
-#endif                  //    reads per iteration: C3 463-480 vs 499 M evals/s, A/B r01l)
-#ifndef DCF_STREAM_GK
-#define DCF_STREAM_GK 1  // 1: single-key stream engine reads round keys from global memory (aes256_tt_gk)
-#endif
-// VALU trims of the single-key stream kernel.  r02n/r02o A/B (same box, 2 runs each, C3 / C2):
-// all off 523.3 M / 4.20 G evals/s; XOR3 524.1 / 4.19; D48+XOR3 520.8 / 4.17; PFXT+XOR3
-// 522.9 / 4.20; all three 521.4 / 4.22; PFXT alone 444 / 3.81 (register allocation flips).
-// Kernel VALU -4 % (1667 -> 1595 instructions) moved nothing: at ~80 % LDS busy the loop is
-// not VALU-bound.
-#ifndef DCF_STREAM_PFXT
-#define DCF_STREAM_PFXT 0  // separate kernel instance when a shared-prefix table is present (no fresh-word path)
-#endif
-#ifndef DCF_STREAM_D48
-#define DCF_STREAM_D48 0   // single key: CWs from 48-byte level rows (cs | cv | ct), one address per stream
-#endif
-#ifndef DCF_STREAM_XOR3
-#define DCF_STREAM_XOR3 1  // round key 0 folded into the input XOR (one v_bitop3 per word)
-#endif
-#ifndef DCF_MK_HK
-// multi-key stream eval: 0 = all round keys in SGPRs (some spill to VGPR lanes); k > 3 =
-// keys k..14 from global memory (aes256_tt_hk).  r02h A/B on C5 (same box, 2 runs each):
-// 0: 393.5 M evals/s, 11: 370.6 (-6 %), 8: 362.5 (-8 %) — vmcnt also counts the y
-// stores, so a key load's wait can cover recent stores; the spill reloads cost less.
-#define DCF_MK_HK 0
-#endif
-#ifndef DCF_MK_SK
-// multi-key stream eval: k > 0 = round keys by scalar loads k rounds ahead (aes256_tt_sk): no SGPR
-// spills (105 SGPRs), but r02 ab_sk (same box, 2 runs): C5 391.7 vs 350.5 (k = 2) / 351.6 (k = 3) M
-// evals/s, -10 %: a scalar load shares lgkmcnt with the LDS lookups, so its wait drains them all.
-#define DCF_MK_SK 0
-#endif
-#ifndef DCF_MK_SL
-#define DCF_MK_SL -1  // multi-key stream eval: k >= 0 = round keys 0..k-1 from SGPRs, k..14 from LDS (aes256_tt_sl)
-#endif
-#ifndef DCF_REFILL_ONCE
-#define DCF_REFILL_ONCE 1  // refill: assign point indices in the loop, start the stream once after it
-                           // (single-key instances with the x width fixed, NBC)
-#endif
-#ifndef DCF_REUSE_CHAIN
-// 1: B reuse over whole runs of right steps at t = 0 (see the reuse block).  Bit-exact, fewer
-// blocks (C3 132.2 -> 126.3 per eval, C2 12.52 -> 12.15), but slower: r02 ab_chain (same box, 2
-// runs): C3 520.9 vs 531.9 M evals/s (the N = 16 instance spills 20 VGPRs), C2 4.55 vs 4.60 G,
-// C5 382.7 vs 391.1 M — its ~25 VALU per stream and iteration cost more than 3-5 % of the blocks.
-#define DCF_REUSE_CHAIN 0
-#endif
-#ifndef DCF_REFILL_BATCH
-#define DCF_REFILL_BATCH 0  // 1: per stream, y stored after the new point's x load (vmcnt order); A/B r02 ab_batch: C3 -0.6 %, C2 / C1 noise
-#endif
-#ifndef DCF_BATCH_FENCE
-#define DCF_BATCH_FENCE asm volatile("" ::: "memory")
-#endif
-#ifndef DCF_STREAM_LATE_STORE
-// 1: y store issued after the refill's loads.  r02 A/B (same box, 2 runs): C3 533.8 vs 538.4,
-// C2 4.06 vs 4.11 G evals/s — slower: the next stream's update still waits vmcnt(0) on it.
-#define DCF_STREAM_LATE_STORE 0
-#endif
-#ifndef DCF_LDS_KEYS_LATE
-#define DCF_LDS_KEYS_LATE true  // ... read late (per round), so they are not all hoisted into VGPRs
-#endif
+constexpr uint32_t kStreamUnit = 256;  // points per refill of a wave
+// Round keys: the single-key engine reads them per round from the device copy of the schedule
+// (aes256_tt_gk, 3 rounds ahead: C3 +3.6 % over SGPR keys, r01o); the multi-key engine keeps
+// them in SGPRs (global keys: C5 -14 %, their waits retire in order behind the CW digest loads;
+// keys in LDS, by scalar loads or half in SGPRs measured slower too — profiles/AB_LOG.md).
 
 // Lane's rank among the set bits of `mask` (bits below this lane).
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
@@ -121,11 +61,6 @@ struct StreamLane {
 template <int NS, bool XREG, bool MULTI>
 __device__ __forceinline__ void stream_load_x(StreamLane<NS, XREG, MULTI>& L, int i, const uint8_t* row,
                                               uint32_t nbytes) {
-#ifdef DCF_PROBE_XHASH  // timing probe (wrong bytes): x words from the row address, no load
-  const uint32_t hx = (uint32_t)(size_t)row * 2654435761u;
-  L.xw[i][0] = hx; L.xw[i][1] = hx ^ 0x9E3779B9u; L.xw[i][2] = hx * 3u; L.xw[i][3] = ~hx;
-  return;
-#endif
   if (nbytes == 16) {
     const uint4 x = *reinterpret_cast<const uint4*>(row);
     L.xw[i][0] = x.x; L.xw[i][1] = x.y; L.xw[i][2] = x.z; L.xw[i][3] = x.w;
@@ -153,14 +88,10 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
     w0 = load_bits32(row, 0, nbytes);
   }
   uint32_t lev0 = 0u;
-  if ((!MULTI || DCF_MK_PFX) && (PFX || pf.levels)) {  // start below the shared prefix: its row of the top-tree table
+  if (PFX || pf.levels) {  // start below the shared prefix: its row of the top-tree table
     lev0 = pf.levels;      // (MULTI: the key's own top tree, k_mk_prefix16, rows k * 2^levels + ...)
     uint4 sv, vv;
-#ifdef DCF_PROBE_ROW0  // timing probe (wrong bytes): every point starts from a few hot rows
-    const uint32_t top = (w0 >> (32u - lev0)) & 63u;
-#else
     const uint32_t top = w0 >> (32u - lev0);
-#endif
     prefix_row(pf, MULTI ? (k << lev0) + top : top, sv, vv, L.t[i]);
     L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w;
     L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
@@ -197,11 +128,11 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
                                               uint32_t nunits, uint32_t total, const uint4* __restrict__ s0s,
                                               const uint4 s0v, uint32_t party, const uint8_t* __restrict__ xs,
                                               uint32_t nbytes, uint64_t ppk, const PrefixTable& pf) {
-  // The loop only hands out point indices; the stream state is written once after it
-  // (DCF_REFILL_ONCE), so it is not a loop-carried value (no copies of it per pass).
+  // Single key, x width fixed: the loop only hands out point indices and the stream state is
+  // written once after it, so it is not a loop-carried value (no copies of it per pass; the
+  // multi-key and runtime-width instances spill VGPRs that way and start streams in the loop).
   uint64_t need = __ballot(mine);
-  // (single key, x width fixed: the multi-key and runtime-width instances spill VGPRs with it)
-  constexpr bool ONCE = DCF_REFILL_ONCE && !MULTI && NBC != 0;
+  constexpr bool ONCE = !MULTI && NBC != 0;
   if (ONCE) {
     uint32_t pnew = 0;
     bool got = false;
@@ -262,41 +193,6 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
   }
 }
 
-// Hand the next point index to every lane whose stream i is free (`mine`): got / pnew, or
-// retire the stream when the counter is exhausted.  Called in wave-uniform control flow;
-// issues no memory access but the work-counter atomic (the stream is started by the caller).
-template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit>
-__device__ __forceinline__ void stream_claim(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint32_t& unext,
-                                             uint32_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
-                                             uint32_t nunits, uint32_t total, uint32_t& pnew, bool& got) {
-  uint64_t need = __ballot(mine);
-  while (need) {
-    if (unext >= uend && !exhausted) {
-      const uint32_t u = dequeue_unit(ctr);
-      if (u >= nunits) {
-        exhausted = true;
-      } else {
-        unext = u * UNIT;
-        uend = min(unext + UNIT, total);
-      }
-    }
-    if (exhausted && unext >= uend) break;
-    const uint32_t rank = lane_rank(need);
-    const bool take = mine && rank < uend - unext;
-    pnew = take ? unext + rank : pnew;
-    got = got || take;
-    const uint64_t taken = __ballot(take);
-    unext += (uint32_t)__popcll(taken);
-    need &= ~taken;
-    mine = mine && !take;
-  }
-  if (mine) {  // nothing left: the stream retires
-    L.alive[i] = false;
-    L.ci[i] = 0;  // keep the idle stream's CW loads in bounds
-    L.lev[i] = 0;
-  }
-}
-
 // The stream's next 32 x bits at level nl (a multiple of 32): from the queue (XREG) or x.
 template <int NS, bool XREG, bool MULTI>
 __device__ __forceinline__ void stream_next_word(StreamLane<NS, XREG, MULTI>& L, int i, uint32_t nl, uint32_t nlev,
@@ -342,21 +238,10 @@ __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ c
   }
 }
 
-// Single-key CW rows for the stream engine (D48): row l = cw_s[l] | cw_v[l] | (cw_t[l], 0, 0, 0),
-// 48 B, and row 8N = zeros, so a stream's current and next level are one address apart.
-__global__ void k_cw_rows48(const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
-                            const uint8_t* __restrict__ cw_t, const uint32_t nlev, uint4* __restrict__ rows) {
-  for (uint32_t l = threadIdx.x; l <= nlev; l += blockDim.x) {
-    const bool z = l == nlev;
-    rows[3 * l] = z ? make_uint4(0u, 0u, 0u, 0u) : cw_s[l];
-    rows[3 * l + 1] = z ? make_uint4(0u, 0u, 0u, 0u) : cw_v[l];
-    rows[3 * l + 2] = make_uint4(z ? 0u : (uint32_t)cw_t[l], 0u, 0u, 0u);
-  }
-}
-
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
-template <int NS, bool XREG, bool MULTI, bool TT2, uint32_t UNIT, bool LK = false, bool GK = false, int HK = 0,
-          bool PFX = false, bool D48 = false, int SL = -1, int NBC = 0, int SK = 0>
+// GK: round keys per round from the device copy rkg (aes256_tt_gk); otherwise from the kernel
+// argument (SGPRs).  PFX: every stream starts below the per-key top trees (multi-key).
+template <int NS, bool XREG, bool MULTI, uint32_t UNIT, bool GK, bool PFX = false, int NBC = 0>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -366,8 +251,6 @@ __device__ __forceinline__ void stream_run(
   const uint32_t nbytes = NBC ? (uint32_t)NBC : nbytes_rt;
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
-  // batched refill (single key, x width fixed, x words queued in registers)
-  constexpr bool BATCH = DCF_REFILL_BATCH && DCF_REFILL_ONCE && XREG && !MULTI && NBC != 0 && !DCF_STREAM_LATE_STORE;
   // one launch covers < 2^32 points (the host cuts larger batches): 32-bit work distribution
   const uint32_t total32 = (uint32_t)total;
   const uint32_t nunits = (uint32_t)((total + UNIT - 1) / UNIT);
@@ -406,81 +289,50 @@ __device__ __forceinline__ void stream_run(
     bool maybe[NS];  // the next level's CWs were loaded
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      // CW row: the key-major digest row (MULTI); for one key the row is the level itself (a
-      // 32-bit index: ci only mirrors lev there, and a retired stream's lev is reset to 0)
+      // CW row: the key-major digest row (MULTI: cw_s = digest, 2 uint4 per level, cw_t = its t
+      // bytes); for one key the row is the level itself (a 32-bit index: ci only mirrors lev
+      // there, and a retired stream's lev is reset to 0)
       const uint32_t cwi = MULTI ? L.ci[i] : L.lev[i];
-      const uint4* row = cw_s + 3 * cwi;  // D48: level rows cs | cv | (ct, 0, 0, 0), plus a zero row 8N
-      if (D48) {
-        cs[i] = row[0];
-        cv[i] = row[1];
-        ct[i] = reinterpret_cast<const uint32_t*>(row + 2)[0];
-      } else if (MULTI) {  // cw_s = digest (2 uint4 per level), cw_t = digest t bytes
+      if (MULTI) {
         cs[i] = cw_s[2 * cwi];
         cv[i] = cw_s[2 * cwi + 1];
       } else {
-        cs[i] = MULTI ? cw_s[cwi] : cw_s[L.lev[i]];
-        cv[i] = MULTI ? cw_v[cwi] : cw_v[L.lev[i]];
+        cs[i] = cw_s[cwi];
+        cv[i] = cw_v[cwi];
       }
-      if (!D48) ct[i] = MULTI ? cw_t[cwi] : cw_t[L.lev[i]];
+      ct[i] = cw_t[cwi];
       // XREG: a fresh stream's x word is still in the queue; its first step is a B step
       // at the root, whose seed may be unmasked, so no reuse follows it anyway.
-#ifndef DCF_NO_B_REUSE
       maybe[i] = L.alive[i] && L.ph[i] == 0u && L.t[i] == 0u && (!XREG || PFX || !L.fresh[i]) &&
                  (L.cur[i] >> 31) != 0u && L.lev[i] + 1u < nlev;
-#else
-      maybe[i] = false;
-#endif
       // Loaded unconditionally (L1-resident): loads under a divergent branch made the
       // compiler wait for them before the AES.
       const uint32_t c2 = cwi + (L.lev[i] + 1u < nlev ? 1u : 0u);
-      if (D48) {  // the next row (row 8N is zeros: no clamp needed)
-        cs2[i] = row[3];
-        cv2[i] = row[4];
-      } else if (MULTI) {
+      if (MULTI) {
         cs2[i] = cw_s[2 * c2];
         cv2[i] = cw_s[2 * c2 + 1];
       } else {
         cs2[i] = cw_s[c2];
         cv2[i] = cw_v[c2];
       }
-      ct2[i] = D48 ? reinterpret_cast<const uint32_t*>(row + 5)[0] : (uint32_t)cw_t[c2];
+      ct2[i] = cw_t[c2];
     }
     // Slot i encrypts ~s (B) in phase 0 and s (A) in phase 1.
     uint32_t st[NS][4];
-    constexpr bool PRE = GK && DCF_STREAM_XOR3;  // round key 0 folded in here (one 3-input XOR per word)
+    // GK: round key 0 is folded into the input XOR (one 3-input XOR per word)
     uint4 k0 = make_uint4(0u, 0u, 0u, 0u);
-    if (PRE) k0 = rkl[0];
+    if (GK) k0 = rkl[0];
     const uint32_t k0w[4] = {k0.x, k0.y, k0.z, k0.w};
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const uint32_t inv = L.ph[i] - 1u;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) st[i][j] = PRE ? xor3(L.s[i][j], inv, k0w[j]) : (L.s[i][j] ^ inv);
+      for (int j = 0; j < 4; ++j) st[i][j] = GK ? xor3(L.s[i][j], inv, k0w[j]) : (L.s[i][j] ^ inv);
     }
-#ifdef DCF_PRIO_UPDATE
-    __builtin_amdgcn_s_setprio(0);
-#endif
-    if (TT2) {
-      aes256_tt2<NS>(st, rk, lds, lc);
-    } else if (GK) {  // round keys from global memory, loaded DCF_GK_AHEAD rounds ahead
-      aes256_tt_gk<NS, PRE>(st, rkl, lds, lc);
-    } else if (SK) {  // round keys by scalar loads, SK rounds ahead (multi-key)
-      aes256_tt_sk<NS, (SK > 0 ? SK : 1)>(st, rkl, lds, lc);
-    } else if (SL >= 0) {  // keys 0..SL-1 from SGPRs, SL..14 from LDS (multi-key)
-      aes256_tt_sl<NS, (SL >= 0 ? SL : 0)>(st, rk, rkl, lds, lc);
-    } else if (HK) {  // keys 0..HK-1 from SGPRs, HK..14 from global memory (multi-key)
-      aes256_tt_hk<NS, (HK > 3 ? HK : 4)>(st, rk, rkl, lds, lc);
-    } else if (LK) {  // round keys from LDS: one ds_read_b128 per round (see k_eval16_stream)
-      const uint4* rkp[NS];
-#pragma unroll
-      for (int i = 0; i < NS; ++i) rkp[i] = rkl;
-      aes_tt_lk<14, NS, DCF_LDS_KEYS_LATE>(st, rkp, lds, lc);
-    } else {
+    if (GK)
+      aes256_tt_gk<NS, true>(st, rkl, lds, lc);
+    else
       aes256_tt<NS>(st, rk, lds, lc);
-    }
-#ifdef DCF_PRIO_UPDATE
-    __builtin_amdgcn_s_setprio(DCF_PRIO_UPDATE);
-#endif
     // Pin the CW loads above the update: without this the compiler sinks the
     // cw_t load into the (divergent) level-done path and waits on it there.
 #pragma unroll
@@ -536,7 +388,6 @@ __device__ __forceinline__ void stream_run(
       L.cur[i] <<= adv;
       if (adv && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
       L.ci[i] += adv;
-#ifndef DCF_REUSE_BRANCH
       {  // reuse: level nl with B known: its B half now, without an AES slot (branch-free)
         const uint32_t xb2 = L.cur[i] >> 31, t1 = L.t[i], tm1 = 0u - t1;
         const uint32_t rm = 0u - (uint32_t)reuse, rr = rm & (0u - xb2);  // reuse / reuse and right
@@ -556,145 +407,43 @@ __device__ __forceinline__ void stream_run(
         L.cur[i] <<= (rr & 1u);
         L.ci[i] += rr & 1u;
         if (rr && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
-        if (DCF_REUSE_CHAIN && !MULTI) {  // (multi-key instances: no registers to spare)
-          // Chain: the reused right step ran at t = 0 and B's bit b = lsb(B^~s) is 0, so t' = b = 0
-          // and s is unchanged again — and so on for every further right step: each one is
-          // v ^= ~s & M with no CW (t = 0) and no AES (lib.rs:176-185).  Take the whole run of 1
-          // bits at once, up to the end of the current x word (or of x); a 0 bit ending the run
-          // inside the word is a left step whose B half (B^~s) & M = d & M is applied now, A next.
-          const uint32_t zm = rr & (tm1 ^ 0xFFFFFFFFu) & ((d0 & 1u) - 1u);  // all ones: chain
-          const uint32_t room = min(32u - (nl & 31u), nlev - nl);          // levels left in this word
-          const uint32_t ones = (uint32_t)__clz((int)~L.cur[i]);
-          // DCF_REUSE_CHAIN 2: the run stops one level short of the word's end, so the chain never
-          // fetches the next x word (a run reaching it leaves its last right step to the AES slot)
-          // (room is 0 once the reused step ended the point: no run then)
-          const uint32_t run = (DCF_REUSE_CHAIN == 2 ? min(ones, room ? room - 1u : 0u) : min(ones, room)) & zm;
-          const uint32_t om = 0u - (run & 1u);                                // odd run: v ^= ~s & M once
-          const uint32_t lm = zm & (0u - (uint32_t)(DCF_REUSE_CHAIN == 2 ? ones < room : run < room));  // ends at a left step
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
-            L.v[i][j] ^= ((om & ~L.s[i][j]) ^ (lm & d[j])) & msk;
-          }
-          nl += run;
-          L.cur[i] = (DCF_REUSE_CHAIN == 2 || run < 32u) ? (L.cur[i] << run) : 0u;
-          L.ci[i] += run;
-          L.ph[i] = lm ? 1u : L.ph[i];
-          if (DCF_REUSE_CHAIN != 2 && run && run == room && nl < nlev)
-            stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
-        }
       }
-#else
-      if (reuse) {  // level nl with B known: its B half now, without an AES slot
-        const uint32_t xb2 = L.cur[i] >> 31, t1 = L.t[i], tm1 = 0u - t1;
-        const uint32_t cs2w[4] = {cs2[i].x, cs2[i].y, cs2[i].z, cs2[i].w};
-        const uint32_t cv2w[4] = {cv2[i].x, cv2[i].y, cv2[i].z, cv2[i].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
-          // v ^= v_hat(side) ^ t*cw.v: right ~s & M, left (B^~s) & M   (lib.rs:182/186)
-          L.v[i][j] ^= ((xb2 ? ~L.s[i][j] : d[j]) & msk) ^ (tm1 & cv2w[j]);
-          if (xb2) L.s[i][j] ^= tm1 & cs2w[j];  // right: s' = s & M ^ t*cw.s   (lib.rs:178)
-        }
-        if (xb2) {  // a right step ends the level: t' = lsb(B^~s) ^ t & cw.tr   (lib.rs:180)
-          L.t[i] = (d0 ^ (t1 & (ct2[i] >> 1))) & 1u;
-          ++nl;
-          L.cur[i] <<= 1;
-          if ((nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
-          L.ci[i] += 1u;
-        } else {
-          L.ph[i] = 1u;  // left: A next
-        }
-      }
-#endif
       L.lev[i] = nl;
     }
-    // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.
-    if constexpr (BATCH) {
-      // Per stream: claim the new point, load its x words, store the finished y (the old state
-      // is still in place), then load the new point's table row.  vmcnt retires in issue order
-      // and counts stores, so the x wait no longer covers the y store.
-#pragma unroll
-      for (int i = 0; i < NS; ++i) {
-        const bool dn = L.alive[i] && L.lev[i] == nlev;
-        if (!__ballot(dn)) continue;
-        bool got = false;
-        uint32_t pnew = 0;
-        stream_claim<NS, XREG, MULTI, UNIT>(L, i, dn, unext, uend, exhausted, ctr, nunits, total32, pnew, got);
-        if (got) stream_load_x(L, i, xs + (uint64_t)pnew * nbytes, nbytes);
-        DCF_BATCH_FENCE;
-        if (dn) {
-          const uint32_t tm = 0u - L.t[i];
-          ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np1v.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np1v.y),
-                                   L.v[i][2] ^ L.s[i][2] ^ (tm & np1v.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np1v.w));
-        }
-        DCF_BATCH_FENCE;
-        if (got) stream_start<NS, XREG, MULTI, PFX, NBC, true>(L, i, pnew, s0s, s0v, party, xs, nbytes, ppk, pf);
-      }
-      continue;
-    }
-    // (vmcnt counts stores too, so the refill's wait for its x word also waits for this store;
-    // issuing it after the refill's loads instead, DCF_STREAM_LATE_STORE, measured slower.)
+    // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.  (vmcnt counts
+    // stores too, so the refill's wait for its x word also waits for this store; issuing the
+    // store after the refill's loads measured slower, AB_LOG r02.)
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
-      uint4 yv = make_uint4(0u, 0u, 0u, 0u);
-      uint32_t yp = 0;
       if (done) {
         const uint4 np = MULTI ? cw_np1[L.pt[i] / (uint32_t)ppk] : np1v;
         const uint32_t tm = 0u - L.t[i];
-        yv = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
-                        L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
-        yp = L.pt[i];
-        if (!DCF_STREAM_LATE_STORE) ys[yp] = yv;
+        ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
+                                 L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
       }
       if (__ballot(done))
         stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total32, s0s,
                                                   s0v, party, xs, nbytes, ppk, pf);
-      if (DCF_STREAM_LATE_STORE && done) {
-        asm volatile("" ::: "memory");  // keep the store below the refill's loads
-        ys[yp] = yv;
-      }
     }
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
   if ((threadIdx.x & 63u) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, (unsigned long long)nblk);
 }
 
-// TT2: the two-table AES (64 KiB of LDS), WG = 640 threads, two workgroups per CU.
-template <int NS, bool XREG, bool MULTI, int WG = kBlock, bool TT2 = false, bool PFX = false, bool D48 = false,
-          int NBC = 0>
-__global__ __launch_bounds__(WG, 1) void k_eval16_stream(
+// One 1024-thread workgroup per CU (the replicated T-tables take 128 KiB of LDS).
+template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0>
+__global__ __launch_bounds__(kBlock, 1) void k_eval16_stream(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
     uint4* __restrict__ ys, const PrefixTable pf, const uint4* __restrict__ rkg) {
-  __shared__ uint32_t lds[TT2 ? kLdsWords2 : kLdsWords];
-  // DCF_LDS_KEYS: the AES-256 schedule in LDS (240 B), one broadcast ds_read_b128 per
-  // round, instead of 60 kernel-argument SGPRs that the compiler partly spills to VGPR
-  // lanes (v_readlane per key word and round).  Measured slower (LDS is the tighter unit).
-  __shared__ uint4 rks[15];
-  if (threadIdx.x < 15)
-    rks[threadIdx.x] = make_uint4(rk.w[4 * threadIdx.x], rk.w[4 * threadIdx.x + 1], rk.w[4 * threadIdx.x + 2],
-                                  rk.w[4 * threadIdx.x + 3]);
-  if (TT2)
-    lds_fill_tables2(lds, tab);
-  else
-    lds_fill_tables(lds, tab);  // its barrier also publishes rks
-  // GK (single key): per-round reads from the device copy of the schedule instead
-  // (global_load_dwordx4 of a uniform address, L1-resident, 3 rounds ahead: no SGPR
-  // spill reloads, no LDS traffic; C3 +3.6 %, r01o A/B).  Multi-key runs keep the
-  // SGPR schedule (C5 -14 % with GK: its CW digest loads share the vector memory path).
-  constexpr bool GK = DCF_STREAM_GK && !MULTI && !TT2;
-  // Multi-key: keys DCF_MK_HK..14 from global memory (0 = all from SGPRs, which spill)
-  constexpr int HK = (MULTI && !TT2) ? DCF_MK_HK : 0;
-  constexpr int SL = (MULTI && !TT2) ? DCF_MK_SL : -1;
-  constexpr int SK = (MULTI && !TT2) ? DCF_MK_SK : 0;
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
   DCF_CLK(2, 0);
-  stream_run<NS, XREG, MULTI, TT2, kStreamUnit, DCF_LDS_KEYS != 0, GK, HK, PFX, D48, SL, NBC, SK>(
-      lds, (GK || HK || SK) ? rkg : rks, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total,
-      ctr, ys, pf);
+  stream_run<NS, XREG, MULTI, kStreamUnit, !MULTI, PFX, NBC>(lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs,
+                                                           nbytes, num_keys, ppk, total, ctr, ys, pf);
   DCF_CLK(2, 1);
 }
 

@@ -178,9 +178,6 @@ __device__ __forceinline__ uint4 w_row_piece(const uint8_t* __restrict__ cw_s, c
   return w;
 }
 
-#ifndef DCF_TAIL_BATCH
-#define DCF_TAIL_BATCH 2
-#endif
 
 __device__ __forceinline__ void tail_load_t(uint4 (&d)[4], const uint4* __restrict__ tv4, uint64_t pp, uint64_t p1) {
   pp = min<uint64_t>(pp, p1 - 1);
@@ -203,8 +200,8 @@ __device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst
   // v_perm builds e * 256 + q * 16 (+ 64 KiB per group of 16 chunks) from the t byte
   // and a lane constant, and c * 4096 mod 64 KiB rides in the ds_read offset field.
   uint32_t qb = 16u * q;
-  // DCF_TAIL_BATCH reads are issued before their XORs (more LDS reads in flight per wave)
-  constexpr uint32_t BT = DCF_TAIL_BATCH;
+  // BT reads are issued before their XORs (more LDS reads in flight per wave)
+  constexpr uint32_t BT = 2;
   for (uint32_t g16 = 0; g16 < nch16; ++g16) {  // full groups of 16 chunks (4 t words)
 #pragma unroll
     for (uint32_t j = 0; j < 16; j += BT) {
@@ -246,10 +243,7 @@ __device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst
   return make_uint4(acc[0], acc[1], acc[2], acc[3]);
 }
 
-#ifndef DCF_TAIL_NT
-#define DCF_TAIL_NT 1  // C4 A/B (r02z, paired-slot tail): nt 36.0-36.2 ms, plain 36.9-37.0
-#endif
-// Non-temporal (written once, never re-read here: measured 4 % faster) buffer store of
+// Non-temporal (written once, never re-read here; C4 A/B r02z: 36.0-36.2 ms vs 36.9-37.0 plain) buffer store of
 // a y piece; `kill` != 0 puts the lane's offset past num_records, which drops it.
 template <int LP>
 __device__ __forceinline__ void tail_store(uint8_t* ys, uint64_t pw, uint32_t pin, uint32_t lam, uint32_t off,
@@ -260,7 +254,7 @@ __device__ __forceinline__ void tail_store(uint8_t* ys, uint64_t pw, uint32_t pi
   uint8_t* wb = reinterpret_cast<uint8_t*>((uintptr_t)(((uint64_t)hi << 32) | lo));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(wb, (short)0, (int)((64 / LP) * lam), 0x00020000);
   const u32x4 v = {y.x, y.y, y.z, y.w};
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (pin * lam + off) | kill, 0, DCF_TAIL_NT ? 2 /* nt */ : 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (pin * lam + off) | kill, 0, 2 /* nt */);
 }
 
 // ------------------------------------------------------------------------
@@ -418,9 +412,6 @@ __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, 
   o4[1] = make_uint4(out[4], out[5], out[6], out[7]);
 }
 
-#ifndef DCF_TAIL2_BATCH
-#define DCF_TAIL2_BATCH 2
-#endif
 template <int R6, int R5>
 __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __restrict__ cw_s,
                                                              const uint8_t* __restrict__ cw_v,
@@ -432,6 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
                                                              uint8_t* __restrict__ ys) {
   using L = Tail2Layout<R6, R5>;
   constexpr int TW = 128, LP = 8;
+  DCF_CLK(4, 0);  // (diagnostic builds) workgroup entry, before the table build
   extern __shared__ uint4 G[];
   if ((uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)G != 0u) __builtin_trap();
   const uint32_t byte0 = (uint32_t)blockIdx.x * TW;
@@ -557,13 +549,14 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   load_t(tb, p + 3 * pstep);
   for (uint64_t pw = pw0; pw < p1; pw += 2 * pstep, p += 2 * pstep) {
     uint32_t aa[4] = {cst.x, cst.y, cst.z, cst.w}, ab[4] = {cst.x, cst.y, cst.z, cst.w};
-    // DCF_TAIL2_BATCH regions (4 reads each) are issued before their XORs: the compiler
+    constexpr int BT = 2;
+    // BT regions (4 reads each) are issued before their XORs: the compiler
     // otherwise waits after every two reads, ~3 reads in flight per wave
 #pragma unroll
-    for (int m0 = 0; m0 < L::R; m0 += DCF_TAIL2_BATCH) {
-      uint4 rb[DCF_TAIL2_BATCH][4];
+    for (int m0 = 0; m0 < L::R; m0 += BT) {
+      uint4 rb[BT][4];
 #pragma unroll
-      for (int k = 0; k < DCF_TAIL2_BATCH; ++k)
+      for (int k = 0; k < BT; ++k)
         if (m0 + k < L::R) {
           rb[k][0] = rd(twa, m0 + k, 0); rb[k][1] = rd(twa, m0 + k, 1);
           rb[k][2] = rd(twb, m0 + k, 0); rb[k][3] = rd(twb, m0 + k, 1);
@@ -573,13 +566,13 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
       // for its own read only (lgkmcnt counts down in order)
       asm volatile("" ::: "memory");
 #pragma unroll
-      for (int k = 0; k < DCF_TAIL2_BATCH; ++k)
+      for (int k = 0; k < BT; ++k)
         if (m0 + k < L::R)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             asm volatile("" : "+v"(rb[k][j].x), "+v"(rb[k][j].y), "+v"(rb[k][j].z), "+v"(rb[k][j].w));
 #pragma unroll
-      for (int k = 0; k < DCF_TAIL2_BATCH; ++k)
+      for (int k = 0; k < BT; ++k)
         if (m0 + k < L::R) {
           const uint4 a0 = rb[k][0], a1 = rb[k][1], b0 = rb[k][2], b1 = rb[k][3];
           aa[0] = xor3(aa[0], a0.x, a1.x); aa[1] = xor3(aa[1], a0.y, a1.y);

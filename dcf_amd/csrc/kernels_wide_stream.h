@@ -40,7 +40,7 @@ struct WidePrefix {
 template <int NS>
 struct WideLane {
   uint32_t s[NS][8], v[NS][8];           // bytes [0,32) of the seed and of the v accumulator
-  uint32_t dB[NS][4];                    // this level's B ^ ~s[0:16) (DCF_WHS_REUSE)
+  uint32_t dB[NS][4];                    // this level's B ^ ~s[0:16) (B reuse)
   uint32_t t[NS], ph[NS], lev[NS], cur[NS], tR[NS], tacc[NS];
   uint32_t xq[NS][3];                    // XREG: the point's next raw x words (byte-swapped on use)
   uint32_t pt[NS];                       // point index within this launch (<= 2^20); x row = xs + pt * N
@@ -101,10 +101,7 @@ __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, c
 // Points per refill of a wave.  A lane of C4 runs only ~16 points per launch (2^22 over 2^18
 // lanes), so the last units decide when the grid drains: 256-point units (4 per lane) left
 // ~11 % of the head's LDS instructions to lanes idling at the end (PMC: 265 per block vs 239).
-#ifndef DCF_WIDE_UNIT
-#define DCF_WIDE_UNIT 64
-#endif
-constexpr uint32_t kWideUnit = DCF_WIDE_UNIT;
+constexpr uint32_t kWideUnit = 64;
 
 template <int NS, bool XREG>
 __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, uint64_t& unext, uint64_t& uend,
@@ -155,14 +152,10 @@ __global__ void k_cw_digest(const uint8_t* __restrict__ cw_s, const uint8_t* __r
   if (q == 0) dig_t[l] = cw_t[ci];
 }
 
-#ifndef DCF_WHS_REUSE
-#define DCF_WHS_REUSE 1  // skip the B block after a right step at t = 0 (same output bytes)
-#endif
-#ifndef DCF_WHS_GK
-#define DCF_WHS_GK 0  // 1: round keys by buffer loads (vector L1) instead of LDS reads (C4 A/B: 38.4-38.5 vs 36.5 ms: the
-                      // key waits retire in order behind the CW loads); 2: both schedules by uniform loads, the lane's
-                      // key picked per word (r03f: 36.6-36.8 vs 35.3-35.4 ms, 56 more VALU per block)
-#endif
+// Round keys: the lane's schedule (cipher 0 or 17) from the LDS copy, one ds_read_b128 per round
+// and block.  Through the vector L1 instead (per-lane buffer loads, or both schedules by uniform
+// loads and a per-word pick) it measured 4-6 % slower on C4: the key waits retire in order behind
+// the CW loads (AB_LOG r02z / r03f).  B reuse: the B block after a right step at t = 0 is skipped.
 // Single key `key` of a num_keys-key CWB; count <= 2^20 points per launch.
 template <int NS, bool MASK_HEAD, bool XREG, int WG = kBlock>
 __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
@@ -171,6 +164,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     const uint8_t* __restrict__ s0p, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint32_t lam, const uint64_t num_keys, const uint64_t key, const uint64_t count, uint32_t* __restrict__ ctr,
     uint8_t* __restrict__ ys, uint32_t* __restrict__ tvec, const WidePrefix pf) {
+  DCF_CLK(5, 0);  // (diagnostic builds) workgroup entry, before the table fill
   __shared__ uint32_t lds[kLdsWords];
   // Schedules of cipher 0 (slots 0..14) and cipher 17 (slots 23..37): 23 slots apart,
   // so lanes reading the two never share a ds_read_b128 bank group.
@@ -179,7 +173,6 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   lds_fill_tables(lds, tab);  // its barrier also publishes rks
   DCF_CLK(1, 0);
   const uint32_t rks_a = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)rks;  // LDS byte address
-  const __amdgpu_buffer_rsrc_t rkrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(rk2), (short)0, 480, 0x00020000);
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
   const uint64_t nunits = (count + kWideUnit - 1) / kWideUnit;
@@ -213,33 +206,6 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     // 17 zeroing moves per step and the loads issued anyway.  Issued before the AES and
     // pinned after it, so they are waited on long after the last y / t-vector stores
     // (vmcnt is in order: a load issued after a store cannot be waited on alone).
-    // DCF_WHS_GK: the lane's round keys through the vector L1 (rounds 0 .. 2 loaded here, before
-    // the CW loads, so waiting for them never waits for those; later rounds 3 ahead in the AES)
-    uint32_t ko[NS];
-    uint4 kq[NS][3], k0g[NS];
-    // DCF_WHS_GK == 2: both schedules by uniform loads (rounds 0 .. 2 here, before the CW loads)
-    constexpr int GA = 3;
-    uint4 qa[GA], qb[GA];
-    if (DCF_WHS_GK == 2) {
-#pragma unroll
-      for (int q = 0; q < GA; ++q) {
-        qa[q] = rk2[q];
-        qb[q] = rk2[15 + q];
-      }
-    }
-    if (DCF_WHS_GK == 1) {
-      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-#pragma unroll
-      for (int i = 0; i < NS; ++i) {
-        ko[i] = 240u * ((L.ph[i] != 0u) & (L.cur[i] >> 31));  // cipher 17's schedule: 15 keys on
-        const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rkrs, ko[i], 0, 0);
-        const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rkrs, ko[i] + 16u, 0, 0);
-        const v4u c = __builtin_amdgcn_raw_buffer_load_b128(rkrs, ko[i] + 32u, 0, 0);
-        k0g[i] = make_uint4(a.x, a.y, a.z, a.w);
-        kq[i][0] = make_uint4(b.x, b.y, b.z, b.w);
-        kq[i][1] = make_uint4(c.x, c.y, c.z, c.w);
-      }
-    }
     uint4 cs[NS][2], cv[NS][2];
     uint32_t ct[NS];
 #pragma unroll
@@ -262,19 +228,10 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       // cipher 17's schedule sits 23 slots on.  The empty asm keeps the compiler from
       // re-associating base + 16 r (rks_a is a link-time symbol: 14 materialised constants and
       // a v_mad per round); the mask proves the sign bit clear, so +16 r folds into ds_read
-      uint4 k0;
-      if (DCF_WHS_GK == 2) {
-        const uint32_t m = 0u - hi;
-        k0 = make_uint4(pick(m, qb[0].x, qa[0].x), pick(m, qb[0].y, qa[0].y), pick(m, qb[0].z, qa[0].z),
-                        pick(m, qb[0].w, qa[0].w));
-      } else if (DCF_WHS_GK == 1) {
-        k0 = k0g[i];
-      } else {
-        uint32_t kb = rks_a + 368u * hi;
-        asm volatile("" : "+v"(kb));
-        ka[i] = kb & 0x3FFFFu;
-        k0 = lds_load16(ka[i]);
-      }
+      uint32_t kb = rks_a + 368u * hi;
+      asm volatile("" : "+v"(kb));
+      ka[i] = kb & 0x3FFFFu;
+      const uint4 k0 = lds_load16(ka[i]);
       const uint32_t hm = 0u - hi;
       const uint32_t k0w[4] = {k0.x, k0.y, k0.z, k0.w};
 #pragma unroll
@@ -283,24 +240,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
         st[i][j] = xor3(sel[i][j], inv[i], k0w[j]);  // round key 0 folded in
       }
     }
-    if (DCF_WHS_GK == 2) {
-      uint32_t hms[NS];
-#pragma unroll
-      for (int i = 0; i < NS; ++i) hms[i] = 0u - ((L.ph[i] != 0u) & (L.cur[i] >> 31));
-      // rounds 1 .. GA - 1 are in qa / qb[0 .. GA - 2] after a shift by one slot
-      uint4 ra[GA], rb[GA];
-#pragma unroll
-      for (int q = 0; q + 1 < GA; ++q) {
-        ra[q] = qa[q + 1];
-        rb[q] = qb[q + 1];
-      }
-      ra[GA - 1] = qa[0];
-      rb[GA - 1] = qb[0];
-      aes_tt_gk2<14, NS, GA>(st, hms, rk2, rk2 + 15, ra, rb, lds, lc);
-    } else if (DCF_WHS_GK == 1)
-      aes_tt_bk<14, NS, 3>(st, ko, rkrs, kq, lds, lc);
-    else
-      aes_tt_lka<14, NS, true>(st, ka, lds, lc);
+    aes_tt_lka<14, NS, true>(st, ka, lds, lc);
 #pragma unroll
     for (int i = 0; i < NS; ++i)
       asm volatile("" : "+v"(cs[i][0].x), "+v"(cs[i][0].y), "+v"(cs[i][0].z), "+v"(cs[i][0].w), "+v"(cs[i][1].x),
@@ -323,13 +263,11 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
 #pragma unroll
       for (int j = 0; j < 4; ++j) d[j] = xor3(st[i][j], sel[i][j], inv[i]);
       L.tR[i] = mB ? (d[0] & 1u) : L.tR[i];  // t_R = lsb(B ^ ~s)[0] (prg.rs:64)
-      if (DCF_WHS_REUSE) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) L.dB[i][j] = pick(mB, d[j], L.dB[i][j]);
-      }
+      for (int j = 0; j < 4; ++j) L.dB[i][j] = pick(mB, d[j], L.dB[i][j]);
       // B reuse: a right step at t = 0 leaves s[0:16) as it is (s_R = s with only [16:32)
       // replaced, ^ 0 cw_s), so the next level's B = E0(~s[0:16)) is this level's
-      const uint32_t ru = DCF_WHS_REUSE ? (mC & (L.t[i] - 1u)) : 0u;
+      const uint32_t ru = mC & (L.t[i] - 1u);
       const uint32_t tb = ((mA ? d[0] : L.tR[i]) & 1u) ^ (L.t[i] & (ct[i] >> xb) & 1u);  // lib.rs:179-180
       const uint32_t csw[8] = {cs[i][0].x, cs[i][0].y, cs[i][0].z, cs[i][0].w,
                                cs[i][1].x, cs[i][1].y, cs[i][1].z, cs[i][1].w};
@@ -393,7 +331,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
         y4[0] = make_uint4(y[0], y[1], y[2], y[3]);
         y4[1] = make_uint4(y[4], y[5], y[6], y[7]);
       }
-      if (DCF_WHS_REUSE) {  // the skipped B step of the next level: v[0:16) ^= B ^ ~s when it goes left
+      {  // the skipped B step of the next level: v[0:16) ^= B ^ ~s when it goes left
         const uint32_t ml = 0u - (uint32_t)(reuse & ((L.cur[i] >> 31) == 0u));
 #pragma unroll
         for (int j = 0; j < 4; ++j) L.v[i][j] = xand(L.v[i][j], ml, L.dB[i][j]);

@@ -19,8 +19,13 @@ import torch
 import torch.distributed as dist
 
 
+def active() -> bool:
+    """A process group is up (possibly of world size 1: the RCCL path still runs then)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def world() -> Tuple[int, int]:
-    if dist.is_available() and dist.is_initialized():
+    if active():
         return dist.get_world_size(), dist.get_rank()
     return 1, 0
 
@@ -41,9 +46,10 @@ def weak_slice(per_rank: int, rank: int) -> Tuple[int, int]:
 
 
 def broadcast_key(tensors: List[torch.Tensor], src: int = 0) -> List[torch.Tensor]:
-    """Broadcast key material (CWB, seeds, ...) from `src` to every rank, in place."""
-    ws, _ = world()
-    if ws > 1:
+    """Broadcast key material (CWB, seeds, ...) from `src` to every rank, in place.  Runs
+    the collective whenever a process group is up, also at world size 1 (so a one-GPU run
+    exercises the same RCCL broadcast an 8-GPU run does)."""
+    if active():
         for t in tensors:
             dist.broadcast(t, src=src)
     return tensors
@@ -60,10 +66,11 @@ def gather_shares(ys: torch.Tensor, dst: int = 0, counts: Optional[Sequence[int]
     (point_slice gives the first total % world ranks one extra point): the row counts are
     all-gathered (or taken from `counts`), every slice is padded to the longest for the
     collective, and dst trims the padding.  Returns the concatenation (on ys's device)
-    on dst, None elsewhere."""
-    ws, rank = world()
-    if ws == 1:
+    on dst, None elsewhere.  With a process group up the collectives run at any world
+    size, 1 included; without one the slice is the whole output."""
+    if not active():
         return ys
+    ws, rank = world()
     dev = ys.device
     host = _host_collectives(ys)
     if counts is None:

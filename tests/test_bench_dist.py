@@ -44,3 +44,21 @@ def test_bench_two_ranks_strong_scaling_check():
         assert r["kernel_ms"] > 0 and r["walk_ms"] > 0 and r["table_ms"] >= 0 and r["prefix_levels"] == 21
     assert pr["imbalance"] >= 1.0
     assert d["key_broadcast"]["ms"] is not None and d["key_broadcast"]["bytes"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_rccl_world1_line():
+    """bench.py at N = 1 with --force-dist over RCCL: the key broadcast, the timing all-reduce,
+    the per-rank all_gather_object and --check's digest gather all go through RCCL, and the
+    line says so (key_broadcast.backend == "nccl")."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "2", "--warmup", "1", "--points", str((1 << 22) + 3), "--no-cpu",
+           "--no-compare", "--dist-backend", "nccl", "--force-dist", "--check"]
+    out = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ), capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["key_broadcast"]["backend"] == "nccl" and d["key_broadcast"]["bytes"] > 0
+    assert d["slice_check"]["slices_match"]
+    assert [r["rank"] for r in d["per_rank"]["ranks"]] == [0]

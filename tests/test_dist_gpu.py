@@ -61,3 +61,52 @@ def test_two_rank_hip_eval_gather_odd_total(tmp_path, total, nb):
     full, ref = np.load(out)
     assert full.shape == (total, 16)
     assert np.array_equal(full, ref)
+
+
+def _rccl_worker(rank, port, out_path, total, nb):
+    """World size 1 over RCCL (backend "nccl"): the same broadcast / gather / object
+    all-gather calls an 8-GPU run makes, on GPU tensors, so RCCL itself executes here."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    import dcf_amd
+    from dcf_amd.dist import broadcast_key, gather_shares, point_slice
+    lam = 16
+    rng = np.random.default_rng(47)
+    keys = [rng.bytes(32) for _ in range(2)]
+    d = dcf_amd.DcfImpl(nb, lam, dcf_amd.Aes256HirosePrg(keys, lam))
+    s0, s1 = rng.bytes(lam), rng.bytes(lam)
+    k = d.gen(dcf_amd.CmpFn(rng.bytes(nb), rng.bytes(lam)), [s0, s1], dcf_amd.BoundState.LtBeta)
+    cwb_src = torch.from_numpy(np.frombuffer(dcf_amd.share_to_cwb(k, nb, lam), np.uint8).copy()).cuda()
+    seeds_src = torch.from_numpy(np.frombuffer(s0 + s1, np.uint8).reshape(2, lam).copy()).cuda()
+    cwb, seeds = cwb_src.clone(), seeds_src.clone()
+    broadcast_key([cwb, seeds])                       # ncclBroadcast (root 0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    xs = torch.randint(0, 256, (total, nb), dtype=torch.uint8, device="cuda", generator=g)
+    start, cnt = point_slice(total, 1, 0)
+    ys = d.eval_device(False, cwb, seeds[0].contiguous(), xs[start:start + cnt].contiguous())
+    full = gather_shares(ys)                          # row-count all_gather + ncclGather on GPU tensors
+    objs = [None]
+    dist.all_gather_object(objs, {"rank": 0, "rows": int(ys.shape[0])})
+    ref = d.eval_device(False, cwb_src, seeds_src[0].contiguous(), xs)
+    torch.cuda.synchronize()
+    np.save(out_path, np.stack([full.cpu().numpy(), ref.cpu().numpy()]))
+    assert torch.equal(cwb, cwb_src) and torch.equal(seeds, seeds_src)
+    assert full.is_cuda and objs == [{"rank": 0, "rows": total}]
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_world1_broadcast_gather_identical():
+    """RCCL executes (nccl backend, world 1): broadcast_key, gather_shares on GPU tensors and
+    all_gather_object; the gathered shares equal one dcf_eval_device byte for byte."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "res.npy")
+        mp.spawn(_rccl_worker, args=(_free_port(), out, 300_007, 16), nprocs=1, join=True)
+        full, ref = np.load(out)
+    assert full.shape == (300_007, 16)
+    assert np.array_equal(full, ref)

@@ -67,7 +67,7 @@ def _ror(vals, n):
 ROT1, ROT2, ROT3, BC0 = (1, 2, 3, 0), (2, 3, 0, 1), (3, 0, 1, 2), (0, 0, 0, 0)
 
 
-LATE_DPP = True  # kernels_lat.h DCF_COL_LATE_DPP: rotate the lookup results instead of the inputs
+LATE_DPP = True  # kernels_lat.h aes256_col: rotate the lookup results instead of the inputs
 
 
 def aes_cols(st, rk):

@@ -2,11 +2,11 @@
 dcf_prg (include/dcf_hip.h "Threading"), on the GPU, byte-identical to the oracle.
 
 * k_eval16_row (32 lanes per point, one lookup per lane and round) serves auto-mode
-  single-key eval up to DCF_EVAL_ROW_MAX points and k_eval16_oct (8 lanes per point) up to
-  DCF_EVAL_OCT_MAX points, through the device entry point and through the host entry
+  single-key eval up to kEvalRowMax points and k_eval16_oct (8 lanes per point) up to
+  kEvalOctMax points, through the device entry point and through the host entry
   point's tiny path (the kernel reads the key and points from, and writes the outputs
   to, mapped pinned memory); k_gen16_col (16 lanes per key) serves gen up to
-  DCF_GEN_COL_MAX keys (dcf_gen and dcf_gen_batch_device).
+  kGenColMax keys (dcf_gen and dcf_gen_batch_device).
 * One prg shared by 8 host threads (the reference's `&self` + `Prg: Sync`, lib.rs:34,52),
   each thread with its own key and points, host and device entry points mixed; and a host
   call queued right after a device call on the same prg with no synchronize in between
