@@ -887,7 +887,17 @@ def run_latency(args, world, rank):
                     "to back (~0.75 us per level at 2.4 GHz); batch the points (C1) for throughput"}
 
 
+def json_stdout():
+    """The JSON line's stream.  File descriptor 1 is pointed at stderr for the rest of the run,
+    so that nothing a library prints on stdout (RCCL's version banner at communicator init)
+    can land beside the one JSON line the driver parses."""
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
+
+
 def main():
+    out_stream = json_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -952,7 +962,7 @@ def main():
         out["metric"] = (f"DCF evals/sec, workload {args.workload.upper()}, {args.prg} PRG "
                          "(not the BASELINE.json headline config)")
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=out_stream, flush=True)
     if pg():
         dist.barrier()
         dist.destroy_process_group()

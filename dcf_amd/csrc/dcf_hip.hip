@@ -247,7 +247,8 @@ struct Lease {
 };
 
 constexpr int kPrefixNoMem = -100;            // build_prefix: table allocation failed (internal)
-constexpr uint64_t kWideChunk = 1ull << 22;   // points per head/tail pass (t-vector scratch 256 MiB)
+constexpr uint64_t kWideChunk = 1ull << 22;   // points per head/tail pass (t-vector scratch 256 MiB at N <= 31)
+constexpr size_t kWideMaxN = 159;             // LAMBDA >= 32 eval: N <= 159 (see eval_wide)
 constexpr uint64_t kGenChunk = 4096;          // keys per wide-gen launch (scratch 3*LAMBDA per key)
 constexpr uint32_t kTailPts = 4096;          // points per tail workgroup (one table build each)
 
@@ -494,6 +495,7 @@ template <int TW, int NCH = 0>
 int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
                 uint32_t lam, uint64_t K, uint64_t key, const uint32_t* tvec, uint64_t cnt, uint8_t* ys,
                 hipStream_t st) {
+  static_assert(TW == 32 || TW == 64 || TW == 128 || TW == 256, "tile width");
   const uint32_t nch = (nlev + 1 + 3) / 4;
   const size_t lds = (size_t)nch * 16 * TW;
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail<TW, NCH>),
@@ -504,58 +506,81 @@ int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, cons
   const uint64_t tiles = (lam + TW - 1) / TW;
   const dim3 grid((unsigned)tiles, (unsigned)((cnt + kTailPts - 1) / kTailPts));
   hipLaunchKernelGGL((k_eval_wide_tail<TW, NCH>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key, tvec,
-                     cnt, kTailPts, ys);
+                     cnt, kTailPts, ys, t_words(nlev));
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }
 
-// Paired-slot tail (k_eval_wide_tail2, 128-byte tiles, 6/5-bit chunks): the t-vectors are
-// repacked into chunk bytes in place, then the tail runs as launch_tail does.
-template <int R6, int R5>
+// Paired-slot tail (k_eval_wide_tail2, 128-byte tiles, 6/5-bit chunks in LDS, G8 8-bit chunks in
+// global memory): the t-vectors are repacked into chunk bytes in place, the global chunk tables
+// are built (gtab: tiles x G8 x 32 KiB of scratch), then the tail runs as launch_tail does.
+template <int R6, int R5, int G8>
 int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
-                 uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
-                 int cus) {
-  using L = Tail2Layout<R6, R5>;
+                 uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, uint4* gtab,
+                 hipStream_t st, int cus) {
+  using L = Tail2Layout<R6, R5, G8>;
   if (nlev + 1 > L::rows()) return fail(DCF_ERR_UNSUPPORTED, "tail2 layout too small");
-  hipLaunchKernelGGL((k_tvec_chunks<R6, R5>), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tvec, nlev, cnt);
+  const uint64_t tiles = (lam + 127) / 128;
+  hipLaunchKernelGGL((k_tvec_chunks<R6, R5, G8>), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tvec, nlev,
+                     cnt);
   HIP_TRY(hipGetLastError());
+  if constexpr (G8 > 0) {
+    hipLaunchKernelGGL((k_tail_gtab<R6, R5, G8>), dim3((unsigned)tiles, (unsigned)G8), dim3(256), 0, st, cws, cwv, np1,
+                       nlev, lam, K, key, gtab);
+    HIP_TRY(hipGetLastError());
+  }
   const size_t lds = L::lds_bytes();
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5>),
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5, G8>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // One workgroup per CU: the batch split into cus / tiles ranges, so the tiles of a range build
   // their tables once and walk its points together (the rows being written at any time stay
   // few), at least 32768 points per workgroup (C4 A/B: 34.36-34.38 ms vs 34.78-35.01 with
   // 32768-point ranges; 4096-point ranges 37.8-38.0).
-  const uint64_t tiles = (lam + 127) / 128;
   const uint64_t ranges = std::max<uint64_t>(1, (uint64_t)cus / tiles);
   const uint64_t per = std::max<uint64_t>(32768, (((cnt + ranges - 1) / ranges) + 255) & ~(uint64_t)255);
   const dim3 grid((unsigned)tiles, (unsigned)((cnt + per - 1) / per));
-  hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key,
-                     tvec, cnt, (uint32_t)per, ys);
+  hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5, G8>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K,
+                     key, tvec, cnt, (uint32_t)per, ys, (const uint4*)gtab);
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }
 
+// Global-table scratch of the largest paired-slot layout (launch_tail2's gtab), per 128-byte tile.
+constexpr size_t kGtabBytesPerTile = 5 * 256 * 128;
+
 // The tail for n = nlev levels: the paired-slot tail when one of its instances covers the
 // n + 1 rows with fewer LDS reads than the 4-bit tail's ceil((n + 1) / 4), else the 4-bit one.
 int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
-             uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
-             int cus) {
+             uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, uint4* gtab,
+             hipStream_t st, int cus) {
   const uint32_t nrows = nlev + 1, nch = (nrows + 3) / 4;
   if (lam % 128 == 0) {
-#define DCF_T2(A, B)                                                                            \
-  if (nrows <= Tail2Layout<A, B>::rows() && 2u * (A + B) < nch)                                 \
-    return launch_tail2<A, B>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus);
-    DCF_T2(1, 0)   // N = 1: 9 rows, 2 reads (4-bit: 3)
-    DCF_T2(1, 1)   // N = 2: 17 rows, 4 reads (5)
-    DCF_T2(2, 1)   // N = 3, 4: 25 / 33 rows, 6 reads (7 / 9)
-    DCF_T2(3, 3)   // N = 6..8: 49..65 rows, 12 reads (13..17)
-    DCF_T2(5, 7)   // N = 12..16: 97..129 rows, 24 reads (25..33)
+#define DCF_T2(A, B, G)                                                                            \
+  if (nrows <= Tail2Layout<A, B, G>::rows() && 2u * (A + B) < nch)                                 \
+    return launch_tail2<A, B, G>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, gtab, st, cus);
+    DCF_T2(1, 0, 0)   // N = 1: 9 rows, 2 reads (4-bit: 3)
+    DCF_T2(1, 1, 0)   // N = 2: 17 rows, 4 reads (5)
+    DCF_T2(2, 1, 0)   // N = 3, 4: 25 / 33 rows, 6 reads (7 / 9)
+    DCF_T2(3, 3, 0)   // N = 6..8: 49..65 rows, 12 reads (13..17)
+#ifndef DCF_T3
+#define DCF_T3 0
+#endif
+#if DCF_T3 == 3
+    DCF_T2(5, 5, 3)
+#elif DCF_T3 == 4
+    DCF_T2(5, 4, 4)
+#elif DCF_T3 == 5
+    DCF_T2(5, 3, 5)
+#endif
+    DCF_T2(5, 7, 0)   // N = 12..16: 97..129 rows, 24 reads (25..33)
 #undef DCF_T2
   }
-  return (nch == 33) ? launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st)
-       : (nch <= 40) ? launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st)
-                     : launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
+  // 4-bit tail: the widest tile whose tables (nch x 16 entries x TW bytes) fit the LDS
+  if (nch == 33) return launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
+  if (nch <= 40) return launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
+  if (nch <= 80) return launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
+  if (nch <= 160) return launch_tail<64>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
+  return launch_tail<32>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
 }
 
 // Dcf::eval at LAMBDA >= 32 for key `key` of a K-key CWB (see kernels_wide.h).
@@ -563,16 +588,20 @@ int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const u
 int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
               const uint8_t* s0, const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nlev = (uint32_t)(8 * n_bytes);
-  if (n_bytes > 31) return fail(DCF_ERR_UNSUPPORTED, "LAMBDA >= 32 eval supports N <= 31");
+  // the 4-bit tail's tables: (8N + 1) / 4 chunks x 16 entries x 32-byte tiles <= 160 KiB
+  if (n_bytes > kWideMaxN) return fail(DCF_ERR_UNSUPPORTED, "LAMBDA >= 32 eval supports N <= 159");
   const size_t n = 8 * n_bytes;
   const uint8_t* cws = cwb;
   const uint8_t* cwv = cwb + n * K * lam;
   const uint8_t* cwt = cwb + 2 * n * K * lam;
   const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
   const uint64_t chunk = m < kWideChunk ? m : kWideChunk;
-  int rc = ensure_ws(w, chunk * kTWords * 4, st);
+  const uint32_t tw = t_words(nlev);  // t-vector words per point
+  const size_t tvb = (chunk * tw * 4 + 255) & ~(size_t)255;
+  int rc = ensure_ws(w, tvb + ((lam + 127) / 128) * kGtabBytesPerTile, st);
   if (rc) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
+  uint4* gtab = reinterpret_cast<uint4*>(w->d_ws + tvb);
   WidePrefix wpf{nullptr, 0u};
   const int mode = c.mode;
   for (uint64_t off = 0; off < m; off += chunk) {
@@ -603,7 +632,7 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
 #define DCF_WHS(MH, XR)                                                                                        \
   hipLaunchKernelGGL((k_eval_wide_head_stream<1, MH, XR, kBlock>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab,     \
                      p->d_rk2, (const uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
-                     lam, K, key, cnt, w->d_ctr, ys + off * lam, tvec, wpf)
+                     lam, K, key, cnt, w->d_ctr, ys + off * lam, tvec, wpf, tw)
       const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16;
       if (lam == 32 && xreg) DCF_WHS(true, true);
       else if (lam == 32) DCF_WHS(true, false);
@@ -613,14 +642,14 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
     } else if (lam == 32)
       hipLaunchKernelGGL(k_eval_wide_head<true>, grid, dim3(kBlock), 0, st, p->d_tab, p->rk[0], p->rk[17], cws, cwv,
                          cwt, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes, lam, K, key, cnt,
-                         ys + off * lam, tvec);
+                         ys + off * lam, tvec, tw);
     else
       hipLaunchKernelGGL(k_eval_wide_head<false>, grid, dim3(kBlock), 0, st, p->d_tab, p->rk[0], p->rk[17], cws,
                          cwv, cwt, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes, lam, K, key, cnt,
-                         ys + off * lam, tvec);
+                         ys + off * lam, tvec, tw);
     HIP_TRY(hipGetLastError());
     if (lam > 32) {
-      rc = run_tail(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus);
+      rc = run_tail(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, gtab, st, p->cus);
       if (rc) return rc;
     }
   }
@@ -847,7 +876,7 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   const bool small = total < (uint64_t)p->cus * kBlock * 2;
   if (p->kind == 1 && p->lambda > 16) return 0;  // MMO at LAMBDA >= 32: no shared prefix (head/tail per block)
   if (p->kind == 1) return small && c.prefix_levels < 0 ? 0 : (int)prefix_depth(p, c, n_bytes, num_keys, total);
-  if (p->lambda > 16) return n_bytes > 31 ? 0 : (int)wide_prefix_depth(p, c, n_bytes, points_per_key);
+  if (p->lambda > 16) return n_bytes > kWideMaxN ? 0 : (int)wide_prefix_depth(p, c, n_bytes, points_per_key);
   if (c.mode == DCF_EVAL_AUTO && small) return num_keys == 1 ? (int)small_prefix_depth(p, c, n_bytes) : 0;
   if (c.mode != DCF_EVAL_AUTO && c.mode != DCF_EVAL_STREAM && c.mode != DCF_EVAL_STREAM_HYBRID) return 0;
   return (int)prefix_depth(p, c, n_bytes, num_keys, total);
@@ -1205,12 +1234,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
     uint64_t blocks = (units + waves - 1) / waves;
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
-    uint4* slabs = nullptr;
-    if (mem) {
-      int rc = ensure_slabs(p, w, st);
-      if (rc) return rc;
-      slabs = reinterpret_cast<uint4*>(w->d_slabs);
-    }
+    if (int rc = ensure_slabs(p, w, st)) return rc;
+    uint4* slabs = reinterpret_cast<uint4*>(w->d_slabs);
     phase_mark(p, L, 1);
     const dim3 g((unsigned)blocks), b((unsigned)(waves * 64));
 #define DCF_HYB(XA, MEM)                                                                                   \
@@ -1242,7 +1267,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
     hipLaunchKernelGGL(k_eval16_shybrid, dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
                        (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, w->d_ctr,
-                       (uint4*)ys, pf, c.shy_mask, (uint32_t)c.shy_prio, reinterpret_cast<uint4*>(w->d_slabs), p->d_km);
+                       (uint4*)ys, pf, c.shy_mask, (uint32_t)c.shy_prio, reinterpret_cast<uint4*>(w->d_slabs), p->d_km,
+                       p->d_rk0);
   } else if (mode == DCF_EVAL_STREAM) {
     constexpr int NS = 2;  // streams per lane
     const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16, multi = num_keys > 1;
@@ -1341,17 +1367,19 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     }
   } else if (mode == DCF_EVAL_BITSLICED) {
     if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
+    if (int rc = ensure_slabs(p, w, st)) return rc;  // cus x 16 wave slabs: one per resident wave
     phase_mark(p, L, 1);
     const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;
     uint64_t blocks = (waves + 3) / 4;
-    const uint64_t cap = (uint64_t)p->cus * 8;
+    const uint64_t cap = (uint64_t)p->cus * 4;  // 4 workgroups of 4 waves per CU (<= 128 VGPRs)
     if (blocks > cap) blocks = cap;
+    uint4* slabs = reinterpret_cast<uint4*>(w->d_slabs);
     if (n_bytes % 4 == 0)
       hipLaunchKernelGGL(k_eval16_bs<true>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
-                         (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
+                         (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, slabs, (uint4*)ys);
     else
       hipLaunchKernelGGL(k_eval16_bs<false>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
-                         (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint4*)ys);
+                         (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, slabs, (uint4*)ys);
   } else {  // lockstep T-table, 64-point units from the work counter
     if ((total + 63) / 64 > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "more than 2^32 64-point units");
     phase_mark(p, L, 1);

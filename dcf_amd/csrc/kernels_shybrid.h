@@ -24,11 +24,10 @@ namespace {
 constexpr int kQpBcast3 = 3 | (3 << 2) | (3 << 4) | (3 << 6);  // c <- 3
 constexpr int kShybridXlSlots = 12;  // LDS: 128 KiB tables + 2 KiB of transposed x per bitsliced wave
 
-// One wave's 512 points (32 per quad) through the bitsliced engine, starting at
-// level pf.levels from the points' rows of the shared-prefix table (or at the
-// root when pf.levels = 0).  x rows are 4-byte aligned (nbytes % 4 == 0, <= 16).
-// v is kept in the wave's scratch slab (as bs_eval_batch_mem) so a lane fits in
-// 128 VGPRs next to 15 other waves.
+// One wave's 512 points (32 per quad) through the bitsliced engine (kernels_bs.h bs_level: s
+// and v in the wave's slab), starting at level pf.levels from the points' rows of the
+// shared-prefix table (or at the root when pf.levels = 0).  x rows are 4-byte aligned
+// (nbytes % 4 == 0, <= 16).
 __device__ __forceinline__ void bs_eval_batch_pf(const uint4* __restrict__ km, const uint4* __restrict__ cw_s,
                                                  const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
                                                  const uint4 np1, const uint4 s0v, const uint32_t party,
@@ -40,112 +39,53 @@ __device__ __forceinline__ void bs_eval_batch_pf(const uint4* __restrict__ km, c
   const uint64_t p0 = p_base + (uint64_t)quad * kBsPoints;
   const uint32_t nlev = 8u * nbytes, nchunk = nbytes >> 2, D = pf.levels;
   const uint4* __restrict__ kmc = km + 8 * c;
-  uint4* __restrict__ vp = slab + lane;  // v quad q at vp[64 q]
+  uint4* __restrict__ vp = slab + lane;
+  uint4* __restrict__ sp = slab + 512 + lane;
   const uint32_t mlast = (c == 3u) ? 0u : 0xFFFFFFFFu;  // register 24 of column 3 = bit 0 of byte 15
-  uint32_t s[32];
   uint32_t T;
   if (D) {
-    // Row of the top-tree table named by each point's first D x bits (Msb0): this
-    // lane's column of s and of v, transposed into bitsliced registers.
-    uint32_t u[32];
+    // Row of the top-tree table named by each point's first D x bits (Msb0): this lane's
+    // column of v, then of s, transposed into bitsliced words.  Gathered 8 rows per pass of a
+    // loop that is not unrolled, shifted into place (a shift register of 32 words): 32
+    // independent 64-bit gather addresses in flight spilled 128 VGPRs.
+    uint32_t a[32];
+    for (uint32_t half = 0; half < 2; ++half) {
+#pragma unroll 1
+      for (uint32_t g = 0; g < 4; ++g) {
+        uint32_t t8[8];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const uint64_t p = min(p0 + j, m - 1);
-      const uint32_t idx = bswap32(*reinterpret_cast<const uint32_t*>(xs + p * nbytes)) >> (32u - D);
-      const uint32_t* row = reinterpret_cast<const uint32_t*>(pf.sv + 2u * idx);
-      s[j] = row[c];
-      u[j] = row[4u + c];
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t p = min(p0 + 8u * g + k, m - 1);
+          const uint32_t idx = bswap32(*reinterpret_cast<const uint32_t*>(xs + p * nbytes)) >> (32u - D);
+          t8[k] = reinterpret_cast<const uint32_t*>(pf.sv + 2u * idx)[(half ? 0u : 4u) + c];
+        }
+#pragma unroll
+        for (int k = 0; k < 24; ++k) a[k] = a[k + 8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[24 + k] = t8[k];
+      }
+      transpose32(a);
+      if (half == 0) bs_store32(vp, a);
     }
-    transpose32(s);
-    transpose32(u);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) vp[64 * q] = make_uint4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]);
-    T = qperm<kQpBcast3>(s[24]);  // t rides in s's masked bit (kernels16.h PrefixTable)
-    s[24] &= mlast;
+    T = qperm<kQpBcast3>(a[24]);  // t rides in s's masked bit (kernels16.h PrefixTable)
+    a[24] &= mlast;
+    bs_store32(sp, a);
   } else {
-    bs_splat(s, sel4(s0v, c));
-#pragma unroll
-    for (int q = 0; q < 8; ++q) vp[64 * q] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t a[32], w0 = sel4(s0v, c);
+    asm volatile("" : "+v"(w0));  // not hoisted out of the batch loop (32 live masks)
+    bs_splat(a, w0);
+    bs_store32(sp, a);
+    for (int i = 0; i < 32; ++i) a[i] = 0u;
+    bs_store32(vp, a);
     T = party ? 0xFFFFFFFFu : 0u;
   }
   uint32_t lev = D;
   for (uint32_t cc = D >> 5; cc < nchunk; ++cc) {
-    __builtin_amdgcn_wave_barrier();
-    if (c == cc) {
-      uint32_t w[32];
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const uint64_t p = min(p0 + j, m - 1);
-        w[j] = bswap32(*reinterpret_cast<const uint32_t*>(xs + p * nbytes + 4 * cc));
-      }
-      transpose32(w);
-#pragma unroll
-      for (int i = 0; i < 32; ++i) xl[(31u - i) * 16u + quad] = w[i];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t b = lev - 32u * cc; b < 32u; ++b, ++lev) {
-      const uint32_t X = xl[b * 16u + quad];  // bit j: x bit of point j (1 = right)
-      const uint4 cs = cw_s[lev], cv = cw_v[lev];
-      const uint32_t ct = cw_t[lev];
-      uint32_t csw = sel4(cs, c), cvw = sel4(cv, c);
-      uint32_t st[32];
-      // B = AES(~s); v ^= ((~s) ^ (B & ~X)) & M ^ (T & cw.v)   (lib.rs:182/186)
-#pragma unroll
-      for (int i = 0; i < 32; ++i) st[i] = s[i];
-      bs_aes256(st, kmc, true);
-      asm volatile("" : "+v"(cvw));
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        uint4 vv = vp[64 * q];
-        uint32_t va[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * q + e;
-          uint32_t hv = (~s[i]) ^ (st[i] & ~X);
-          if (i == 24) hv &= mlast;
-          va[e] ^= hv ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)cvw, i, 1));
-        }
-        vp[64 * q] = make_uint4(va[0], va[1], va[2], va[3]);
-      }
-      const uint32_t tR = qperm<kQpBcast0>(st[0] ^ ~s[0]);
-      // A = AES(s); s' = (s ^ (A & ~X)) & M ^ (T & cw.s)   (lib.rs:177-178, 183/187)
-#pragma unroll
-      for (int i = 0; i < 32; ++i) st[i] = s[i];
-      bs_aes256(st, kmc, false);
-      const uint32_t tL = qperm<kQpBcast0>(st[0] ^ s[0]);
-      asm volatile("" : "+v"(csw));
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        uint32_t hs = s[i] ^ (st[i] & ~X);
-        if (i == 24) hs &= mlast;
-        s[i] = hs ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)csw, i, 1));
-      }
-      // t' = side t ^ (t & side cw.t)   (lib.rs:179-180)
-      const uint32_t ctl = 0u - (ct & 1u), ctr = 0u - ((ct >> 1) & 1u);
-      T = ((X & tR) | (~X & tL)) ^ (T & ((X & ctr) | (~X & ctl)));
-    }
+    bs_stage_x<true>(xl, xs, nbytes, m, p0, cc);
+    for (uint32_t b = lev - 32u * cc; b < 32u; ++b, ++lev)
+      bs_level(kmc, vp, sp, xl + b * 16u + quad, T, cw_s[lev], cw_v[lev], cw_t[lev]);
   }
-  // y = v ^ s ^ t * cw_np1   (lib.rs:192), then back to one dword per point
-  const uint32_t npw = sel4(np1, c);
-  uint32_t y[32];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const uint4 vv = vp[64 * q];
-    const uint32_t va[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int i = 4 * q + e;
-      y[i] = va[e] ^ s[i] ^ (T & (uint32_t)__builtin_amdgcn_sbfe((int)npw, i, 1));
-    }
-  }
-  transpose32(y);
-  uint32_t* y32 = reinterpret_cast<uint32_t*>(ys);
-#pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const uint64_t p = p0 + j;
-    if (p < m) y32[p * 4 + c] = y[j];
-  }
+  bs_finish(vp, sp, T, sel4(np1, c), m, p0, ys);
 }
 
 // Single key, nbytes % 4 == 0 and <= 16.  tt_mask: stream waves (bit w = wave w),
@@ -155,15 +95,17 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_shybrid(
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t total, uint32_t* __restrict__ ctr, uint4* __restrict__ ys, const PrefixTable pf,
-    const uint32_t tt_mask, const uint32_t prio, uint4* __restrict__ slabs, const uint4* __restrict__ km) {
+    const uint32_t tt_mask, const uint32_t prio, uint4* __restrict__ slabs, const uint4* __restrict__ km,
+    const uint4* __restrict__ rkg) {
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint32_t xl_all[kShybridXlSlots][32 * 16];
   lds_fill_tables(lds, tab);
   const uint32_t wave = threadIdx.x >> 6;
   if ((tt_mask >> wave) & 1u) {
     if (prio & 1u) __builtin_amdgcn_s_setprio(2);
-    stream_run<2, true, false, kWavePoints, false>(lds, nullptr, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, 1,
-                                                   total, total, ctr, ys, pf);
+    // round keys per round from the device copy, as the stream kernel (SGPR keys spill)
+    stream_run<2, true, false, kWavePoints, true>(lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, 1,
+                                                  total, total, ctr, ys, pf);
     return;
   }
   const uint32_t slot = (uint32_t)__popc(~tt_mask & ((1u << wave) - 1u) & 0xFFFFu);

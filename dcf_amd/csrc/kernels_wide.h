@@ -28,10 +28,14 @@
 
 namespace {
 
-// Per-point t-vector (head -> tail), 64 B: byte c holds rows 4c..4c+3 of the
-// t-sequence in bits 0..3 (bit k = t_{4c+k}), i.e. the four-Russians index of
-// chunk c, ready for v_perm address building in the tail.  n + 1 <= 256 rows, N <= 31.
+// Per-point t-vector (head -> tail), tw words (64 B for N <= 31): byte c holds rows 4c..4c+3
+// of the t-sequence in bits 0..3 (bit k = t_{4c+k}), i.e. the four-Russians index of chunk c,
+// ready for v_perm address building in the tail.  tw = t_words(nlev): 16 for n + 1 <= 256 rows,
+// else ceil((n + 1) / 16) rounded up to whole uint4.
 constexpr int kTWords = 16;
+__host__ __device__ constexpr uint32_t t_words(uint32_t nlev) {
+  return nlev + 1u <= 256u ? 16u : ((((nlev + 1u + 15u) / 16u) + 3u) & ~3u);
+}
 
 __device__ __forceinline__ void load_tab4(uint32_t* t4, const uint32_t* __restrict__ tab) {
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) t4[i] = tab[i];
@@ -71,7 +75,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head(
     const uint8_t* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint8_t* __restrict__ cw_np1,
     const uint8_t* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint32_t lam, const uint64_t num_keys, const uint64_t key, const uint64_t count, uint8_t* __restrict__ ys,
-    uint32_t* __restrict__ tvec) {
+    uint32_t* __restrict__ tvec, const uint32_t tw) {
   // Key `key` of a num_keys-key CWB: row l of cw_s / cw_v at (l * num_keys + key) * lam.
   __shared__ uint32_t lds[kLdsWords];
   lds_fill_tables(lds, tab);
@@ -92,7 +96,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head(
     }
     uint32_t t = party;
     uint32_t tacc = party, r = 1;  // t_r goes to bit (r & 3) of byte r >> 2
-    uint32_t* trow = tvec + gg * kTWords;
+    uint32_t* trow = tvec + gg * tw;
     const uint8_t* x = xs + gg * nbytes;
     uint32_t lev = 0;
     for (uint32_t c = 0; c < nchunk; ++c) {
@@ -179,17 +183,21 @@ __device__ __forceinline__ uint4 w_row_piece(const uint8_t* __restrict__ cw_s, c
 }
 
 
-__device__ __forceinline__ void tail_load_t(uint4 (&d)[4], const uint4* __restrict__ tv4, uint64_t pp, uint64_t p1) {
+// The point's first 16 t-vector words (64 chunks); tw4 = uint4 per t-vector row.
+__device__ __forceinline__ void tail_load_t(uint4 (&d)[4], const uint4* __restrict__ tv4, uint64_t pp, uint64_t p1,
+                                            uint32_t tw4) {
   pp = min<uint64_t>(pp, p1 - 1);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) d[k] = tv4[4 * pp + k];
+  for (int k = 0; k < 4; ++k) d[k] = tv4[tw4 * pp + k];
 }
 
 // One 16-byte piece of y for the point whose t-vector is t: cst ^ XOR over chunks c of
 // G[c][t nibble c] (four-Russians, see k_eval_wide_tail).
+// trow: the point's t-vector row, read directly for chunks past the first 64 (N >= 32).
 template <int TW, int LP, int NCH>
 __device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst, const char* gb, const uint4* G,
-                                            uint32_t q, uint32_t nch16_rt, uint32_t nrem_rt) {
+                                            uint32_t q, uint32_t nch16_rt, uint32_t nrem_rt,
+                                            const uint4* __restrict__ trow) {
   // NCH > 0: chunk count fixed at compile time (fully unrolled; N = 16 has 33 chunks)
   const uint32_t nch16 = NCH > 0 ? (uint32_t)NCH / 16u : nch16_rt;
   const uint32_t nrem = NCH > 0 ? (uint32_t)NCH % 16u : nrem_rt;
@@ -203,6 +211,10 @@ __device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst
   // BT reads are issued before their XORs (more LDS reads in flight per wave)
   constexpr uint32_t BT = 2;
   for (uint32_t g16 = 0; g16 < nch16; ++g16) {  // full groups of 16 chunks (4 t words)
+    if (NCH == 0 && g16 >= 4) {  // past the 16 queued words
+      const uint4 w = trow[g16];
+      tq[0] = w.x; tq[1] = w.y; tq[2] = w.z; tq[3] = w.w;
+    }
 #pragma unroll
     for (uint32_t j = 0; j < 16; j += BT) {
       uint4 b[BT];
@@ -231,6 +243,10 @@ __device__ __forceinline__ uint4 tail_piece(const uint4 (&t)[4], const uint4 cst
 #pragma unroll
     for (int k = 0; k < 12; ++k) tq[k] = tq[k + 4];  // word queue: no dynamic register indexing
     qb += 0x10000u;
+  }
+  if (NCH == 0 && nch16 >= 4 && nrem) {
+    const uint4 w = trow[nch16];
+    tq[0] = w.x; tq[1] = w.y; tq[2] = w.z; tq[3] = w.w;
   }
 #pragma unroll
   for (uint32_t cc = 0; cc < 15; ++cc) {  // remaining nch % 16 chunks
@@ -271,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
                                                             const uint32_t lam, const uint64_t num_keys,
                                                             const uint64_t key, const uint32_t* __restrict__ tvec,
                                                             const uint64_t count, const uint32_t pts_per_block,
-                                                            uint8_t* __restrict__ ys) {
+                                                            uint8_t* __restrict__ ys, const uint32_t tw) {
   constexpr int LP = TW / 16;
   extern __shared__ uint4 G[];
   if (TW == 256 && (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)G != 0u) __builtin_trap();
@@ -311,15 +327,16 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
   const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
   const uint32_t pstep = blockDim.x / LP;
   const uint32_t pin = (threadIdx.x & 63u) / LP;  // the lane's point among the wave's 64 / LP
-  // t-vectors (64 B per point) are loaded two points ahead into ping-pong registers,
+  // t-vectors (their first 64 B) are loaded two points ahead into ping-pong registers,
   // clamped instead of guarded, and the y store below is unconditional too: with no
   // branch around any vector-memory instruction the compiler counts vmcnt exactly and
   // waits for the t-vector loads only, never for an older non-temporal y store.
   const uint4* tv4 = reinterpret_cast<const uint4*>(tvec);
+  const uint32_t tw4 = tw / 4u;
   uint64_t p = p0 + threadIdx.x / LP;
   uint4 ta[4], tb[4];
-  tail_load_t(ta, tv4, p, p1);
-  tail_load_t(tb, tv4, p + pstep, p1);
+  tail_load_t(ta, tv4, p, p1, tw4);
+  tail_load_t(tb, tv4, p + pstep, p1, tw4);
   const char* gb = reinterpret_cast<const char*>(G);
   const uint32_t nch16 = nch >> 4, nrem = nch & 15u;
   // Buffer store: base = the wave's first point row, dead lanes get an offset past
@@ -328,15 +345,15 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
   for (;;) {
     if (p >= p1) break;
     {
-      const uint4 y = tail_piece<TW, LP, NCH>(ta, cst, gb, G, q, nch16, nrem);
-      tail_load_t(ta, tv4, p + 2 * pstep, p1);
+      const uint4 y = tail_piece<TW, LP, NCH>(ta, cst, gb, G, q, nch16, nrem, tv4 + tw4 * min<uint64_t>(p, p1 - 1));
+      tail_load_t(ta, tv4, p + 2 * pstep, p1, tw4);
       tail_store<LP>(ys, p - pin, pin, lam, off, lane_live ? 0u : dead, y);
     }
     p += pstep;
     if (p >= p1) break;
     {
-      const uint4 y = tail_piece<TW, LP, NCH>(tb, cst, gb, G, q, nch16, nrem);
-      tail_load_t(tb, tv4, p + 2 * pstep, p1);
+      const uint4 y = tail_piece<TW, LP, NCH>(tb, cst, gb, G, q, nch16, nrem, tv4 + tw4 * min<uint64_t>(p, p1 - 1));
+      tail_load_t(tb, tv4, p + 2 * pstep, p1, tw4);
       tail_store<LP>(ys, p - pin, pin, lam, off, lane_live ? 0u : dead, y);
     }
     p += pstep;
@@ -362,23 +379,54 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
 // the index of chunk k: chunks 0 .. 2 R6 - 1 are 6 rows each from row 0, then 5-row chunks.
 // Rows past n + 1 are zero.  Kept in place in the head's 64-byte t-vector rows (first 32 B).
 // ------------------------------------------------------------------------
-template <int R6, int R5>
+//
+// G8 > 0 (LDS + L2 split): the last G8 chunks are 8 bits wide and their tables (256 entries x 128 B
+// per chunk and tile, built once per call by k_tail_gtab) live in global memory, read through the
+// vector L1 / L2 (a tile's tables are 32 KiB per chunk: L2-resident, both ranges of a tile share an
+// XCD) instead of the LDS: the LDS is the tail's bound, so moving rows to the other read path
+// shortens it.
+template <int R6, int R5, int G8 = 0>
 struct Tail2Layout {
-  static constexpr int R = R6 + R5, NC = 2 * R;
+  static constexpr int R = R6 + R5, NL = 2 * R, NC = NL + G8;
   static_assert(NC <= 32, "t-vector holds 32 chunk bytes");
-  static constexpr uint32_t width(int k) { return k < 2 * R6 ? 6u : 5u; }
-  static constexpr uint32_t start(int k) { return k < 2 * R6 ? 6u * k : 12u * R6 + 5u * (k - 2 * R6); }
+  static constexpr uint32_t width(int k) { return k < 2 * R6 ? 6u : (k < NL ? 5u : 8u); }
+  static constexpr uint32_t start(int k) {
+    return k < 2 * R6 ? 6u * k : (k < NL ? 12u * R6 + 5u * (k - 2 * R6) : 12u * R6 + 10u * R5 + 8u * (k - NL));
+  }
   static constexpr uint32_t region(int m) { return m < R6 ? 16384u * m : 16384u * R6 + 8192u * (m - R6); }
-  static constexpr uint32_t rows() { return 12u * R6 + 10u * R5; }
-  static constexpr uint32_t lds_bytes() { return region(R); }
+  static constexpr uint32_t rows() { return 12u * R6 + 10u * R5 + 8u * G8; }
+  static constexpr uint32_t lds_bytes() { return region(R) + 16u; }  // + the workgroup's block counter
+  static constexpr uint32_t gtab_uint4_per_tile() { return G8 * 256u * 8u; }
 };
+
+// The global chunk tables of k_eval_wide_tail2<R6, R5, G8>: gtab[tile][g][entry][q] (uint4), entry e
+// of chunk NL + g = XOR of the W-row pieces of its set bits.  Grid (tiles, G8), 256 threads.
+template <int R6, int R5, int G8>
+__global__ void k_tail_gtab(const uint8_t* __restrict__ cw_s, const uint8_t* __restrict__ cw_v,
+                            const uint8_t* __restrict__ cw_np1, const uint32_t nlev, const uint32_t lam,
+                            const uint64_t num_keys, const uint64_t key, uint4* __restrict__ gtab) {
+  using L = Tail2Layout<R6, R5, G8>;
+  const uint32_t tile = blockIdx.x, g = blockIdx.y, st = L::start(L::NL + (int)g);
+  uint4* out = gtab + ((uint64_t)tile * G8 + g) * 2048u;
+  for (uint32_t it = threadIdx.x; it < 2048u; it += blockDim.x) {
+    const uint32_t e = it >> 3, q = it & 7u, off = tile * 128u + 16u * q;
+    uint4 acc = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b)
+      if ((e >> b) & 1u) {
+        const uint4 w = w_row_piece(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, st + b, off);
+        acc.x ^= w.x; acc.y ^= w.y; acc.z ^= w.z; acc.w ^= w.w;
+      }
+    out[it] = acc;
+  }
+}
 
 // Old nibble t-vector (row r at byte r >> 2, bit r & 3; words 0 .. nlev >> 4 valid) -> chunk
 // bytes of Tail2Layout<R6, R5>, in place (bytes [0, 32) of each 64-byte row).  One thread
 // per point: 36 of 64 bytes read, 32 written.
-template <int R6, int R5>
+template <int R6, int R5, int G8 = 0>
 __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, const uint64_t count) {
-  using L = Tail2Layout<R6, R5>;
+  using L = Tail2Layout<R6, R5, G8>;
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= count) return;
   uint32_t* row = tvec + p * kTWords;
@@ -412,7 +460,7 @@ __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, 
   o4[1] = make_uint4(out[4], out[5], out[6], out[7]);
 }
 
-template <int R6, int R5>
+template <int R6, int R5, int G8 = 0>
 __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __restrict__ cw_s,
                                                              const uint8_t* __restrict__ cw_v,
                                                              const uint8_t* __restrict__ cw_np1,
@@ -420,8 +468,8 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
                                                              const uint32_t lam, const uint64_t num_keys,
                                                              const uint64_t key, const uint32_t* __restrict__ tvec,
                                                              const uint64_t count, const uint32_t pts_per_block,
-                                                             uint8_t* __restrict__ ys) {
-  using L = Tail2Layout<R6, R5>;
+                                                             uint8_t* __restrict__ ys, const uint4* __restrict__ gtab) {
+  using L = Tail2Layout<R6, R5, G8>;
   constexpr int TW = 128, LP = 8;
   DCF_CLK(4, 0);  // (diagnostic builds) workgroup entry, before the table build
   extern __shared__ uint4 G[];
@@ -488,6 +536,9 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
       }
     }
   }
+  // the workgroup's block counter, past the tables
+  uint32_t* bctr = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(G) + L::region(L::R));
+  if (threadIdx.x == 0) *bctr = 0u;
   __syncthreads();
   DCF_CLK(0, 0);
   const uint32_t q = threadIdx.x % LP;
@@ -507,8 +558,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   const uint32_t rsel = pi ? 0x02030001u : 0x03020100u;
   const uint64_t p0 = (uint64_t)blockIdx.y * pts_per_block;
   const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
-  const uint32_t pstep = blockDim.x / LP;
-  const uint32_t pin = (threadIdx.x & 63u) / LP;
+  const uint32_t pin = (threadIdx.x & 63u) / LP;  // the lane's point among the wave's 8
   const uint4* tv4 = reinterpret_cast<const uint4*>(tvec);
   auto load_t = [&](uint4 (&d)[2], uint64_t pp) {
     pp = min<uint64_t>(pp, p1 - 1);
@@ -529,26 +579,50 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
     const uint32_t a = __builtin_amdgcn_perm(tw[c >> 2], (i ? lc1 : lc0) | grp, 0x0c020000u | ((4u + (c & 3)) << 8));
     return lds_load16(a + (rb & 0xFFFFu));  // the rest of the region base rides in the offset field
   };
-  // Two points per lane and iteration (A = p, B = p + pstep): their 2 x 24 reads are
-  // independent, so each wave keeps more LDS reads in flight.  The loop condition is
-  // wave-uniform (the wave's first point): no branch around a vector-memory instruction, so
-  // the compiler counts vmcnt exactly — the t-vectors, loaded at the end of an iteration, are
-  // waited on at the end of the next one (vmcnt(2): past the two y stores).  Past-the-end lanes load a clamped row and
-  // their stores are dropped (offset past num_records).
+  // Work: 16-point blocks of the workgroup's range, claimed per wave from the LDS counter (A = the
+  // block's first 8 points, B = the next 8; a lane owns one 16-byte piece of one point of each).
+  // The waves of a workgroup do not progress at one rate (VALU / LDS issue goes to the older
+  // wave first), so a static split left the younger waves working alone for the last third of
+  // the launch (in-kernel stamps: wave 0 done at 11 ms of a 17.5 ms kernel).  A block is claimed
+  // one iteration ahead so its t-vectors load behind the current block's work.  The loop
+  // condition is wave-uniform: no branch around a vector-memory instruction, so the compiler
+  // counts vmcnt exactly (the t-vectors, loaded at the end of an iteration, are waited on at the
+  // end of the next one, past the two y stores).  Past-the-end lanes load a clamped row and their
+  // stores are dropped (offset past num_records).
+  const uint32_t nblk = (uint32_t)((p1 - p0 + 15) / 16);
+  auto claim = [&]() -> uint32_t {
+    uint32_t b = 0u;
+    if ((threadIdx.x & 63u) == 0) b = __hip_atomic_fetch_add(bctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(b);
+  };
   const uint32_t dead = 0x80000000u;
   const uint32_t kill = lane_live ? 0u : dead;
-  uint64_t p = p0 + threadIdx.x / LP;
-  const uint64_t pw0 = p0 + (threadIdx.x / 64u) * (64u / LP);
   uint4 ta[2], tb[2];
   uint32_t twa[NW], twb[NW];
-  load_t(ta, p);
-  load_t(tb, p + pstep);
+  uint32_t bc = claim();
+  load_t(ta, p0 + 16u * bc + pin);
+  load_t(tb, p0 + 16u * bc + 8u + pin);
   rotate(ta, twa);
   rotate(tb, twb);
-  load_t(ta, p + 2 * pstep);
-  load_t(tb, p + 3 * pstep);
-  for (uint64_t pw = pw0; pw < p1; pw += 2 * pstep, p += 2 * pstep) {
+  uint32_t bn = claim();
+  load_t(ta, p0 + 16u * bn + pin);
+  load_t(tb, p0 + 16u * bn + 8u + pin);
+  // G8: this tile's global chunk tables; chunk NL + g's entry index is byte NL + g of the chunk
+  // vector (byte (NL + g) ^ pi of the pair-rotated words)
+  const uint4* __restrict__ gt = gtab + (uint64_t)blockIdx.x * L::gtab_uint4_per_tile() + q;
+  auto gentry = [&](const uint32_t (&tw)[NW], int g) {
+    const uint32_t k = (uint32_t)(L::NL + g) ^ pi;
+    return (tw[k >> 2] >> (8u * (k & 3u))) & 0xFFu;
+  };
+  while (bc < nblk) {
     uint32_t aa[4] = {cst.x, cst.y, cst.z, cst.w}, ab[4] = {cst.x, cst.y, cst.z, cst.w};
+    // the global entries first: their L2 round trip overlaps the LDS reads below
+    uint4 ga[G8 > 0 ? G8 : 1], gb[G8 > 0 ? G8 : 1];
+#pragma unroll
+    for (int g = 0; g < G8; ++g) {
+      ga[g] = gt[(uint32_t)g * 2048u + gentry(twa, g) * 8u];
+      gb[g] = gt[(uint32_t)g * 2048u + gentry(twb, g) * 8u];
+    }
     constexpr int BT = 2;
     // BT regions (4 reads each) are issued before their XORs: the compiler
     // otherwise waits after every two reads, ~3 reads in flight per wave
@@ -581,14 +655,21 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
           ab[2] = xor3(ab[2], b0.z, b1.z); ab[3] = xor3(ab[3], b0.w, b1.w);
         }
     }
-    tail_store<LP>(ys, p - pin, pin, lam, off, kill | (p < p1 ? 0u : dead), make_uint4(aa[0], aa[1], aa[2], aa[3]));
-    const uint64_t pb = p + pstep;
-    tail_store<LP>(ys, pb - pin, pin, lam, off, kill | (pb < p1 ? 0u : dead), make_uint4(ab[0], ab[1], ab[2], ab[3]));
-    // the next iteration's t-vectors (loaded one iteration ago, before these two stores)
+#pragma unroll
+    for (int g = 0; g < G8; ++g) {
+      aa[0] ^= ga[g].x; aa[1] ^= ga[g].y; aa[2] ^= ga[g].z; aa[3] ^= ga[g].w;
+      ab[0] ^= gb[g].x; ab[1] ^= gb[g].y; ab[2] ^= gb[g].z; ab[3] ^= gb[g].w;
+    }
+    const uint64_t pw = p0 + 16u * bc, pa = pw + pin, pb = pa + 8u;
+    tail_store<LP>(ys, pw, pin, lam, off, kill | (pa < p1 ? 0u : dead), make_uint4(aa[0], aa[1], aa[2], aa[3]));
+    tail_store<LP>(ys, pw + 8u, pin, lam, off, kill | (pb < p1 ? 0u : dead), make_uint4(ab[0], ab[1], ab[2], ab[3]));
+    // the next block's t-vectors (loaded one iteration ago, before these two stores)
+    bc = bn;
     rotate(ta, twa);
     rotate(tb, twb);
-    load_t(ta, p + 4 * pstep);
-    load_t(tb, p + 5 * pstep);
+    bn = claim();
+    load_t(ta, p0 + 16u * bn + pin);
+    load_t(tb, p0 + 16u * bn + 8u + pin);
   }
   DCF_CLK(0, 1);
 }

@@ -50,7 +50,7 @@ struct WideLane {
 template <int NS, bool XREG>
 __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, const uint8_t* __restrict__ s0p,
                                            uint32_t party, const uint8_t* __restrict__ xs, uint32_t nbytes,
-                                           const WidePrefix& pf, uint32_t* __restrict__ tvec) {
+                                           const WidePrefix& pf, uint32_t* __restrict__ tvec, uint32_t tw) {
   const uint4* s4 = reinterpret_cast<const uint4*>(s0p);  // k.s0s[0] (lib.rs:168), L2-resident
   const uint4 a = s4[0], b = s4[1];
   L.s[i][0] = a.x; L.s[i][1] = a.y; L.s[i][2] = a.z; L.s[i][3] = a.w;
@@ -92,7 +92,7 @@ __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, c
     L.v[i][4] = b1.x; L.v[i][5] = b1.y; L.v[i][6] = b1.z; L.v[i][7] = b1.w;
     L.t[i] = e.x;
     L.tacc[i] = e.z;  // rows 16 (D >> 4) .. D of the t-vector
-    if (D >= 15u) tvec[(uint64_t)p * kTWords] = e.y;  // rows 0..15, complete (row 15 = t_15 of depth 15)
+    if (D >= 15u) tvec[(uint64_t)p * tw] = e.y;  // rows 0..15, complete (row 15 = t_15 of depth 15)
     L.lev[i] = D;
     L.cur[i] <<= D;
   }
@@ -108,7 +108,7 @@ __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, u
                                             bool& exhausted, uint32_t* __restrict__ ctr, uint64_t nunits,
                                             uint64_t count, const uint8_t* __restrict__ s0p, uint32_t party,
                                             const uint8_t* __restrict__ xs, uint32_t nbytes, const WidePrefix& pf,
-                                            uint32_t* __restrict__ tvec) {
+                                            uint32_t* __restrict__ tvec, uint32_t tw) {
   uint64_t need = __ballot(mine);
   while (need) {
     if (unext >= uend && !exhausted) {
@@ -129,7 +129,7 @@ __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, u
     }
     const uint32_t rank = lane_rank(need);
     const bool take = mine && (uint64_t)rank < uend - unext;
-    if (take) wide_start<NS, XREG>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes, pf, tvec);
+    if (take) wide_start<NS, XREG>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes, pf, tvec, tw);
     const uint64_t taken = __ballot(take);
     unext += (uint64_t)__popcll(taken);
     need &= ~taken;
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     const uint8_t* __restrict__ dig_t, const uint8_t* __restrict__ cw_np1,
     const uint8_t* __restrict__ s0p, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint32_t lam, const uint64_t num_keys, const uint64_t key, const uint64_t count, uint32_t* __restrict__ ctr,
-    uint8_t* __restrict__ ys, uint32_t* __restrict__ tvec, const WidePrefix pf) {
+    uint8_t* __restrict__ ys, uint32_t* __restrict__ tvec, const WidePrefix pf, const uint32_t tw) {
   DCF_CLK(5, 0);  // (diagnostic builds) workgroup entry, before the table fill
   __shared__ uint32_t lds[kLdsWords];
   // Schedules of cipher 0 (slots 0..14) and cipher 17 (slots 23..37): 23 slots apart,
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
 #pragma unroll
   for (int i = 0; i < NS; ++i)
     wide_refill<NS, XREG>(L, i, true, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes, pf,
-                          tvec);
+                          tvec, tw);
 
   for (;;) {
     bool any = false;
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       // t-vector: row r = lev + 1 gets t_r (byte r >> 2, bit r & 3), as k_eval_wide_head writes it
       const uint32_t r = L.lev[i] + adv;
       L.tacc[i] |= (am & L.t[i]) << (8u * ((r >> 2) & 3u) + (r & 3u));
-      uint32_t* trow = tvec + (uint64_t)L.pt[i] * kTWords;
+      uint32_t* trow = tvec + (uint64_t)L.pt[i] * tw;
       const bool pdone = adv && r == nlev;
       if (adv && ((r & 15u) == 15u || pdone)) {
         trow[r >> 4] = L.tacc[i];
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       const bool done = L.alive[i] && L.lev[i] == nlev;
       if (__ballot(done))
         wide_refill<NS, XREG>(L, i, done, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes, pf,
-                              tvec);
+                              tvec, tw);
     }
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks), accumulated over passes

@@ -57,7 +57,9 @@ def test_bench_rccl_world1_line():
            "--no-compare", "--dist-backend", "nccl", "--force-dist", "--check"]
     out = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ), capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
-    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    # stdout is the one JSON line (RCCL's banner at communicator init goes to stderr)
+    assert len(out.stdout.strip().splitlines()) == 1, out.stdout[:2000]
+    d = json.loads(out.stdout)
     assert d["n_gpus"] == 1 and d["value"] > 0
     assert d["key_broadcast"]["backend"] == "nccl" and d["key_broadcast"]["bytes"] > 0
     assert d["slice_check"]["slices_match"]

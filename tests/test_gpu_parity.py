@@ -589,31 +589,46 @@ def test_gen_batch_large_counter_path(dcf, nb):
     assert np.array_equal(rec[lt], B[lt]) and not rec[~lt].any()
 
 
-def test_wide_largest_n_and_beyond(dcf):
-    """LAMBDA >= 32 at the largest supported input, N = 31 (248 levels: the head's t-vector holds
-    rows 0..248 of its 256, the 63-chunk 4-bit tail), both parties vs the oracle; N = 32 is refused
-    with DCF_ERR_UNSUPPORTED (-7) rather than evaluated wrong.  Gen has no such limit."""
-    lam, m = 128, 64
-    rng = np.random.default_rng(0x31)
+@pytest.mark.parametrize("nb,lam,m,mode", [(31, 128, 64, 0), (32, 128, 64, 0), (32, 128, 700, 0), (48, 128, 700, 0),
+                                             (48, 128, 300, 1), (64, 256, 600, 0), (100, 128, 200, 0),
+                                             (159, 128, 96, 0)])
+def test_wide_large_n_vs_oracle(dcf, nb, lam, m, mode):
+    """LAMBDA >= 32 at large inputs (the reference takes any N, lib.rs:163-165): the t-vector grows
+    past 64 B from N = 32 (8N + 1 > 256 rows), the 4-bit tail narrows its tiles to keep its tables
+    in the LDS (128-byte tiles to N = 39, 64 to N = 79, 32 to N = 159).  Stream head (mode 0; with
+    m >= 512 below a shared-prefix table) and lockstep head (mode 1), both parties vs the oracle,
+    alpha itself among the points."""
+    rng = np.random.default_rng(0x31 + nb + m)
     keys = [rng.bytes(32) for _ in range(18)]
     prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
-    for nb in (31, 32):
-        d = dcf.DcfImpl(nb, lam, prg)
-        alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
-        ok = O.gen(P, alpha, beta, s0, s1, 0)
-        k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
-        raw = ok.cw_s.tobytes() + ok.cw_v.tobytes() + ok.cw_t.tobytes()
-        assert dcf.share_to_cwb(k, nb, lam) == raw + bytes((-len(raw)) % 16) + ok.cw_np1.tobytes()
-        xs = _rand(rng, (m, nb))
-        xs[0] = np.frombuffer(alpha, np.uint8)
-        for b, s in ((0, s0), (1, s1)):
-            if nb == 31:
-                got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
-                assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), b
-            else:
-                with pytest.raises(dcf.DcfError) as e:
-                    d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
-                assert e.value.code == -7
+    prg.set_eval_mode(mode)
+    d = dcf.DcfImpl(nb, lam, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+    ok = O.gen(P, alpha, beta, s0, s1, 0)
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
+    raw = ok.cw_s.tobytes() + ok.cw_v.tobytes() + ok.cw_t.tobytes()
+    assert dcf.share_to_cwb(k, nb, lam) == raw + bytes((-len(raw)) % 16) + ok.cw_np1.tobytes()
+    xs = _rand(rng, (m, nb))
+    xs[0] = np.frombuffer(alpha, np.uint8)
+    xs[1] = xs[0]
+    xs[1, -1] ^= 1  # a neighbour of alpha: differs in the last level only
+    for b, s in ((0, s0), (1, s1)):
+        got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+        assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), b
+
+
+def test_wide_beyond_largest_n_refused(dcf):
+    """N = 160 at LAMBDA >= 32 is refused with DCF_ERR_UNSUPPORTED (-7) rather than evaluated wrong
+    (the 4-bit tail's tables of 32-byte tiles would exceed the LDS)."""
+    lam, nb = 128, 160
+    rng = np.random.default_rng(0x160)
+    keys = [rng.bytes(32) for _ in range(18)]
+    d = dcf.DcfImpl(nb, lam, dcf.Aes256HirosePrg(keys, lam))
+    s0, s1 = rng.bytes(lam), rng.bytes(lam)
+    k = d.gen(dcf.CmpFn(rng.bytes(nb), rng.bytes(lam)), [s0, s1], dcf.BoundState.LtBeta)
+    with pytest.raises(dcf.DcfError) as e:
+        d.eval(False, dcf.Share([s0], k.cws, k.cw_np1), _rand(rng, (8, nb)))
+    assert e.value.code == -7
 
 
 @pytest.mark.parametrize("nb,m", [(16, 3000), (4, 70_000), (16, 100_000), (2, 1000)])
