@@ -87,7 +87,7 @@ def engine_peak(engine: str) -> float:
 def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels: int = 0):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json: one entry per profiled launch shape, written by
-    scripts/prof_summary.py from scripts/gpu_profile.sh: 2 x FETCH_SIZE + WRITE_SIZE,
+    scripts/prof_summary.py from scripts/leases/gpu_profile.sh: 2 x FETCH_SIZE + WRITE_SIZE,
     MI355X_MICROARCH.md §HBM), only when a profile ran this exact launch shape; else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:

@@ -33,7 +33,7 @@ EXPORTS = [
     "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device", "dcf_eval_full_domain_device",
     "dcf_share_bincode_bytes", "dcf_share_to_bincode", "dcf_share_from_bincode",
     "dcf_point_slice", "dcf_eval_multi_gpu", "dcf_eval_multi_gpu_device", "dcf_prg_set_prefix_max_bytes",
-    "dcf_prg_device_bytes", "dcf_prg_host_pinned_bytes", "dcf_prg_workspaces", "dcf_prg_set_phase_timing",
+    "dcf_prg_device_bytes", "dcf_prg_host_pinned_bytes", "dcf_prg_workspaces", "dcf_prg_trim", "dcf_prg_set_phase_timing",
     "dcf_prg_last_eval_phases",
 ]
 
@@ -95,6 +95,7 @@ def load(path: str = LIB_PATH):
         "dcf_prg_device_bytes": ([vp], sz),
         "dcf_prg_host_pinned_bytes": ([vp], sz),
         "dcf_prg_workspaces": ([vp], i),
+        "dcf_prg_trim": ([vp], i),
         "dcf_prg_set_phase_timing": ([vp, i], i),
         "dcf_prg_last_eval_phases": ([vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                       ctypes.POINTER(i)], i),

@@ -375,7 +375,7 @@ __device__ __forceinline__ void aes128_tt(uint32_t (&st)[NB][4], const uint4* co
 // the ratio of the deltas x 100 MHz.  The stamps go to a buffer of their own by plain vector
 // stores (dcf_debug_clock_stamps reads them back); no output is computed from them.
 #ifdef DCF_CLOCK_STAMPS
-constexpr uint32_t kClkSlots = 6, kClkGroups = 4096;
+constexpr uint32_t kClkSlots = 8, kClkGroups = 4096;
 __device__ unsigned long long g_clk_stamps[kClkSlots * kClkGroups * 4];
 __device__ __forceinline__ void clk_stamp(uint32_t slot, uint32_t phase) {
   const uint32_t wg = blockIdx.x + gridDim.x * blockIdx.y;

@@ -928,12 +928,22 @@ int dcf_prg_workspaces(const dcf_prg* p) {
   return (int)p->all_ws.size();
 }
 
+// The measurement hooks read the last eval's workspace only while no call holds it: under the
+// pool lock (a lease takes that lock to pop the workspace), after the workspace's last device
+// work has finished.
+static bool ws_idle(const dcf_prg* p, const Workspace* w) {
+  return std::find(p->free_ws.begin(), p->free_ws.end(), w) != p->free_ws.end();
+}
+
 int dcf_prg_last_eval_blocks(dcf_prg* p, uint64_t* blocks) {
   if (!p || !blocks) return fail(DCF_ERR_ARG, "null argument");
   *blocks = 0;
+  std::lock_guard<std::mutex> g(p->pool_mu);
   Workspace* w = p->last_ws.load();
   if (!w || !w->d_ctr) return DCF_OK;
+  if (!ws_idle(p, w)) return fail(DCF_ERR_ARG, "the last eval's workspace is in use by another call");
   DeviceGuard dg(p->device);
+  if (w->pending) HIP_TRY(hipEventSynchronize(w->done));
   HIP_TRY(hipMemcpy(blocks, w->d_ctr + 2, sizeof(uint64_t), hipMemcpyDeviceToHost));
   return DCF_OK;
 }
@@ -949,13 +959,30 @@ int dcf_prg_last_eval_phases(dcf_prg* p, float* prep_ms, float* walk_ms, int* pr
   if (!p || !prep_ms || !walk_ms) return fail(DCF_ERR_ARG, "null argument");
   *prep_ms = *walk_ms = 0.f;
   if (prefix_levels) *prefix_levels = 0;
+  std::lock_guard<std::mutex> g(p->pool_mu);
   Workspace* w = p->last_ws.load();
   if (!w || !w->timed) return fail(DCF_ERR_ARG, "no timed eval yet (dcf_prg_set_phase_timing)");
+  if (!ws_idle(p, w)) return fail(DCF_ERR_ARG, "the last eval's workspace is in use by another call");
   DeviceGuard dg(p->device);
   HIP_TRY(hipEventElapsedTime(prep_ms, w->tev[0], w->tev[1]));
   HIP_TRY(hipEventElapsedTime(walk_ms, w->tev[1], w->tev[2]));
   if (prefix_levels) *prefix_levels = (int)w->last_prefix;
   return DCF_OK;
+}
+
+int dcf_prg_trim(dcf_prg* p) {
+  if (!p) return fail(DCF_ERR_ARG, "null prg");
+  std::vector<Workspace*> idle;
+  {
+    std::lock_guard<std::mutex> g(p->pool_mu);
+    idle.swap(p->free_ws);
+    for (Workspace* w : idle) p->all_ws.erase(std::find(p->all_ws.begin(), p->all_ws.end(), w));
+    Workspace* last = p->last_ws.load();
+    if (std::find(idle.begin(), idle.end(), last) != idle.end()) p->last_ws.store(nullptr);
+  }
+  DeviceGuard dg(p->device);
+  for (Workspace* w : idle) free_workspace(w);  // waits for each one's last device work
+  return (int)idle.size();
 }
 
 int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priority) {
@@ -1277,8 +1304,14 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     const uint8_t* sct = cwt;
     if (multi) {  // key-major digest of the K keys (kernels_stream.h)
       if (int rc = grow(&w->d_kdig, &w->kdig_bytes, (size_t)num_keys * n * 33, st)) return rc;
+#if defined(DCF_C5V) && (DCF_C5V & 1)
+      hipLaunchKernelGGL(k_cw_keymajor_tiled, dim3((unsigned)((num_keys + kKmKeys - 1) / kKmKeys), (n + kKmLevs - 1) / kKmLevs),
+                         dim3(256), 0, st, cws, cwv, cwt, (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig,
+                         w->d_kdig + (size_t)num_keys * n * 32);
+#else
       hipLaunchKernelGGL(k_cw_keymajor, dim3((unsigned)((num_keys + 15) / 16)), dim3(256), 0, st, cws, cwv, cwt,
                          (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig, w->d_kdig + (size_t)num_keys * n * 32);
+#endif
       HIP_TRY(hipGetLastError());
       scs = (const uint4*)w->d_kdig;
       sct = w->d_kdig + (size_t)num_keys * n * 32;
@@ -1301,10 +1334,16 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
         }
       }
       if (w->pfx_bytes >= need) {
+#if defined(DCF_C5V) && (DCF_C5V & 2)
+        hipLaunchKernelGGL(k_mk_prefix_dfs16, dim3((unsigned)((num_keys + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                           p->d_tab, cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party, (uint64_t)num_keys,
+                           (uint4*)w->d_pfx, p->d_rk0, w->d_ctr);
+#else
         hipLaunchKernelGGL(k_mk_prefix16<true>,
                            dim3((unsigned)(((num_keys << kMkPfxRoot) + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            st, p->d_tab, p->rk[0], cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party,
                            (uint64_t)num_keys, (uint4*)w->d_pfx, p->d_rk0, w->d_ctr);
+#endif
         HIP_TRY(hipGetLastError());
         pf = PrefixTable{(const uint4*)w->d_pfx, kMkPfxLevels};
         w->last_prefix = kMkPfxLevels;

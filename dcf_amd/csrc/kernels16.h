@@ -599,6 +599,83 @@ __global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
   }
 }
 
+// Multi-key top trees, one thread per key: the key's whole kMkPfxLevels-level tree depth-first
+// (2^L - 1 PRG calls, 62 blocks at L = 5; k_mk_prefix16 walks the root levels once per thread,
+// 72), the right child of every expansion above the bottom waiting on a register stack (one
+// 9-word slot per depth, as k_prefix_build16's tail).  Leaf-parent i (bits Msb-first = the
+// choices at depths 0 .. L-2) resumes from the slot at the depth of i's lowest set bit and writes
+// rows 2i, 2i + 1 of the key's 2^L.  CWs per expansion are per-lane loads (lanes = consecutive
+// keys: one contiguous KiB per level and field).
+__global__ __launch_bounds__(kBlock, 1) void k_mk_prefix_dfs16(
+    const uint32_t* __restrict__ tab, const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
+    const uint8_t* __restrict__ cw_t, const uint4* __restrict__ s0s, const uint32_t party, const uint64_t num_keys,
+    uint4* __restrict__ table, const uint4* __restrict__ rkg, uint32_t* __restrict__ ctr) {
+  constexpr uint32_t H = kMkPfxLevels;
+  __shared__ uint32_t lds[kLdsWords];
+  lds_fill_tables(lds, tab);
+  const uint32_t lc = lane_const();
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t live = __ballot(k < num_keys);
+  if ((threadIdx.x & 63u) == 0 && live)
+    atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1,
+              2ull * ((1u << H) - 1u) * (unsigned long long)__popcll(live));
+  if (k >= num_keys) return;  // after the only barrier (lds_fill_tables)
+  const RoundKeys rk{};       // unused: round keys per round from rkg
+  uint32_t stk[H - 1][9];     // pending right children: s[4] | v[4] | t, by depth
+  uint32_t n[9];
+  {
+    const uint4 sv = s0s[k];
+    n[0] = sv.x; n[1] = sv.y; n[2] = sv.z; n[3] = sv.w;
+    n[4] = n[5] = n[6] = n[7] = 0u;
+    n[8] = party;
+  }
+  uint4* rows = table + 2ull * (k << H);
+  for (uint32_t i = 0; i < (1u << (H - 1u)); ++i) {
+    uint32_t d = 0;
+    if (i) {  // resume at the right child saved at depth H - 2 - ctz(i) (wave-uniform)
+      const uint32_t r = H - 2u - (uint32_t)__builtin_ctz(i);
+#pragma unroll
+      for (uint32_t q = 0; q + 1 < H; ++q)
+        if (q == r)
+#pragma unroll
+          for (int e = 0; e < 9; ++e) n[e] = stk[q][e];
+      d = r + 1u;
+    }
+    for (;; ++d) {  // expand depth d (level d of the key's tree)
+      const uint4 cs = cw_s[(uint64_t)d * num_keys + k], cv = cw_v[(uint64_t)d * num_keys + k];
+      const uint32_t ct = cw_t[(uint64_t)d * num_keys + k];
+      const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+      const uint32_t s[4] = {n[0], n[1], n[2], n[3]}, v[4] = {n[4], n[5], n[6], n[7]};
+      uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
+      fd_children<true>(lds, lc, rk, csw, cvw, ct, s, v, n[8], sl, vl, tl, sr, vr, tr, rkg);
+      if (d + 1u == H) {  // bottom: rows 2i, 2i + 1
+        uint4* row = rows + 4u * i;
+        row[0] = make_uint4(sl[0], sl[1], sl[2], (sl[3] & kMaskLast) | ((tl & 1u) << 24));
+        row[1] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+        row[2] = make_uint4(sr[0], sr[1], sr[2], (sr[3] & kMaskLast) | ((tr & 1u) << 24));
+        row[3] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
+        break;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q + 1 < H; ++q)
+        if (q == d) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            stk[q][e] = sr[e];
+            stk[q][4 + e] = vr[e];
+          }
+          stk[q][8] = tr;
+        }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        n[e] = sl[e];
+        n[4 + e] = vl[e];
+      }
+      n[8] = tl;
+    }
+  }
+}
+
 // Shared-prefix table (PrefixTable rows) of depth D in ONE launch, Hirose PRG.
 // The level-by-level build (k_fd_level16, one launch per level) spends most of its time
 // on the narrow upper levels (C2: 23 launches, ~1 ms of a 5 ms step).  Here workgroup w
@@ -623,6 +700,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
   __shared__ uint4 root_s, root_v;
   __shared__ uint32_t root_t;
   lds_fill_tables(lds, tab);
+  DCF_CLK(6, 0);  // (diagnostic builds) after the table fill; (6, 1) after the breadth-first levels
   const uint32_t lc = lane_const();
   const uint32_t w = blockIdx.x;
   uint8_t* X = buf_a + (uint64_t)w * region_bytes;
@@ -651,6 +729,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     }
   }
   __syncthreads();
+  DCF_CLK(7, 0);  // (diagnostic builds) root path done; (7, 1) thread 0's depth-first tail done
   for (uint32_t lev = S; lev < D - H; ++lev) {
     const uint32_t np = 1u << (lev - S);  // this workgroup's parents at level lev
     const bool last = lev + 1u == D;
@@ -704,6 +783,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     X = Y;
     Y = tmp;
   }
+  DCF_CLK(6, 1);
   if (H == 0) return;
   // Depth-first tail: thread j expands node j (j + blockDim, ...) of level B = D - H H
   // levels down in registers — the right child of every expansion above the bottom waits
@@ -769,6 +849,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
       }
     }
   }
+  DCF_CLK(7, 1);
 }
 
 // Last H levels of the full-domain expansion depth-first (as k_prefix_build16's tail): one

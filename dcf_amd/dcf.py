@@ -223,6 +223,14 @@ class Aes256HirosePrg:
         """Workspaces in the prg's pool (the most calls that were in flight at once)."""
         return int(_lib.load().dcf_prg_workspaces(self._h))
 
+    def trim(self) -> int:
+        """Free the workspaces no call holds (device scratch, prefix tables, pinned staging);
+        returns how many were freed."""
+        n = int(_lib.load().dcf_prg_trim(self._h))
+        if n < 0:
+            check(n)
+        return n
+
     def set_phase_timing(self, on: bool) -> None:
         """Record HIP events around every eval's preparation and walk (measurement hook)."""
         check(_lib.load().dcf_prg_set_phase_timing(self._h, int(bool(on))))

@@ -156,15 +156,20 @@ int dcf_prg_set_prefix_max_bytes(dcf_prg* prg, size_t max_bytes);
  * all of its workspaces). */
 size_t dcf_prg_device_bytes(const dcf_prg* prg);
 /* Pinned host memory this dcf_prg holds for the host-pointer entry points (per workspace: up
- * to two 128 MiB x + y chunks of the eval pipeline, sized to the largest call, plus a 1 MiB
- * mapped buffer for tiny calls), kept until dcf_prg_free. */
+ * to two 128 MiB x + y chunks of the eval pipeline, sized to the largest call, a 1 MiB mapped
+ * buffer for tiny calls and a mapped buffer of up to 64 MiB for mid-size evals: ~321 MiB per
+ * workspace at most, one workspace per call in flight), kept until dcf_prg_trim / dcf_prg_free. */
 size_t dcf_prg_host_pinned_bytes(const dcf_prg* prg);
 /* Number of workspaces in the prg's pool (the most calls that were in flight at once). */
 int dcf_prg_workspaces(const dcf_prg* prg);
+/* Free every workspace no call holds right now (their device scratch, prefix tables, pinned
+ * staging); calls in flight keep theirs.  The next call allocates afresh.  Returns the number
+ * of workspaces freed. */
+int dcf_prg_trim(dcf_prg* prg);
 
 /* Hybrid engine tuning (results are identical for every setting):
- *   slab_variant 1: 16-wave workgroups, bitsliced s/v state in a scratch slab;
- *   slab_variant 0: 12-wave workgroups, bitsliced state in registers;
+ *   slab_variant 1: 16-wave workgroups; slab_variant 0: 12-wave workgroups (the bitsliced
+ *                  waves keep their s / v state in per-wave scratch slabs either way);
  *   ttable_waves:  waves per workgroup running the T-table engine (the rest
  *                  run the bitsliced engine; clamped to [1, 16] / [0, 12]). */
 int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves, int slab_variant);
@@ -173,7 +178,9 @@ int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves, int slab_variant);
  *   ttable_wave_mask: bit w set = wave w of the 16-wave workgroup runs the stream
  *                     T-table engine, clear = the bitsliced engine; waves w and
  *                     w + 4 share a SIMD (at least 4 bits set);
- *   priority:         1 = stream waves issue at raised priority (s_setprio). */
+ *   priority:         1 = stream waves issue at raised priority (s_setprio).
+ * A DCF_EVAL_STREAM_HYBRID eval takes fewer than 2^31 points per call (DCF_ERR_UNSUPPORTED
+ * otherwise; the default stream engine splits larger batches into launches itself). */
 int dcf_prg_set_stream_hybrid(dcf_prg* prg, unsigned ttable_wave_mask, int priority);
 
 /* AES blocks the last eval call on this prg (the last one to return, from any thread)
@@ -182,7 +189,8 @@ int dcf_prg_set_stream_hybrid(dcf_prg* prg, unsigned ttable_wave_mask, int prior
  * shared-prefix table build, except the multi-key per-key top trees, whose blocks are
  * included), counted on the device; 0 for engines that do not count.
  * Measurement hook for the bench; call after the eval's stream has been synchronized.  0
- * before any eval. */
+ * before any eval; DCF_ERR_ARG while that call's workspace is leased by another call (the
+ * hook never reads a workspace in use). */
 int dcf_prg_last_eval_blocks(dcf_prg* prg, uint64_t* blocks);
 
 /* Phase timing of eval calls (measurement hook, off by default).  When on, every eval call
@@ -190,7 +198,8 @@ int dcf_prg_last_eval_blocks(dcf_prg* prg, uint64_t* blocks);
  * prefix table, per-key top trees or CW digest/rows were built) and at the end.
  * dcf_prg_last_eval_phases reads the last eval call's split (call after synchronizing its
  * stream): prep_ms = table / digest preparation, walk_ms = the walk kernels, prefix_levels =
- * the shared-prefix depth it used (0 = none).  DCF_ERR_ARG if no timed eval has run. */
+ * the shared-prefix depth it used (0 = none).  DCF_ERR_ARG if no timed eval has run, or while
+ * that call's workspace is leased by another call. */
 int dcf_prg_set_phase_timing(dcf_prg* prg, int on);
 int dcf_prg_last_eval_phases(dcf_prg* prg, float* prep_ms, float* walk_ms, int* prefix_levels);
 

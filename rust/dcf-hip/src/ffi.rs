@@ -35,6 +35,7 @@ extern "C" {
     pub fn dcf_prg_device_bytes(prg: *const DcfPrg) -> usize;
     pub fn dcf_prg_host_pinned_bytes(prg: *const DcfPrg) -> usize;
     pub fn dcf_prg_workspaces(prg: *const DcfPrg) -> c_int;
+    pub fn dcf_prg_trim(prg: *mut DcfPrg) -> c_int;
     pub fn dcf_prg_set_hybrid_split(prg: *mut DcfPrg, ttable_waves: c_int, slab_variant: c_int) -> c_int;
     pub fn dcf_prg_set_stream_hybrid(prg: *mut DcfPrg, ttable_wave_mask: c_uint, priority: c_int) -> c_int;
     pub fn dcf_prg_last_eval_blocks(prg: *mut DcfPrg, blocks: *mut u64) -> c_int;

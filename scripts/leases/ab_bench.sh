@@ -1,5 +1,5 @@
 # A/B kernel variants: bench.py against each in-tree library build given (default build first).
-# Usage (GPU box): bash scripts/ab_bench.sh <tag> "<lib paths>" [bench args...]
+# Usage (GPU box): bash scripts/leases/ab_bench.sh <tag> "<lib paths>" [bench args...]
 set -o pipefail
 TAG=$1; LIBS=$2; shift 2
 OUT=gpurun_out/$TAG

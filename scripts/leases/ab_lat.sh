@@ -1,4 +1,4 @@
-# A/B of the single-call latency workload (benches/dcf.rs) and C1: bash scripts/ab_lat.sh <tag> _v...
+# A/B of the single-call latency workload (benches/dcf.rs) and C1: bash scripts/leases/ab_lat.sh <tag> _v...
 T=$1; shift; mkdir -p gpurun_out/$T
 for rep in 1 2; do for v in "" "$@"; do
   DCF_HIP_LIB=$PWD/dcf_amd/libdcf_hip$v.so timeout -k 10 300 python bench.py --workload lat > gpurun_out/$T/lat$v.json 2>/dev/null || exit 1

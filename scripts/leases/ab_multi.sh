@@ -1,5 +1,5 @@
 # A/B of kernel variants over several workloads: default lib vs libdcf_hip_<v>.so for each v.
-# Usage (GPU box): WL="c3 c2 c5" REPS=2 bash scripts/ab_multi.sh <tag> <v>...
+# Usage (GPU box): WL="c3 c2 c5" REPS=2 bash scripts/leases/ab_multi.sh <tag> <v>...
 set -o pipefail
 T=$1; shift; mkdir -p gpurun_out/$T
 for rep in $(seq ${REPS:-2}); do for w in ${WL:-c3 c2}; do for v in "" "$@"; do

@@ -1,5 +1,5 @@
 # Kernel-trace A/B of library builds: rocprofv3 --kernel-trace --stats of bench.py per build.
-# Usage (GPU box): bash scripts/ab_prof.sh <tag> "<lib paths>" [bench args...]
+# Usage (GPU box): bash scripts/leases/ab_prof.sh <tag> "<lib paths>" [bench args...]
 # Summaries: python scripts/prof_summary.py gpurun_out/<tag>/<i> (one directory per build, 0 = default).
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,4 +1,4 @@
-# C1 (100k points, both parties): engine / prefix-depth sweep.  bash scripts/c1_sweep.sh
+# C1 (100k points, both parties): engine / prefix-depth sweep.  bash scripts/leases/c1_sweep.sh
 set -o pipefail
 O=gpurun_out/c1
 mkdir -p $O

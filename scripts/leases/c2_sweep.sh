@@ -1,4 +1,4 @@
-# C2 (N = 4, 2^24 points): shared-prefix depth sweep.  bash scripts/c2_sweep.sh
+# C2 (N = 4, 2^24 points): shared-prefix depth sweep.  bash scripts/leases/c2_sweep.sh
 set -o pipefail
 O=gpurun_out/c2s
 mkdir -p $O

@@ -1,4 +1,4 @@
-# bash scripts/depth_sweep.sh <tag> <workload> <depths...>: bench at forced shared-prefix depths
+# bash scripts/leases/depth_sweep.sh <tag> <workload> <depths...>: bench at forced shared-prefix depths
 T=$1; W=$2; shift 2
 mkdir -p gpurun_out/$T
 for d in "$@"; do

@@ -1,5 +1,5 @@
 # C3 bench line + rocprofv3 kernel trace of the same workload in one lease.
-#   bash scripts/gpu_c3_lease.sh <tag>
+#   bash scripts/leases/gpu_c3_lease.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/$1; mkdir -p $O

@@ -1,5 +1,5 @@
 # GPU parity + rocprofv3 kernel stats + HBM PMC passes for the default bench workload.
-# Usage (from repo root, on the GPU box): bash scripts/gpu_profile.sh [tag]
+# Usage (from repo root, on the GPU box): bash scripts/leases/gpu_profile.sh [tag]
 set -o pipefail
 TAG=${1:-r01}
 export TMPDIR=/tmp

@@ -1,5 +1,5 @@
 # rocprofv3 kernel trace + PMC passes for one bench workload (run on the GPU box).
-#   bash scripts/gpu_profile_w.sh <tag> <workload> [extra bench args...]
+#   bash scripts/leases/gpu_profile_w.sh <tag> <workload> [extra bench args...]
 # Writes gpurun_out/<tag>/{trace,pmc_fetch,pmc_write,pmc_sq}_<workload>/ (one pass each,
 # MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE in separate passes).
 set -o pipefail

@@ -17,4 +17,4 @@ timeout -k 10 400 python bench.py --workload c5 --steps 3 --warmup 1 > $O/bench_
 python -c "import json; d=json.load(open('$O/bench_c5.json')); r=d['roofline']; print('c5', round(d['value']/1e6,1), round(r['frac'],3), r['eval_only'], d['phases_ms'])"
 DCF_HIP_LIB=$PWD/dcf_amd/libdcf_hip_clk.so timeout -k 10 400 python scripts/clock_probe.py > $O/clock_probe.json 2> $O/clock_probe.err || { tail -20 $O/clock_probe.err; exit 1; }
 python -c "import json; d=json.load(open('$O/clock_probe.json')); print({k: d[k] for k in ('c4_ms_per_step','c4','c3_ms_per_step','c3')}); print(d['amd_smi_c4']); print(d['amd_smi_c3'])"
-bash scripts/gpu_c3_lease.sh r03b_c3
+bash scripts/leases/gpu_c3_lease.sh r03b_c3

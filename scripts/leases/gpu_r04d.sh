@@ -12,3 +12,6 @@ for rep in 1 2; do for v in default t3g3 t3g4 t3g5; do
   DCF_HIP_LIB=$L timeout -k 10 300 python bench.py --workload c4 --steps 10 --warmup 3 --no-cpu --no-compare > $O/c4_${v}_$rep.json 2>/dev/null || exit 1
   python -c "import json; d=json.load(open('$O/c4_${v}_$rep.json')); r=d['roofline']; print('c4 $v', round(d['value']/1e6,2), round(d['ms_per_step'],3), round(r['frac'],4))"
 done; done
+# C2 in-kernel timeline (prefix-table build phases vs the walk), clock-stamp build
+DCF_HIP_LIB=$PWD/dcf_amd/libdcf_hip_clk.so timeout -k 10 300 python scripts/c2_timeline.py > $O/c2_timeline.json 2> $O/c2_timeline.err || { tail -30 $O/c2_timeline.err; exit 1; }
+cat $O/c2_timeline.json

@@ -1,4 +1,4 @@
-# GPU tests + default bench + extra workloads.  bash scripts/gpu_round.sh <tag> [workloads...]
+# GPU tests + default bench + extra workloads.  bash scripts/leases/gpu_round.sh <tag> [workloads...]
 # Each bench line is kept as gpurun_out/<tag>/bench_<w>.json.  NO_TESTS=1 skips pytest.
 set -o pipefail
 TAG=$1; shift

@@ -1,5 +1,5 @@
 # PMC set a (LDS/VALU/clock counters) for the default library and each A/B library given.
-# Usage (GPU box): bash scripts/pmc_ab.sh <tag> "<lib paths>" [points]
+# Usage (GPU box): bash scripts/leases/pmc_ab.sh <tag> "<lib paths>" [points]
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; LIBS=$2; PTS=${3:-67108864}

@@ -1,6 +1,6 @@
 # C5 HBM traffic per step (2 x FETCH_SIZE + WRITE_SIZE over gen, both parties' top trees,
 # digests and evals; separate --pmc passes), recorded into profiles/pmc_traffic.json, then
-# the C5 bench line with it.   bash scripts/pmc_c5.sh <tag>
+# the C5 bench line with it.   bash scripts/leases/pmc_c5.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/$1; mkdir -p $O

@@ -1,6 +1,6 @@
 # Effective engine clock per kernel: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / kernel time,
 # both from one rocprofv3 run (--kernel-trace with one GRBM counter).
-#   bash scripts/pmc_clock.sh <tag> [workload:steps ...]   -> gpurun_out/<tag>/clock.md
+#   bash scripts/leases/pmc_clock.sh <tag> [workload:steps ...]   -> gpurun_out/<tag>/clock.md
 set -o pipefail
 export TMPDIR=/tmp
 T=$1; shift

@@ -1,5 +1,5 @@
 # PMC comparison of eval engines (LDS/VALU/clock counters), one rocprofv3 pass per engine and counter set.
-# Usage (GPU box): bash scripts/pmc_engines.sh <tag> "<modes>" [points] [set]
+# Usage (GPU box): bash scripts/leases/pmc_engines.sh <tag> "<modes>" [points] [set]
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-pmc}; MODES=${2:-"1 4"}; PTS=${3:-67108864}; SET=${4:-a}

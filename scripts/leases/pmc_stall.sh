@@ -1,5 +1,5 @@
 # Wave-state PMC pass (where the waves' cycles go) for the given workloads, one rocprofv3 pass each.
-# Usage (GPU box): bash scripts/pmc_stall.sh <tag> "<workload[:points]>..."
+# Usage (GPU box): bash scripts/leases/pmc_stall.sh <tag> "<workload[:points]>..."
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; WS=$2

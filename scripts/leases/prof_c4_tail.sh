@@ -1,5 +1,5 @@
 # Kernel trace + LDS/VALU PMC of C4 for the default lib and variants:
-#   bash scripts/prof_c4_tail.sh <tag> [variant...]   (variant v = dcf_amd/libdcf_hip_<v>.so)
+#   bash scripts/leases/prof_c4_tail.sh <tag> [variant...]   (variant v = dcf_amd/libdcf_hip_<v>.so)
 set -o pipefail
 export TMPDIR=/tmp
 T=$1; shift

@@ -233,6 +233,31 @@ def test_eval_device_large_sample_and_reconstruction(dcf, nb, m, mode):
     assert not rec[~lt].any()
 
 
+@pytest.mark.parametrize("nb,K,P", [(1, 70, 64), (3, 130, 40), (5, 65, 33), (16, 200, 32)])
+def test_multikey_stream_widths_vs_oracle(dcf, nb, K, P):
+    """Multi-key stream eval (per-key top trees, key-major CW digest) at 8N levels that are not a
+    multiple of the digest's 16-level tiles and key counts that are not a multiple of 64."""
+    import torch
+    rng = np.random.default_rng(nb * 7919 + K)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, Po = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    prg.set_eval_mode(4)
+    d = dcf.DcfImpl(nb, 16, prg)
+    alpha, beta, s0, s1 = (_rand(rng, (K, nb)), _rand(rng, (K, 16)), _rand(rng, (K, 16)), _rand(rng, (K, 16)))
+    T = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    cwb = d.gen_batch_device(T(alpha), T(beta), T(s0), T(s1), dcf.BoundState(0))
+    xs = _rand(rng, (K * P, nb))
+    y0 = d.eval_multikey_device(False, cwb, T(s0), T(xs), P)
+    y1 = d.eval_multikey_device(True, cwb, T(s1), T(xs), P)
+    torch.cuda.synchronize()
+    y0h, y1h = y0.cpu().numpy(), y1.cpu().numpy()
+    for key in sorted(set([0, K - 1] + list(rng.integers(0, K, 5)))):
+        ok = O.gen(Po, alpha[key].tobytes(), beta[key].tobytes(), s0[key].tobytes(), s1[key].tobytes(), 0)
+        sl = slice(key * P, (key + 1) * P)
+        assert np.array_equal(y0h[sl], O.eval_(Po, 0, ok, s0[key].tobytes(), xs[sl]))
+        assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl]))
+
+
 @pytest.mark.parametrize("mode", [0, 1, 4])
 @pytest.mark.parametrize("K,P", [(1, 100), (37, 64), (10, 13), (300, 128)])
 def test_gen_batch_and_multikey_eval_vs_oracle(dcf, K, P, mode):

@@ -141,6 +141,14 @@ def test_one_prg_many_threads(dcf):
             assert np.array_equal(o, outs[0]), i
         if dev is not None:
             assert np.array_equal(dev, outs[0]), i
+    # every workspace is idle now: trim frees them all, and the prg keeps working
+    n = prg.workspaces()
+    pinned = prg.host_pinned_bytes()
+    assert pinned > 0 and prg.trim() == n and prg.workspaces() == 0 and prg.host_pinned_bytes() == 0
+    nb, alpha, beta, s0, s1, xs, outs, dev = _job(dcf, prg, 3, False)
+    ok = O.gen(P, alpha, beta, s0, s1, 1)
+    assert np.array_equal(outs[0][:64], O.eval_(P, 1, ok, s1, xs[:64], nthreads=CPU_THREADS))
+    assert prg.workspaces() == 1
 
 
 def test_host_call_after_device_call_without_sync(dcf):
