@@ -491,10 +491,12 @@ int try_prefix(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, int party
   return DCF_OK;
 }
 
+// Tails over cnt points of cnt / ppk consecutive keys key, key + 1, ... (ppk points each, s0: their
+// s0s back to back; one key: ppk = cnt); grid rows = keys x ranges per key.
 template <int TW, int NCH = 0>
 int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
                 uint32_t lam, uint64_t K, uint64_t key, const uint32_t* tvec, uint64_t cnt, uint8_t* ys,
-                hipStream_t st) {
+                hipStream_t st, uint64_t ppk) {
   static_assert(TW == 32 || TW == 64 || TW == 128 || TW == 256, "tile width");
   const uint32_t nch = (nlev + 1 + 3) / 4;
   const size_t lds = (size_t)nch * 16 * TW;
@@ -504,83 +506,69 @@ int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, cons
   // kTailPts points (r02i A/B on C4: 41.1-41.3 ms vs 41.7-42.3 with ranges sized to 1, 2 or 4
   // workgroups per CU).
   const uint64_t tiles = (lam + TW - 1) / TW;
-  const dim3 grid((unsigned)tiles, (unsigned)((cnt + kTailPts - 1) / kTailPts));
+  const uint64_t rpk = (ppk + kTailPts - 1) / kTailPts;
+  const dim3 grid((unsigned)tiles, (unsigned)((cnt / ppk) * rpk));
   hipLaunchKernelGGL((k_eval_wide_tail<TW, NCH>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key, tvec,
-                     cnt, kTailPts, ys, t_words(nlev));
+                     cnt, kTailPts, ys, t_words(nlev), ppk, (uint32_t)rpk);
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }
 
-// Paired-slot tail (k_eval_wide_tail2, 128-byte tiles, 6/5-bit chunks in LDS, G8 8-bit chunks in
-// global memory): the t-vectors are repacked into chunk bytes in place, the global chunk tables
-// are built (gtab: tiles x G8 x 32 KiB of scratch), then the tail runs as launch_tail does.
-template <int R6, int R5, int G8>
+// Paired-slot tail (k_eval_wide_tail2, 128-byte tiles, 6/5-bit chunks in LDS): the t-vectors are
+// repacked into chunk bytes in place, then the tail runs as launch_tail does.  (8-bit chunks in
+// global memory beside the LDS tables, read through the vector L1 / L2, measured 11-24 % slower on
+// C4: profiles/AB_LOG.md r04d.)
+template <int R6, int R5>
 int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
-                 uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, uint4* gtab,
-                 hipStream_t st, int cus) {
-  using L = Tail2Layout<R6, R5, G8>;
+                 uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
+                 int cus, uint64_t ppk) {
+  using L = Tail2Layout<R6, R5>;
   if (nlev + 1 > L::rows()) return fail(DCF_ERR_UNSUPPORTED, "tail2 layout too small");
   const uint64_t tiles = (lam + 127) / 128;
-  hipLaunchKernelGGL((k_tvec_chunks<R6, R5, G8>), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tvec, nlev,
-                     cnt);
+  hipLaunchKernelGGL((k_tvec_chunks<R6, R5>), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tvec, nlev, cnt);
   HIP_TRY(hipGetLastError());
-  if constexpr (G8 > 0) {
-    hipLaunchKernelGGL((k_tail_gtab<R6, R5, G8>), dim3((unsigned)tiles, (unsigned)G8), dim3(256), 0, st, cws, cwv, np1,
-                       nlev, lam, K, key, gtab);
-    HIP_TRY(hipGetLastError());
-  }
   const size_t lds = L::lds_bytes();
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5, G8>),
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // One workgroup per CU: the batch split into cus / tiles ranges, so the tiles of a range build
   // their tables once and walk its points together (the rows being written at any time stay
   // few), at least 32768 points per workgroup (C4 A/B: 34.36-34.38 ms vs 34.78-35.01 with
   // 32768-point ranges; 4096-point ranges 37.8-38.0).
+  // Several keys (ppk < cnt): each key's points are ranges of their own (its own tables).
   const uint64_t ranges = std::max<uint64_t>(1, (uint64_t)cus / tiles);
   const uint64_t per = std::max<uint64_t>(32768, (((cnt + ranges - 1) / ranges) + 255) & ~(uint64_t)255);
-  const dim3 grid((unsigned)tiles, (unsigned)((cnt + per - 1) / per));
-  hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5, G8>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K,
-                     key, tvec, cnt, (uint32_t)per, ys, (const uint4*)gtab);
+  const uint64_t rpk = (ppk + per - 1) / per;
+  const dim3 grid((unsigned)tiles, (unsigned)((cnt / ppk) * rpk));
+  hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key,
+                     tvec, cnt, (uint32_t)per, ys, ppk, (uint32_t)rpk);
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }
 
-// Global-table scratch of the largest paired-slot layout (launch_tail2's gtab), per 128-byte tile.
-constexpr size_t kGtabBytesPerTile = 5 * 256 * 128;
-
 // The tail for n = nlev levels: the paired-slot tail when one of its instances covers the
 // n + 1 rows with fewer LDS reads than the 4-bit tail's ceil((n + 1) / 4), else the 4-bit one.
+// ppk: points per key (= cnt for one key).
 int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
-             uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, uint4* gtab,
-             hipStream_t st, int cus) {
+             uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
+             int cus, uint64_t ppk) {
   const uint32_t nrows = nlev + 1, nch = (nrows + 3) / 4;
   if (lam % 128 == 0) {
-#define DCF_T2(A, B, G)                                                                            \
-  if (nrows <= Tail2Layout<A, B, G>::rows() && 2u * (A + B) < nch)                                 \
-    return launch_tail2<A, B, G>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, gtab, st, cus);
-    DCF_T2(1, 0, 0)   // N = 1: 9 rows, 2 reads (4-bit: 3)
-    DCF_T2(1, 1, 0)   // N = 2: 17 rows, 4 reads (5)
-    DCF_T2(2, 1, 0)   // N = 3, 4: 25 / 33 rows, 6 reads (7 / 9)
-    DCF_T2(3, 3, 0)   // N = 6..8: 49..65 rows, 12 reads (13..17)
-#ifndef DCF_T3
-#define DCF_T3 0
-#endif
-#if DCF_T3 == 3
-    DCF_T2(5, 5, 3)
-#elif DCF_T3 == 4
-    DCF_T2(5, 4, 4)
-#elif DCF_T3 == 5
-    DCF_T2(5, 3, 5)
-#endif
-    DCF_T2(5, 7, 0)   // N = 12..16: 97..129 rows, 24 reads (25..33)
+#define DCF_T2(A, B)                                                                               \
+  if (nrows <= Tail2Layout<A, B>::rows() && 2u * (A + B) < nch)                                    \
+    return launch_tail2<A, B>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus, ppk);
+    DCF_T2(1, 0)   // N = 1: 9 rows, 2 reads (4-bit: 3)
+    DCF_T2(1, 1)   // N = 2: 17 rows, 4 reads (5)
+    DCF_T2(2, 1)   // N = 3, 4: 25 / 33 rows, 6 reads (7 / 9)
+    DCF_T2(3, 3)   // N = 6..8: 49..65 rows, 12 reads (13..17)
+    DCF_T2(5, 7)   // N = 12..16: 97..129 rows, 24 reads (25..33)
 #undef DCF_T2
   }
   // 4-bit tail: the widest tile whose tables (nch x 16 entries x TW bytes) fit the LDS
-  if (nch == 33) return launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
-  if (nch <= 40) return launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
-  if (nch <= 80) return launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
-  if (nch <= 160) return launch_tail<64>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
-  return launch_tail<32>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st);
+  if (nch == 33) return launch_tail<256, 33>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
+  if (nch <= 40) return launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
+  if (nch <= 80) return launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
+  if (nch <= 160) return launch_tail<64>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
+  return launch_tail<32>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
 }
 
 // Dcf::eval at LAMBDA >= 32 for key `key` of a K-key CWB (see kernels_wide.h).
@@ -598,10 +586,9 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
   const uint64_t chunk = m < kWideChunk ? m : kWideChunk;
   const uint32_t tw = t_words(nlev);  // t-vector words per point
   const size_t tvb = (chunk * tw * 4 + 255) & ~(size_t)255;
-  int rc = ensure_ws(w, tvb + ((lam + 127) / 128) * kGtabBytesPerTile, st);
+  int rc = ensure_ws(w, tvb, st);
   if (rc) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
-  uint4* gtab = reinterpret_cast<uint4*>(w->d_ws + tvb);
   WidePrefix wpf{nullptr, 0u};
   const int mode = c.mode;
   for (uint64_t off = 0; off < m; off += chunk) {
@@ -616,7 +603,7 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
           w->dig_levels = nlev;
         }
         hipLaunchKernelGGL(k_cw_digest, dim3((4 * nlev + 255) / 256), dim3(256), 0, st, cws, cwv, cwt, nlev, lam, K,
-                           key, (uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64);
+                           key, 1u, (uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64);
         HIP_TRY(hipGetLastError());
         const uint32_t d = wide_prefix_depth(p, c, n_bytes, m);
         if (d) {
@@ -630,9 +617,9 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
       if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
       // one point per lane, one 1024-thread workgroup per CU (the T-tables fill the LDS)
 #define DCF_WHS(MH, XR)                                                                                        \
-  hipLaunchKernelGGL((k_eval_wide_head_stream<1, MH, XR, kBlock>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab,     \
+  hipLaunchKernelGGL((k_eval_wide_head_stream<1, MH, XR, false, kBlock>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p->d_tab, \
                      p->d_rk2, (const uint4*)w->d_dig, w->d_dig + (size_t)nlev * 64, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes,   \
-                     lam, K, key, cnt, w->d_ctr, ys + off * lam, tvec, wpf, tw)
+                     lam, K, key, cnt, w->d_ctr, ys + off * lam, tvec, wpf, tw, (uint32_t)cnt)
       const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16;
       if (lam == 32 && xreg) DCF_WHS(true, true);
       else if (lam == 32) DCF_WHS(true, false);
@@ -649,8 +636,66 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
                          ys + off * lam, tvec, tw);
     HIP_TRY(hipGetLastError());
     if (lam > 32) {
-      rc = run_tail(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, gtab, st, p->cus);
+      rc = run_tail(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus, cnt);
       if (rc) return rc;
+    }
+  }
+  return DCF_OK;
+}
+
+// Dcf::eval at LAMBDA >= 32 for keys 0 .. K - 1, ppk points each (key-major xs / ys, s0s[K][LAMBDA]),
+// several keys per pass: one key-major CW digest, one stream-head launch (each point's key =
+// point / ppk) and one tail launch whose workgroups build the tables of their own key.  For
+// ppk <= kWideBatchPpk (larger keys amortise their own launches: eval_wide per key).  No shared
+// prefix; the lockstep head (DCF_EVAL_TTABLE) and the MMO PRG keep the per-key path.
+constexpr uint64_t kWideBatchPpk = 32768;
+constexpr uint64_t kWideBatchKeys = 8192;  // keys per pass: tail grid rows (keys x ranges) < 65536
+int eval_wide_batch(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t ppk, int party,
+                    const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, hipStream_t st) {
+  const uint32_t lam = (uint32_t)p->lambda, nlev = (uint32_t)(8 * n_bytes);
+  if (n_bytes > kWideMaxN) return fail(DCF_ERR_UNSUPPORTED, "LAMBDA >= 32 eval supports N <= 159");
+  const size_t n = 8 * n_bytes;
+  const uint8_t* cws = cwb;
+  const uint8_t* cwv = cwb + n * K * lam;
+  const uint8_t* cwt = cwb + 2 * n * K * lam;
+  const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
+  const uint64_t kp = std::max<uint64_t>(1, std::min<uint64_t>({K, kWideChunk / ppk, kWideBatchKeys}));
+  const uint32_t tw = t_words(nlev);
+  const size_t tvb = (kp * ppk * tw * 4 + 255) & ~(size_t)255;
+  if (int rc = ensure_ws(w, tvb, st)) return rc;
+  if (w->dig_levels < kp * nlev) {
+    size_t have = (size_t)w->dig_levels * 65;
+    if (int rc = grow(&w->d_dig, &have, (size_t)kp * nlev * 65, st)) return rc;
+    w->dig_levels = (uint32_t)(kp * nlev);
+  }
+  uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
+  const WidePrefix none{nullptr, 0u};
+  const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16;
+  for (uint64_t k0 = 0; k0 < K; k0 += kp) {
+    const uint64_t nk = std::min<uint64_t>(kp, K - k0), cnt = nk * ppk;
+    HIP_TRY(hipMemsetAsync(w->d_ctr, 0, 8, st));  // the pass's work counter (the block count stays)
+    uint4* dig = (uint4*)w->d_dig;
+    uint8_t* dig_t = w->d_dig + (size_t)nk * nlev * 64;
+    hipLaunchKernelGGL(k_cw_digest, dim3((unsigned)((4 * nlev * nk + 255) / 256)), dim3(256), 0, st, cws, cwv, cwt, nlev,
+                       lam, K, k0, (uint32_t)nk, dig, dig_t);
+    HIP_TRY(hipGetLastError());
+    const uint64_t units = (cnt + kWideUnit - 1) / kWideUnit;
+    const uint64_t blocks = std::min<uint64_t>((units + 15) / 16, (uint64_t)p->cus);
+    const uint8_t* s0p = s0s + k0 * lam;
+    const uint8_t* xp = xs + k0 * ppk * n_bytes;
+    uint8_t* yp = ys + k0 * ppk * lam;
+#define DCF_WHB(MH, XR)                                                                                           \
+  hipLaunchKernelGGL((k_eval_wide_head_stream<1, MH, XR, true, kBlock>), dim3((unsigned)blocks), dim3(kBlock), 0, st, \
+                     p->d_tab, p->d_rk2, (const uint4*)dig, dig_t, np1, s0p, (uint32_t)party, xp, (uint32_t)n_bytes,  \
+                     lam, K, k0, cnt, w->d_ctr, yp, tvec, none, tw, (uint32_t)ppk)
+    if (lam == 32 && xreg) DCF_WHB(true, true);
+    else if (lam == 32) DCF_WHB(true, false);
+    else if (xreg) DCF_WHB(false, true);
+    else DCF_WHB(false, false);
+#undef DCF_WHB
+    HIP_TRY(hipGetLastError());
+    if (lam > 32) {
+      if (int rc = run_tail(cws, cwv, np1, s0p, nlev, lam, K, k0, tvec, cnt, yp, st, p->cus, ppk)) return rc;
     }
   }
   return DCF_OK;
@@ -1151,8 +1196,10 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
   hipStream_t st = L.st;
   const uint64_t total = (uint64_t)num_keys * ppk;
   const size_t n = 8 * n_bytes, lam = p->lambda;
-  if (lam > 16) {  // head/tail pipeline per key
+  if (lam > 16) {  // head/tail pipeline: keys with few points batched, else per key
     phase_mark(p, L, 1);
+    if (num_keys > 1 && ppk > 0 && p->kind == 0 && c.mode != DCF_EVAL_TTABLE && ppk <= kWideBatchPpk)
+      return eval_wide_batch(p, w, n_bytes, num_keys, ppk, party, cwb, s0s, xs, ys, st);
     for (uint64_t k = 0; k < num_keys; ++k) {
       int rc = p->kind == 1 ? eval_mmo_wide(p, w, n_bytes, num_keys, k, party, cwb, s0s + k * lam,
                                             xs + k * ppk * n_bytes, ppk, ys + k * ppk * lam, st)
@@ -1304,14 +1351,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     const uint8_t* sct = cwt;
     if (multi) {  // key-major digest of the K keys (kernels_stream.h)
       if (int rc = grow(&w->d_kdig, &w->kdig_bytes, (size_t)num_keys * n * 33, st)) return rc;
-#if defined(DCF_C5V) && (DCF_C5V & 1)
-      hipLaunchKernelGGL(k_cw_keymajor_tiled, dim3((unsigned)((num_keys + kKmKeys - 1) / kKmKeys), (n + kKmLevs - 1) / kKmLevs),
-                         dim3(256), 0, st, cws, cwv, cwt, (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig,
-                         w->d_kdig + (size_t)num_keys * n * 32);
-#else
       hipLaunchKernelGGL(k_cw_keymajor, dim3((unsigned)((num_keys + 15) / 16)), dim3(256), 0, st, cws, cwv, cwt,
                          (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig, w->d_kdig + (size_t)num_keys * n * 32);
-#endif
       HIP_TRY(hipGetLastError());
       scs = (const uint4*)w->d_kdig;
       sct = w->d_kdig + (size_t)num_keys * n * 32;
@@ -1334,16 +1375,10 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
         }
       }
       if (w->pfx_bytes >= need) {
-#if defined(DCF_C5V) && (DCF_C5V & 2)
-        hipLaunchKernelGGL(k_mk_prefix_dfs16, dim3((unsigned)((num_keys + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                           p->d_tab, cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party, (uint64_t)num_keys,
-                           (uint4*)w->d_pfx, p->d_rk0, w->d_ctr);
-#else
         hipLaunchKernelGGL(k_mk_prefix16<true>,
                            dim3((unsigned)(((num_keys << kMkPfxRoot) + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            st, p->d_tab, p->rk[0], cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party,
                            (uint64_t)num_keys, (uint4*)w->d_pfx, p->d_rk0, w->d_ctr);
-#endif
         HIP_TRY(hipGetLastError());
         pf = PrefixTable{(const uint4*)w->d_pfx, kMkPfxLevels};
         w->last_prefix = kMkPfxLevels;

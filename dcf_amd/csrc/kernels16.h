@@ -599,83 +599,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_mk_prefix16(
   }
 }
 
-// Multi-key top trees, one thread per key: the key's whole kMkPfxLevels-level tree depth-first
-// (2^L - 1 PRG calls, 62 blocks at L = 5; k_mk_prefix16 walks the root levels once per thread,
-// 72), the right child of every expansion above the bottom waiting on a register stack (one
-// 9-word slot per depth, as k_prefix_build16's tail).  Leaf-parent i (bits Msb-first = the
-// choices at depths 0 .. L-2) resumes from the slot at the depth of i's lowest set bit and writes
-// rows 2i, 2i + 1 of the key's 2^L.  CWs per expansion are per-lane loads (lanes = consecutive
-// keys: one contiguous KiB per level and field).
-__global__ __launch_bounds__(kBlock, 1) void k_mk_prefix_dfs16(
-    const uint32_t* __restrict__ tab, const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
-    const uint8_t* __restrict__ cw_t, const uint4* __restrict__ s0s, const uint32_t party, const uint64_t num_keys,
-    uint4* __restrict__ table, const uint4* __restrict__ rkg, uint32_t* __restrict__ ctr) {
-  constexpr uint32_t H = kMkPfxLevels;
-  __shared__ uint32_t lds[kLdsWords];
-  lds_fill_tables(lds, tab);
-  const uint32_t lc = lane_const();
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t live = __ballot(k < num_keys);
-  if ((threadIdx.x & 63u) == 0 && live)
-    atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1,
-              2ull * ((1u << H) - 1u) * (unsigned long long)__popcll(live));
-  if (k >= num_keys) return;  // after the only barrier (lds_fill_tables)
-  const RoundKeys rk{};       // unused: round keys per round from rkg
-  uint32_t stk[H - 1][9];     // pending right children: s[4] | v[4] | t, by depth
-  uint32_t n[9];
-  {
-    const uint4 sv = s0s[k];
-    n[0] = sv.x; n[1] = sv.y; n[2] = sv.z; n[3] = sv.w;
-    n[4] = n[5] = n[6] = n[7] = 0u;
-    n[8] = party;
-  }
-  uint4* rows = table + 2ull * (k << H);
-  for (uint32_t i = 0; i < (1u << (H - 1u)); ++i) {
-    uint32_t d = 0;
-    if (i) {  // resume at the right child saved at depth H - 2 - ctz(i) (wave-uniform)
-      const uint32_t r = H - 2u - (uint32_t)__builtin_ctz(i);
-#pragma unroll
-      for (uint32_t q = 0; q + 1 < H; ++q)
-        if (q == r)
-#pragma unroll
-          for (int e = 0; e < 9; ++e) n[e] = stk[q][e];
-      d = r + 1u;
-    }
-    for (;; ++d) {  // expand depth d (level d of the key's tree)
-      const uint4 cs = cw_s[(uint64_t)d * num_keys + k], cv = cw_v[(uint64_t)d * num_keys + k];
-      const uint32_t ct = cw_t[(uint64_t)d * num_keys + k];
-      const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
-      const uint32_t s[4] = {n[0], n[1], n[2], n[3]}, v[4] = {n[4], n[5], n[6], n[7]};
-      uint32_t sl[4], vl[4], sr[4], vr[4], tl, tr;
-      fd_children<true>(lds, lc, rk, csw, cvw, ct, s, v, n[8], sl, vl, tl, sr, vr, tr, rkg);
-      if (d + 1u == H) {  // bottom: rows 2i, 2i + 1
-        uint4* row = rows + 4u * i;
-        row[0] = make_uint4(sl[0], sl[1], sl[2], (sl[3] & kMaskLast) | ((tl & 1u) << 24));
-        row[1] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
-        row[2] = make_uint4(sr[0], sr[1], sr[2], (sr[3] & kMaskLast) | ((tr & 1u) << 24));
-        row[3] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
-        break;
-      }
-#pragma unroll
-      for (uint32_t q = 0; q + 1 < H; ++q)
-        if (q == d) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            stk[q][e] = sr[e];
-            stk[q][4 + e] = vr[e];
-          }
-          stk[q][8] = tr;
-        }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        n[e] = sl[e];
-        n[4 + e] = vl[e];
-      }
-      n[8] = tl;
-    }
-  }
-}
-
 // Shared-prefix table (PrefixTable rows) of depth D in ONE launch, Hirose PRG.
 // The level-by-level build (k_fd_level16, one launch per level) spends most of its time
 // on the narrow upper levels (C2: 23 launches, ~1 ms of a 5 ms step).  Here workgroup w
@@ -697,8 +620,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     uint4* __restrict__ table, const uint4* __restrict__ rkg) {
   constexpr bool GKB = true;
   __shared__ uint32_t lds[kLdsWords];
-  __shared__ uint4 root_s, root_v;
-  __shared__ uint32_t root_t;
+  // the narrow levels below the root path: up to 1024 nodes of 32 B (s with t in bit 0 of byte 15 |
+  // v); then the depth-first tail's work counter
+  __shared__ uint4 nodes[2048];
   lds_fill_tables(lds, tab);
   DCF_CLK(6, 0);  // (diagnostic builds) after the table fill; (6, 1) after the breadth-first levels
   const uint32_t lc = lane_const();
@@ -706,7 +630,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
   uint8_t* X = buf_a + (uint64_t)w * region_bytes;
   uint8_t* Y = buf_b + (uint64_t)w * region_bytes;
   const uint32_t R = region_nodes;
-  if (threadIdx.x < 64) {  // wave 0: the path root -> node w of level S (every lane the same node)
+  // wave 0: the path root -> node w of level S (every lane the same node); thread 0 keeps it for
+  // the first expansion
+  uint32_t rs[4] = {0u, 0u, 0u, 0u}, rv[4] = {0u, 0u, 0u, 0u}, rt = 0u;
+  if (threadIdx.x < 64) {
     const uint4 sv = s0[0];
     uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w}, v[4] = {0u, 0u, 0u, 0u}, t = party;
     for (uint32_t lev = 0; lev < S; ++lev) {
@@ -722,15 +649,52 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
       }
       t = right ? tr : tl;
     }
-    if (threadIdx.x == 0) {
-      root_s = make_uint4(s[0], s[1], s[2], s[3]);
-      root_v = make_uint4(v[0], v[1], v[2], v[3]);
-      root_t = t;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      rs[k] = s[k];
+      rv[k] = v[k];
     }
+    rt = t;
   }
-  __syncthreads();
   DCF_CLK(7, 0);  // (diagnostic builds) root path done; (7, 1) thread 0's depth-first tail done
-  for (uint32_t lev = S; lev < D - H; ++lev) {
+  uint32_t L0 = S;  // first level whose parents come from the global buffers (or the root / LDS)
+  // Levels whose children fit the LDS node buffer (<= 512 parents), expanded in place: a level
+  // costs two workgroup barriers instead of a round trip through the global buffers (C2 A/B r04e:
+  // table build 0.571-0.583 vs 0.574-0.599 ms, 4.766-4.772 vs 4.760-4.767 G evals/s).  At least one
+  // level through the global buffers follows (it reads this loop's last level from the LDS).
+  for (; L0 + 1u < D - H && L0 - S <= 9u; ++L0) {
+    const uint32_t np = 1u << (L0 - S), j = threadIdx.x;
+    const uint4 cs = cw_s[L0], cv = cw_v[L0];
+    const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
+    const uint32_t ct = cw_t[L0];
+    uint32_t sl[4], vl[4], sr[4], vr[4], tl = 0u, tr = 0u;
+    if (j < np) {
+      uint32_t s[4], v[4], t;
+      if (L0 == S) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          s[k] = rs[k];
+          v[k] = rv[k];
+        }
+        t = rt;
+      } else {
+        const uint4 a = nodes[2 * j], b = nodes[2 * j + 1];
+        s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w & kMaskLast;
+        v[0] = b.x; v[1] = b.y; v[2] = b.z; v[3] = b.w;
+        t = (a.w >> 24) & 1u;
+      }
+      fd_children<GKB>(lds, lc, rk, csw, cvw, ct, s, v, t, sl, vl, tl, sr, vr, tr, rkg);
+    }
+    __syncthreads();  // every parent read before any child overwrites it
+    if (j < np) {
+      nodes[4 * j] = make_uint4(sl[0], sl[1], sl[2], (sl[3] & kMaskLast) | (tl << 24));
+      nodes[4 * j + 1] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
+      nodes[4 * j + 2] = make_uint4(sr[0], sr[1], sr[2], (sr[3] & kMaskLast) | (tr << 24));
+      nodes[4 * j + 3] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
+    }
+    __syncthreads();
+  }
+  for (uint32_t lev = L0; lev < D - H; ++lev) {
     const uint32_t np = 1u << (lev - S);  // this workgroup's parents at level lev
     const bool last = lev + 1u == D;
     const uint4 cs = cw_s[lev], cv = cw_v[lev];
@@ -747,9 +711,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
     uint4 nsv = make_uint4(0u, 0u, 0u, 0u), nvv = nsv;
     uint32_t nt = 0u;
     if (threadIdx.x < np) {
-      nsv = lev == S ? root_s : xs_[threadIdx.x];
-      nvv = lev == S ? root_v : xv_[threadIdx.x];
-      nt = lev == S ? root_t : xt_[threadIdx.x];
+      if (lev == S) {  // np = 1: thread 0, the root path's node
+        nsv = make_uint4(rs[0], rs[1], rs[2], rs[3]);
+        nvv = make_uint4(rv[0], rv[1], rv[2], rv[3]);
+        nt = rt;
+      } else if (lev == L0) {  // the last LDS level (np <= 1024: one parent per thread)
+        const uint4 a = nodes[2 * threadIdx.x], b = nodes[2 * threadIdx.x + 1];
+        nsv = make_uint4(a.x, a.y, a.z, a.w & kMaskLast);
+        nvv = b;
+        nt = (a.w >> 24) & 1u;
+      } else {
+        nsv = xs_[threadIdx.x];
+        nvv = xv_[threadIdx.x];
+        nt = xt_[threadIdx.x];
+      }
     }
     for (uint32_t j = threadIdx.x; j < np; j += blockDim.x) {
       const uint4 sv = nsv, vv = nvv;
@@ -795,7 +770,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
   const uint4* xs_ = reinterpret_cast<const uint4*>(X);
   const uint4* xv_ = xs_ + R;
   const uint8_t* xt_ = X + (uint64_t)R * 32u;
-  for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+  // Nodes are claimed 64 at a time per wave from an LDS counter (the node buffer is free by now):
+  // the waves of a workgroup do not progress at one rate (issue goes to the older wave first), and
+  // with a static split the oldest wave finished its nodes well before the youngest (in-kernel
+  // stamps, C2: wave 0 at 0.39 ms of a ~0.58 ms build, profiles/r04d2_c2_timeline.json).
+  uint32_t* dctr = reinterpret_cast<uint32_t*>(nodes);
+  if (threadIdx.x == 0) *dctr = 0u;
+  __syncthreads();
+  for (;;) {  // nb is a multiple of 64 (B - S >= 10)
+    uint32_t base = 0u;
+    if ((threadIdx.x & 63u) == 0)
+      base = __hip_atomic_fetch_add(dctr, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= nb) break;
+    const uint32_t j = base + (threadIdx.x & 63u);
     uint32_t stk[kPfxDfsMax - 1][9];  // pending right children: s[4] | v[4] | t, by depth
     uint32_t n[9];
     {
@@ -849,6 +837,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_prefix_build16(
       }
     }
   }
+#ifdef DCF_CLOCK_STAMPS
+  __syncthreads();  // (diagnostic builds) stamp when the workgroup's last wave is done
+#endif
   DCF_CLK(7, 1);
 }
 

@@ -238,42 +238,6 @@ __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ c
   }
 }
 
-// Key-major CW digest, tiled: a workgroup transposes 64 keys x 16 levels through 33 KiB of LDS
-// (4 workgroups per CU): per level 1 KiB contiguous reads of cw_s and of cw_v, per key 512 B
-// contiguous writes of dig and 16 B of dig_t.  A key's LDS row is padded to 33 uint4 so the
-// transposing writes spread over the banks.
-constexpr uint32_t kKmKeys = 64, kKmLevs = 16;
-__global__ __launch_bounds__(256) void k_cw_keymajor_tiled(const uint4* __restrict__ cw_s,
-                                                           const uint4* __restrict__ cw_v,
-                                                           const uint8_t* __restrict__ cw_t, const uint32_t nlev,
-                                                           const uint64_t num_keys, uint4* __restrict__ dig,
-                                                           uint8_t* __restrict__ dig_t) {
-  constexpr uint32_t RW = 2 * kKmLevs + 1;  // uint4 per key row
-  __shared__ uint4 sh[kKmKeys * RW];
-  __shared__ uint8_t sht[kKmKeys * kKmLevs];
-  const uint64_t k0 = (uint64_t)blockIdx.x * kKmKeys;
-  const uint32_t l0 = blockIdx.y * kKmLevs;
-  const uint32_t nk = (uint32_t)min<uint64_t>(kKmKeys, num_keys - k0), nl = min(kKmLevs, nlev - l0);
-  for (uint32_t it = threadIdx.x; it < kKmKeys * kKmLevs; it += blockDim.x) {
-    const uint32_t l = it / kKmKeys, kk = it % kKmKeys;
-    if (kk < nk && l < nl) {
-      const uint64_t src = (uint64_t)(l0 + l) * num_keys + k0 + kk;
-      sh[kk * RW + 2 * l] = cw_s[src];
-      sh[kk * RW + 2 * l + 1] = cw_v[src];
-      sht[kk * kKmLevs + l] = cw_t[src];
-    }
-  }
-  __syncthreads();
-  for (uint32_t it = threadIdx.x; it < kKmKeys * 2 * kKmLevs; it += blockDim.x) {
-    const uint32_t kk = it / (2 * kKmLevs), r = it % (2 * kKmLevs);
-    if (kk < nk && r < 2 * nl) dig[(k0 + kk) * nlev * 2 + 2 * l0 + r] = sh[kk * RW + r];
-  }
-  for (uint32_t it = threadIdx.x; it < kKmKeys * kKmLevs; it += blockDim.x) {
-    const uint32_t kk = it / kKmLevs, l = it % kKmLevs;
-    if (kk < nk && l < nl) dig_t[(k0 + kk) * nlev + l0 + l] = sht[kk * kKmLevs + l];
-  }
-}
-
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
 // GK: round keys per round from the device copy rkg (aes256_tt_gk); otherwise from the kernel
 // argument (SGPRs).  PFX: every stream starts below the per-key top trees (multi-key).

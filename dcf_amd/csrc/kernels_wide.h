@@ -285,10 +285,15 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
                                                             const uint8_t* __restrict__ cw_np1,
                                                             const uint8_t* __restrict__ s0, const uint32_t nlev,
                                                             const uint32_t lam, const uint64_t num_keys,
-                                                            const uint64_t key, const uint32_t* __restrict__ tvec,
+                                                            const uint64_t key0, const uint32_t* __restrict__ tvec,
                                                             const uint64_t count, const uint32_t pts_per_block,
-                                                            uint8_t* __restrict__ ys, const uint32_t tw) {
+                                                            uint8_t* __restrict__ ys, const uint32_t tw,
+                                                            const uint64_t ppk, const uint32_t rpk) {
   constexpr int LP = TW / 16;
+  // Row blockIdx.y of the grid = range rr of key kk of the launch's keys (ppk points each, rpk
+  // ranges per key; one key: ppk = count, rpk = gridDim.y)
+  const uint32_t kk = blockIdx.y / rpk, rr = blockIdx.y % rpk;
+  const uint64_t key = key0 + kk;
   extern __shared__ uint4 G[];
   if (TW == 256 && (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)G != 0u) __builtin_trap();
   const uint32_t nrows = nlev + 1, nch = (nrows + 3) >> 2;
@@ -320,11 +325,12 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
   const bool lane_live = off >= 32u && off < lam;
   uint4 cst = make_uint4(0u, 0u, 0u, 0u);
   if (lane_live) {
-    cst = *reinterpret_cast<const uint4*>(s0 + off);
+    cst = *reinterpret_cast<const uint4*>(s0 + (uint64_t)kk * lam + off);
     if (off + 16 == lam) cst.w &= kMaskLast;
   }
-  const uint64_t p0 = (uint64_t)blockIdx.y * pts_per_block;
-  const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
+  const uint64_t kb = (uint64_t)kk * ppk;
+  const uint64_t p0 = kb + (uint64_t)rr * pts_per_block;
+  const uint64_t p1 = min<uint64_t>(min<uint64_t>(count, kb + ppk), p0 + pts_per_block);
   const uint32_t pstep = blockDim.x / LP;
   const uint32_t pin = (threadIdx.x & 63u) / LP;  // the lane's point among the wave's 64 / LP
   // t-vectors (their first 64 B) are loaded two points ahead into ping-pong registers,
@@ -379,54 +385,23 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
 // the index of chunk k: chunks 0 .. 2 R6 - 1 are 6 rows each from row 0, then 5-row chunks.
 // Rows past n + 1 are zero.  Kept in place in the head's 64-byte t-vector rows (first 32 B).
 // ------------------------------------------------------------------------
-//
-// G8 > 0 (LDS + L2 split): the last G8 chunks are 8 bits wide and their tables (256 entries x 128 B
-// per chunk and tile, built once per call by k_tail_gtab) live in global memory, read through the
-// vector L1 / L2 (a tile's tables are 32 KiB per chunk: L2-resident, both ranges of a tile share an
-// XCD) instead of the LDS: the LDS is the tail's bound, so moving rows to the other read path
-// shortens it.
-template <int R6, int R5, int G8 = 0>
+template <int R6, int R5>
 struct Tail2Layout {
-  static constexpr int R = R6 + R5, NL = 2 * R, NC = NL + G8;
+  static constexpr int R = R6 + R5, NC = 2 * R;
   static_assert(NC <= 32, "t-vector holds 32 chunk bytes");
-  static constexpr uint32_t width(int k) { return k < 2 * R6 ? 6u : (k < NL ? 5u : 8u); }
-  static constexpr uint32_t start(int k) {
-    return k < 2 * R6 ? 6u * k : (k < NL ? 12u * R6 + 5u * (k - 2 * R6) : 12u * R6 + 10u * R5 + 8u * (k - NL));
-  }
+  static constexpr uint32_t width(int k) { return k < 2 * R6 ? 6u : 5u; }
+  static constexpr uint32_t start(int k) { return k < 2 * R6 ? 6u * k : 12u * R6 + 5u * (k - 2 * R6); }
   static constexpr uint32_t region(int m) { return m < R6 ? 16384u * m : 16384u * R6 + 8192u * (m - R6); }
-  static constexpr uint32_t rows() { return 12u * R6 + 10u * R5 + 8u * G8; }
+  static constexpr uint32_t rows() { return 12u * R6 + 10u * R5; }
   static constexpr uint32_t lds_bytes() { return region(R) + 16u; }  // + the workgroup's block counter
-  static constexpr uint32_t gtab_uint4_per_tile() { return G8 * 256u * 8u; }
 };
-
-// The global chunk tables of k_eval_wide_tail2<R6, R5, G8>: gtab[tile][g][entry][q] (uint4), entry e
-// of chunk NL + g = XOR of the W-row pieces of its set bits.  Grid (tiles, G8), 256 threads.
-template <int R6, int R5, int G8>
-__global__ void k_tail_gtab(const uint8_t* __restrict__ cw_s, const uint8_t* __restrict__ cw_v,
-                            const uint8_t* __restrict__ cw_np1, const uint32_t nlev, const uint32_t lam,
-                            const uint64_t num_keys, const uint64_t key, uint4* __restrict__ gtab) {
-  using L = Tail2Layout<R6, R5, G8>;
-  const uint32_t tile = blockIdx.x, g = blockIdx.y, st = L::start(L::NL + (int)g);
-  uint4* out = gtab + ((uint64_t)tile * G8 + g) * 2048u;
-  for (uint32_t it = threadIdx.x; it < 2048u; it += blockDim.x) {
-    const uint32_t e = it >> 3, q = it & 7u, off = tile * 128u + 16u * q;
-    uint4 acc = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (uint32_t b = 0; b < 8; ++b)
-      if ((e >> b) & 1u) {
-        const uint4 w = w_row_piece(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, st + b, off);
-        acc.x ^= w.x; acc.y ^= w.y; acc.z ^= w.z; acc.w ^= w.w;
-      }
-    out[it] = acc;
-  }
-}
 
 // Old nibble t-vector (row r at byte r >> 2, bit r & 3; words 0 .. nlev >> 4 valid) -> chunk
 // bytes of Tail2Layout<R6, R5>, in place (bytes [0, 32) of each 64-byte row).  One thread
 // per point: 36 of 64 bytes read, 32 written.
-template <int R6, int R5, int G8 = 0>
+template <int R6, int R5>
 __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, const uint64_t count) {
-  using L = Tail2Layout<R6, R5, G8>;
+  using L = Tail2Layout<R6, R5>;
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= count) return;
   uint32_t* row = tvec + p * kTWords;
@@ -460,17 +435,21 @@ __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, 
   o4[1] = make_uint4(out[4], out[5], out[6], out[7]);
 }
 
-template <int R6, int R5, int G8 = 0>
+template <int R6, int R5>
 __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __restrict__ cw_s,
                                                              const uint8_t* __restrict__ cw_v,
                                                              const uint8_t* __restrict__ cw_np1,
                                                              const uint8_t* __restrict__ s0, const uint32_t nlev,
                                                              const uint32_t lam, const uint64_t num_keys,
-                                                             const uint64_t key, const uint32_t* __restrict__ tvec,
+                                                             const uint64_t key0, const uint32_t* __restrict__ tvec,
                                                              const uint64_t count, const uint32_t pts_per_block,
-                                                             uint8_t* __restrict__ ys, const uint4* __restrict__ gtab) {
-  using L = Tail2Layout<R6, R5, G8>;
+                                                             uint8_t* __restrict__ ys, const uint64_t ppk,
+                                                             const uint32_t rpk) {
+  using L = Tail2Layout<R6, R5>;
   constexpr int TW = 128, LP = 8;
+  // Row blockIdx.y of the grid = range rr of key kk of the launch's keys (as k_eval_wide_tail)
+  const uint32_t kk = blockIdx.y / rpk, rr = blockIdx.y % rpk;
+  const uint64_t key = key0 + kk;
   DCF_CLK(4, 0);  // (diagnostic builds) workgroup entry, before the table build
   extern __shared__ uint4 G[];
   if ((uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)G != 0u) __builtin_trap();
@@ -547,7 +526,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   const bool lane_live = off >= 32u && off < lam;
   uint4 cst = make_uint4(0u, 0u, 0u, 0u);
   if (lane_live) {
-    cst = *reinterpret_cast<const uint4*>(s0 + off);
+    cst = *reinterpret_cast<const uint4*>(s0 + (uint64_t)kk * lam + off);
     if (off + 16 == lam) cst.w &= kMaskLast;
   }
   // lane constants (address byte 0 = slot, byte 2 = 64 KiB group): step i of a region reads
@@ -556,8 +535,9 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   // pi = 1: swap the chunk bytes of each region (stored pre-swapped by k_tvec_chunks instead, the
   // tail has 6 fewer v_perm per point: C4 A/B 34.8-35.1 vs 34.5-34.8 ms, no gain — kept here)
   const uint32_t rsel = pi ? 0x02030001u : 0x03020100u;
-  const uint64_t p0 = (uint64_t)blockIdx.y * pts_per_block;
-  const uint64_t p1 = min<uint64_t>(count, p0 + pts_per_block);
+  const uint64_t kb = (uint64_t)kk * ppk;
+  const uint64_t p0 = kb + (uint64_t)rr * pts_per_block;
+  const uint64_t p1 = min<uint64_t>(min<uint64_t>(count, kb + ppk), p0 + pts_per_block);
   const uint32_t pin = (threadIdx.x & 63u) / LP;  // the lane's point among the wave's 8
   const uint4* tv4 = reinterpret_cast<const uint4*>(tvec);
   auto load_t = [&](uint4 (&d)[2], uint64_t pp) {
@@ -589,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   // counts vmcnt exactly (the t-vectors, loaded at the end of an iteration, are waited on at the
   // end of the next one, past the two y stores).  Past-the-end lanes load a clamped row and their
   // stores are dropped (offset past num_records).
-  const uint32_t nblk = (uint32_t)((p1 - p0 + 15) / 16);
+  const uint32_t nblk = p1 > p0 ? (uint32_t)((p1 - p0 + 15) / 16) : 0u;
   auto claim = [&]() -> uint32_t {
     uint32_t b = 0u;
     if ((threadIdx.x & 63u) == 0) b = __hip_atomic_fetch_add(bctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -607,22 +587,8 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   uint32_t bn = claim();
   load_t(ta, p0 + 16u * bn + pin);
   load_t(tb, p0 + 16u * bn + 8u + pin);
-  // G8: this tile's global chunk tables; chunk NL + g's entry index is byte NL + g of the chunk
-  // vector (byte (NL + g) ^ pi of the pair-rotated words)
-  const uint4* __restrict__ gt = gtab + (uint64_t)blockIdx.x * L::gtab_uint4_per_tile() + q;
-  auto gentry = [&](const uint32_t (&tw)[NW], int g) {
-    const uint32_t k = (uint32_t)(L::NL + g) ^ pi;
-    return (tw[k >> 2] >> (8u * (k & 3u))) & 0xFFu;
-  };
   while (bc < nblk) {
     uint32_t aa[4] = {cst.x, cst.y, cst.z, cst.w}, ab[4] = {cst.x, cst.y, cst.z, cst.w};
-    // the global entries first: their L2 round trip overlaps the LDS reads below
-    uint4 ga[G8 > 0 ? G8 : 1], gb[G8 > 0 ? G8 : 1];
-#pragma unroll
-    for (int g = 0; g < G8; ++g) {
-      ga[g] = gt[(uint32_t)g * 2048u + gentry(twa, g) * 8u];
-      gb[g] = gt[(uint32_t)g * 2048u + gentry(twb, g) * 8u];
-    }
     constexpr int BT = 2;
     // BT regions (4 reads each) are issued before their XORs: the compiler
     // otherwise waits after every two reads, ~3 reads in flight per wave
@@ -654,11 +620,6 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
           ab[0] = xor3(ab[0], b0.x, b1.x); ab[1] = xor3(ab[1], b0.y, b1.y);
           ab[2] = xor3(ab[2], b0.z, b1.z); ab[3] = xor3(ab[3], b0.w, b1.w);
         }
-    }
-#pragma unroll
-    for (int g = 0; g < G8; ++g) {
-      aa[0] ^= ga[g].x; aa[1] ^= ga[g].y; aa[2] ^= ga[g].z; aa[3] ^= ga[g].w;
-      ab[0] ^= gb[g].x; ab[1] ^= gb[g].y; ab[2] ^= gb[g].z; ab[3] ^= gb[g].w;
     }
     const uint64_t pw = p0 + 16u * bc, pa = pw + pin, pb = pa + 8u;
     tail_store<LP>(ys, pw, pin, lam, off, kill | (pa < p1 ? 0u : dead), make_uint4(aa[0], aa[1], aa[2], aa[3]));

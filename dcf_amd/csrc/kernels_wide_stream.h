@@ -43,15 +43,20 @@ struct WideLane {
   uint32_t dB[NS][4];                    // this level's B ^ ~s[0:16) (B reuse)
   uint32_t t[NS], ph[NS], lev[NS], cur[NS], tR[NS], tacc[NS];
   uint32_t xq[NS][3];                    // XREG: the point's next raw x words (byte-swapped on use)
-  uint32_t pt[NS];                       // point index within this launch (<= 2^20); x row = xs + pt * N
+  uint32_t pt[NS];                       // point index within this launch (<= 2^22); x row = xs + pt * N
+  uint32_t kk[NS];                       // MK: the point's key within this launch (pt / points per key)
   bool alive[NS];
 };
 
-template <int NS, bool XREG>
+template <int NS, bool XREG, bool MK>
 __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, const uint8_t* __restrict__ s0p,
                                            uint32_t party, const uint8_t* __restrict__ xs, uint32_t nbytes,
-                                           const WidePrefix& pf, uint32_t* __restrict__ tvec, uint32_t tw) {
-  const uint4* s4 = reinterpret_cast<const uint4*>(s0p);  // k.s0s[0] (lib.rs:168), L2-resident
+                                           const WidePrefix& pf, uint32_t* __restrict__ tvec, uint32_t tw,
+                                           uint32_t ppk, uint32_t lam) {
+  const uint32_t kk = MK ? p / ppk : 0u;
+  L.kk[i] = kk;
+  // k.s0s[0] (lib.rs:168) of the point's key, L2-resident
+  const uint4* s4 = reinterpret_cast<const uint4*>(s0p + (uint64_t)kk * lam);
   const uint4 a = s4[0], b = s4[1];
   L.s[i][0] = a.x; L.s[i][1] = a.y; L.s[i][2] = a.z; L.s[i][3] = a.w;
   L.s[i][4] = b.x; L.s[i][5] = b.y; L.s[i][6] = b.z; L.s[i][7] = b.w;
@@ -103,12 +108,12 @@ __device__ __forceinline__ void wide_start(WideLane<NS>& L, int i, uint32_t p, c
 // ~11 % of the head's LDS instructions to lanes idling at the end (PMC: 265 per block vs 239).
 constexpr uint32_t kWideUnit = 64;
 
-template <int NS, bool XREG>
+template <int NS, bool XREG, bool MK>
 __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, uint64_t& unext, uint64_t& uend,
                                             bool& exhausted, uint32_t* __restrict__ ctr, uint64_t nunits,
                                             uint64_t count, const uint8_t* __restrict__ s0p, uint32_t party,
                                             const uint8_t* __restrict__ xs, uint32_t nbytes, const WidePrefix& pf,
-                                            uint32_t* __restrict__ tvec, uint32_t tw) {
+                                            uint32_t* __restrict__ tvec, uint32_t tw, uint32_t ppk, uint32_t lam) {
   uint64_t need = __ballot(mine);
   while (need) {
     if (unext >= uend && !exhausted) {
@@ -129,7 +134,7 @@ __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, u
     }
     const uint32_t rank = lane_rank(need);
     const bool take = mine && (uint64_t)rank < uend - unext;
-    if (take) wide_start<NS, XREG>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes, pf, tvec, tw);
+    if (take) wide_start<NS, XREG, MK>(L, i, (uint32_t)(unext + rank), s0p, party, xs, nbytes, pf, tvec, tw, ppk, lam);
     const uint64_t taken = __ballot(take);
     unext += (uint64_t)__popcll(taken);
     need &= ~taken;
@@ -137,33 +142,36 @@ __device__ __forceinline__ void wide_refill(WideLane<NS>& L, int i, bool mine, u
   }
 }
 
-// Compact CW digest of key `key` for the stream head: dig[4 l .. 4 l + 4) = cw_s[l][0:32) |
-// cw_v[l][0:32), dig_t[l] = cw_t[l].
+// Compact CW digest of keys key0 .. key0 + nk - 1 for the stream head, key-major: for key kk of
+// the range, dig[4 (kk nlev + l) .. + 4) = cw_s[l][0:32) | cw_v[l][0:32), dig_t[kk nlev + l] = cw_t[l].
 __global__ void k_cw_digest(const uint8_t* __restrict__ cw_s, const uint8_t* __restrict__ cw_v,
                             const uint8_t* __restrict__ cw_t, const uint32_t nlev, const uint32_t lam,
-                            const uint64_t num_keys, const uint64_t key, uint4* __restrict__ dig,
+                            const uint64_t num_keys, const uint64_t key0, const uint32_t nk, uint4* __restrict__ dig,
                             uint8_t* __restrict__ dig_t) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 4 * nlev) return;
-  const uint32_t l = i >> 2, q = i & 3u;
-  const uint64_t ci = (uint64_t)l * num_keys + key;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4ull * nlev * nk) return;
+  const uint32_t kk = (uint32_t)(i / (4u * nlev)), r = (uint32_t)(i % (4u * nlev));
+  const uint32_t l = r >> 2, q = r & 3u;
+  const uint64_t ci = (uint64_t)l * num_keys + key0 + kk;
   const uint8_t* src = (q < 2 ? cw_s : cw_v) + ci * lam + 16u * (q & 1u);
   dig[i] = *reinterpret_cast<const uint4*>(src);
-  if (q == 0) dig_t[l] = cw_t[ci];
+  if (q == 0) dig_t[(uint64_t)kk * nlev + l] = cw_t[ci];
 }
 
 // Round keys: the lane's schedule (cipher 0 or 17) from the LDS copy, one ds_read_b128 per round
 // and block.  Through the vector L1 instead (per-lane buffer loads, or both schedules by uniform
 // loads and a per-word pick) it measured 4-6 % slower on C4: the key waits retire in order behind
 // the CW loads (AB_LOG r02z / r03f).  B reuse: the B block after a right step at t = 0 is skipped.
-// Single key `key` of a num_keys-key CWB; count <= 2^20 points per launch.
-template <int NS, bool MASK_HEAD, bool XREG, int WG = kBlock>
+// Key `key` of a num_keys-key CWB; count <= 2^22 points per launch.  MK (batched keys): the
+// launch's points are keys key .. key + count / ppk - 1, ppk points each (point p: key p / ppk),
+// dig / dig_t / s0p hold those keys back to back, no shared prefix.
+template <int NS, bool MASK_HEAD, bool XREG, bool MK, int WG = kBlock>
 __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
     const uint8_t* __restrict__ dig_t, const uint8_t* __restrict__ cw_np1,
     const uint8_t* __restrict__ s0p, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint32_t lam, const uint64_t num_keys, const uint64_t key, const uint64_t count, uint32_t* __restrict__ ctr,
-    uint8_t* __restrict__ ys, uint32_t* __restrict__ tvec, const WidePrefix pf, const uint32_t tw) {
+    uint8_t* __restrict__ ys, uint32_t* __restrict__ tvec, const WidePrefix pf, const uint32_t tw, const uint32_t ppk) {
   DCF_CLK(5, 0);  // (diagnostic builds) workgroup entry, before the table fill
   __shared__ uint32_t lds[kLdsWords];
   // Schedules of cipher 0 (slots 0..14) and cipher 17 (slots 23..37): 23 slots apart,
@@ -186,11 +194,12 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     L.alive[i] = false;
     L.lev[i] = 0u;
     L.ph[i] = 0u;
+    L.kk[i] = 0u;  // an idle stream's CW loads stay in bounds
   }
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    wide_refill<NS, XREG>(L, i, true, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes, pf,
-                          tvec, tw);
+    wide_refill<NS, XREG, MK>(L, i, true, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes, pf,
+                              tvec, tw, ppk, lam);
 
   for (;;) {
     bool any = false;
@@ -210,7 +219,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     uint32_t ct[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
-      const uint32_t lv = min(L.lev[i], nlev - 1u);
+      const uint32_t lv = min(L.lev[i], nlev - 1u) + (MK ? L.kk[i] * nlev : 0u);
       const uint4* d4 = dig + 4u * lv;
       cs[i][0] = d4[0]; cs[i][1] = d4[1];
       cv[i][0] = d4[2]; cv[i][1] = d4[3];
@@ -320,7 +329,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       }
       L.lev[i] = r;
       if (pdone) {  // y[0:32) = v ^ s ^ t * cw_np1 (lib.rs:192)
-        const uint4* np4 = reinterpret_cast<const uint4*>(cw_np1 + key * lam);
+        const uint4* np4 = reinterpret_cast<const uint4*>(cw_np1 + (key + (MK ? L.kk[i] : 0u)) * lam);
         const uint4 n0 = np4[0], n1 = np4[1];
         const uint32_t nw[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
         const uint32_t tn = 0u - L.t[i];
@@ -341,8 +350,8 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
       if (__ballot(done))
-        wide_refill<NS, XREG>(L, i, done, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes, pf,
-                              tvec, tw);
+        wide_refill<NS, XREG, MK>(L, i, done, unext, uend, exhausted, ctr, nunits, count, s0p, party, xs, nbytes,
+                                  pf, tvec, tw, ppk, lam);
     }
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks), accumulated over passes

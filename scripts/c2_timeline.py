@@ -72,7 +72,7 @@ def main():
 
     out = {"c2_ms_per_step": ms, "one_eval_event_ms": one_ms,
            "build_entry_after_fill": dist(live(b_fill, 1)), "build_root_path_done": dist(live(b_root, 1)),
-           "build_bfs_done": dist(live(b_fill, 3)), "build_dfs_done_thread0": dist(live(b_root, 3)),
+           "build_bfs_done": dist(live(b_fill, 3)), "build_done_last_wave": dist(live(b_root, 3)),
            "walk_entry_after_fill": dist(live(walk, 1)), "walk_end_wave0": dist(live(walk, 3)),
            "note": "s_memrealtime stamps (100 MHz) of the last eval; ms relative to the first build "
                    "workgroup's stamp after its LDS table fill"}

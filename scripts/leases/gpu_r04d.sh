@@ -3,6 +3,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r04d2; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
 for v in t3g3 t3g4 t3g5; do
   DCF_HIP_LIB=$PWD/dcf_amd/libdcf_hip_$v.so timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "wide or c4" > $O/pytest_$v.log 2>&1 || { tail -40 $O/pytest_$v.log; exit 1; }
   echo "$v $(tail -1 $O/pytest_$v.log)"

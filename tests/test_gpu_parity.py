@@ -429,6 +429,34 @@ def test_wide_gen_batch_and_multikey(dcf):
         assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl]))
 
 
+@pytest.mark.parametrize("lam,nb,K,P", [(32, 2, 9, 5), (64, 3, 40, 17), (96, 2, 12, 33), (128, 16, 70, 64),
+                                         (256, 5, 300, 8), (128, 4, 3, 40000)])
+def test_wide_multikey_batched_vs_oracle(dcf, lam, nb, K, P):
+    """LAMBDA >= 32 multi-key eval: keys with <= 32768 points go through one batched head / tail
+    pass (per-point key, per-workgroup key tables; the 4-bit tail at LAMBDA = 96, the paired-slot
+    tail at 128 / 256); 40000 points per key takes the per-key path.  Both parties reconstruct."""
+    import torch
+    rng = np.random.default_rng(lam * 31 + K)
+    keys = [rng.bytes(32) for _ in range(18)]
+    prg, Po = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    alpha, beta, s0, s1 = (_rand(rng, (K, nb)), _rand(rng, (K, lam)), _rand(rng, (K, lam)), _rand(rng, (K, lam)))
+    T = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    cwb = d.gen_batch_device(T(alpha), T(beta), T(s0), T(s1), dcf.BoundState.LtBeta)
+    xs = _rand(rng, (K * P, nb))
+    xs[::P] = alpha
+    y0 = d.eval_multikey_device(False, cwb, T(s0), T(xs), P)
+    y1 = d.eval_multikey_device(True, cwb, T(s1), T(xs), P)
+    torch.cuda.synchronize()
+    y0h, y1h = y0.cpu().numpy(), y1.cpu().numpy()
+    for key in sorted(set([0, K - 1] + list(rng.integers(0, K, 4)))):
+        ok = O.gen(Po, alpha[key].tobytes(), beta[key].tobytes(), s0[key].tobytes(), s1[key].tobytes(), 0)
+        sl = slice(key * P, (key + 1) * P)
+        assert np.array_equal(y0h[sl], O.eval_(Po, 0, ok, s0[key].tobytes(), xs[sl], nthreads=8)), key
+        assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl], nthreads=8)), key
+    assert not (y0h[::P] ^ y1h[::P]).any()  # f(alpha) = 0 for every key
+
+
 @pytest.mark.parametrize("split,variant", [(0, 0), (6, 0), (12, 0), (1, 1), (8, 1), (15, 1), (16, 1)])
 def test_hybrid_splits_identical(dcf, split, variant):
     """Every T-table/bitsliced wave split of the hybrid engine returns the same bytes."""
