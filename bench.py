@@ -98,16 +98,20 @@ def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels:
     for e in (t if isinstance(t, list) else [t]):
         if (e.get("kernel"), e.get("points_per_launch"), e.get("n_bytes"), e.get("lambda"),
                 e.get("prefix_levels", 0)) == (kernel, points, n_bytes, lam, prefix_levels):
-            return e.get("traffic_bytes")
+            return e
     return None
 
 
 def traffic_fields(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels: int, alg_bytes: float):
     """(traffic, source): the PMC figure when profiles/ holds this launch shape, otherwise
     the algorithmic bytes, labelled as such (never null)."""
-    t = pmc_traffic(kernel, points, n_bytes, lam, prefix_levels)
-    if t is not None:
-        return t, "pmc: 2 x FETCH_SIZE + WRITE_SIZE per launch (profiles/pmc_traffic.json)"
+    e = pmc_traffic(kernel, points, n_bytes, lam, prefix_levels)
+    if e is not None and e.get("traffic_bytes") is not None:
+        src = f"pmc: 2 x FETCH_SIZE + WRITE_SIZE per launch ({e.get('source', '?')}, via profiles/pmc_traffic.json)"
+        if e.get("traffic_bytes_x1") is not None:
+            src += (f"; 1 x FETCH_SIZE + WRITE_SIZE = {e['traffic_bytes_x1'] / 1e9:.2f} GB (the x2 correction is for "
+                    f"wide streaming reads; 32-B row gathers are fetched as 64-B requests, so x1 may be the closer figure)")
+        return e["traffic_bytes"], src
     return alg_bytes, "algorithmic bytes (no PMC profile of this exact launch shape in profiles/pmc_traffic.json)"
 
 

@@ -1400,9 +1400,10 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     const uint64_t ppl = multi ? kpl * ppk : (1ull << 31);  // points per launch
     for (uint64_t c0 = 0; c0 < total; c0 += ppl) {
       const uint64_t cnt = std::min<uint64_t>(ppl, total - c0), k0 = multi ? c0 / ppk : 0, kc = multi ? cnt / ppk : 1;
-      // the table build counted its work units on the counter: each walk's counter starts at 0
-      // (the block count beside it keeps the per-key top trees' blocks)
-      HIP_TRY(hipMemsetAsync(w->d_ctr, 0, 8, st));
+      // each walk's work counter starts at 0 (the block count beside it keeps the per-key top
+      // trees' blocks): eval_launch zeroed it for the first launch (the table builds and the
+      // digest do not touch it), so a one-launch eval has no fill between the build and the walk
+      if (c0 > 0) HIP_TRY(hipMemsetAsync(w->d_ctr, 0, 8, st));
       const uint64_t units = (cnt + kStreamUnit - 1) / kStreamUnit;
       uint64_t blocks = (units + 15) / 16;
       if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;

@@ -103,6 +103,81 @@ __device__ __forceinline__ uint32_t aes256_col16(uint32_t st, const uint32_t (&r
   return x ^ rkA[14];
 }
 
+// One PRG call (prg.rs:42-73) on a 32-lane half-wave with k_eval16_row's layout: lane p of a
+// 16-lane row holds column a = p & 3 of the state; row 0 encrypts A = AES(s), row 1 B = AES(~s)
+// with aes256_col16, and v_permlane16_swap hands each row the other's block (rows 2 and 3 repeat
+// rows 0 and 1).  A level costs one 16-lane AES chain (~1234 cycles) instead of a lone lane's
+// T-table rounds.  Used where a few nodes are on the critical path: the root path and the first
+// levels of k_prefix_build16 (kernels16.h).
+struct RowPrg {
+  uint32_t rkA[15], rkB[15], selA, selB, selF, fmask, lc, a, inv, msk;
+  __device__ __forceinline__ void init(const RoundKeys& rk) {
+    const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, bq = p >> 2;
+    a = p & 3u;
+    lc = lane_const();
+#pragma unroll
+    for (int r = 0; r < 15; ++r) {
+      const uint32_t w0 = rk.w[4 * r], w1 = rk.w[4 * r + 1], w2 = rk.w[4 * r + 2], w3 = rk.w[4 * r + 3];
+      rkA[r] = (a & 2u) ? ((a & 1u) ? w3 : w2) : ((a & 1u) ? w1 : w0);
+      rkB[r] = (bq & 2u) ? ((bq & 1u) ? w3 : w2) : ((bq & 1u) ? w1 : w0);
+    }
+    const uint32_t kA = (a - bq) & 3u, kB = (bq - a) & 3u;
+    selA = col16_sel(kA, kA);
+    selB = col16_sel(kB, kB);
+    selF = col16_sel(kB, (kB + 2u) & 3u);
+    fmask = 0xFFu << (8u * kB);
+    inv = 0u - ((lane >> 4) & 1u);
+    msk = (a == 3u) ? kMaskLast : 0xFFFFFFFFu;
+  }
+  // Column a of both children of node (s, v, t) given column a of the level's CW (lib.rs:174-189):
+  // left s' = (A ^ s) & M ^ t cw.s, v' = v ^ (B ^ ~s) & M ^ t cw.v; right s' = s & M ^ t cw.s,
+  // v' = v ^ ~s & M ^ t cw.v; tl / tr from column 0, broadcast over each quad.
+  __device__ __forceinline__ void children(const uint32_t* lds, uint32_t s, uint32_t v, uint32_t t, uint32_t cs,
+                                           uint32_t cv, uint32_t ct, uint32_t& sl, uint32_t& vl, uint32_t& tl,
+                                           uint32_t& sr, uint32_t& vr, uint32_t& tr) const {
+    const uint32_t mine = aes256_col16(s ^ inv, rkA, rkB, lds, lc, selA, selB, selF, fmask);
+    const auto sw = __builtin_amdgcn_permlane16_swap(mine, mine, false, false);
+    const uint32_t A = sw[0], B = sw[1], tm = 0u - t;
+    sl = ((A ^ s) & msk) ^ (tm & cs);
+    vl = v ^ ((B ^ ~s) & msk) ^ (tm & cv);
+    sr = (s & msk) ^ (tm & cs);
+    vr = v ^ (~s & msk) ^ (tm & cv);
+    tl = dpp<kQpBcast0>(((A ^ s) & 1u) ^ (t & ct & 1u));          // lib.rs:179-180
+    tr = dpp<kQpBcast0>(((B ^ ~s) & 1u) ^ (t & (ct >> 1) & 1u));
+  }
+};
+
+// The root path of k_prefix_build16: the node of level S named by the bits of w (Msb-first), one
+// wave, RowPrg per level (C2's 8 levels took 24 us as lone-lane T-table rounds,
+// profiles/r04f_c2_timeline.json).  Returns the node (s, v, t) in every lane.
+__device__ __forceinline__ void row_root_path(const uint32_t* lds, const RowPrg& rp, const uint4* __restrict__ cw_s,
+                                              const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t,
+                                              const uint4 s0, const uint32_t party, const uint32_t S,
+                                              const uint32_t w, uint32_t (&rs)[4], uint32_t (&rv)[4], uint32_t& rt) {
+  const uint32_t a = rp.a;
+  const uint32_t s0w[4] = {s0.x, s0.y, s0.z, s0.w};
+  uint32_t s = s0w[0];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) s = (a == (uint32_t)k) ? s0w[k] : s;
+  uint32_t v = 0u, t = party;
+  for (uint32_t lev = 0; lev < S; ++lev) {
+    const uint32_t cs = reinterpret_cast<const uint32_t*>(cw_s + lev)[a];
+    const uint32_t cv = reinterpret_cast<const uint32_t*>(cw_v + lev)[a], ct = cw_t[lev];
+    uint32_t sl, vl, tl, sr, vr, tr;
+    rp.children(lds, s, v, t, cs, cv, ct, sl, vl, tl, sr, vr, tr);
+    const bool right = (w >> (S - 1u - lev)) & 1u;
+    s = right ? sr : sl;
+    v = right ? vr : vl;
+    t = right ? tr : tl;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    rs[k] = __builtin_amdgcn_readlane(s, k);
+    rv[k] = __builtin_amdgcn_readlane(v, k);
+  }
+  rt = __builtin_amdgcn_readlane(t, 0);
+}
+
 // The 128 KiB replicated T-tables (lds_fill_tables' layout), every load of a thread issued
 // before its stores: a latency kernel cannot afford 32 dependent load/store round trips.
 constexpr int kFillPer = kLdsWords / kBlock;
