@@ -29,7 +29,7 @@ ERRORS = {
 EXPORTS = [
     "dcf_version", "dcf_last_error", "dcf_hirose_prg_new", "dcf_mmo_prg_new", "dcf_prg_kind", "dcf_prg_free", "dcf_prg_lambda", "dcf_prg_set_eval_mode",
     "dcf_prg_set_hybrid_split", "dcf_prg_set_stream_hybrid", "dcf_prg_last_eval_blocks", "dcf_prg_set_prefix_levels", "dcf_eval_prefix_levels",
-    "dcf_cwb_bytes", "dcf_cwb_np1_offset", "dcf_gen", "dcf_eval", "dcf_prg_gen",
+    "dcf_eval_keys_per_launch", "dcf_cwb_bytes", "dcf_cwb_np1_offset", "dcf_gen", "dcf_eval", "dcf_prg_gen",
     "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device", "dcf_eval_full_domain_device",
     "dcf_share_bincode_bytes", "dcf_share_to_bincode", "dcf_share_from_bincode",
     "dcf_point_slice", "dcf_eval_multi_gpu", "dcf_eval_multi_gpu_device", "dcf_prg_set_prefix_max_bytes",
@@ -78,6 +78,7 @@ def load(path: str = LIB_PATH):
         "dcf_prg_last_eval_blocks": ([vp, ctypes.POINTER(ctypes.c_uint64)], i),
         "dcf_prg_set_prefix_levels": ([vp, i], i),
         "dcf_eval_prefix_levels": ([vp, sz, sz, sz], i),
+        "dcf_eval_keys_per_launch": ([sz, sz], sz),
         "dcf_cwb_bytes": ([sz, sz, sz], sz),
         "dcf_cwb_np1_offset": ([sz, sz, sz], sz),
         "dcf_gen": ([vp, sz, u8p, u8p, u8p, u8p, i, u8p], i),

@@ -118,8 +118,6 @@ struct Workspace {
   size_t slab_bytes = 0;
   uint8_t* d_pfx = nullptr;   // shared-prefix table + its build buffers / per-key top trees
   size_t pfx_bytes = 0;
-  uint8_t* d_rows = nullptr;  // single-key stream eval: 48-byte CW rows (k_cw_rows48)
-  size_t rows_bytes = 0;
   uint8_t* d_mkey = nullptr;  // dcf_eval_multi_gpu_device: this device's copy of the key (CWB + s0)
   size_t mkey_bytes = 0;
   // Host-pointer entry points: three non-blocking streams (copy-in, compute, copy-out), their
@@ -137,6 +135,10 @@ struct Workspace {
   // Ordering of the device work of successive leases (see above).
   hipEvent_t done = nullptr;
   hipStream_t done_stream = nullptr;
+  // Multi-key LAMBDA = 16 eval: a second stream for the per-key top trees, built while the
+  // key-major digest is written on the call's stream (fork / join events).
+  hipStream_t aux = nullptr;
+  hipEvent_t aux_ev[2] = {};
   bool pending = false;
   uint32_t host_streams = 0;  // hs[] the current host call queued work on (bit i = hs[i])
   // dcf_prg_set_phase_timing: events around the last eval's preparation and walk kernels.
@@ -867,15 +869,19 @@ int dcf_prg_kind(const dcf_prg* p) { return p ? p->kind : -1; }
 static void free_workspace(Workspace* w) {
   for (hipStream_t s : w->hs)  // host-path work still queued (an error return drains these too)
     if (s) (void)hipStreamSynchronize(s);
+  if (w->aux) (void)hipStreamSynchronize(w->aux);
   if (w->pending) (void)hipEventSynchronize(w->done);  // the last device call's kernels
   for (void* b : {(void*)w->d_ctr, (void*)w->d_ws, (void*)w->d_dig, (void*)w->d_kdig, w->d_slabs, (void*)w->d_pfx,
-                  (void*)w->d_rows, (void*)w->d_mkey, (void*)w->d_stage})
+                  (void*)w->d_mkey, (void*)w->d_stage})
     if (b) (void)hipFree(b);
   if (w->h_stage) (void)hipHostFree(w->h_stage);
   if (w->h_tiny) (void)hipHostFree(w->h_tiny);
   if (w->h_mid) (void)hipHostFree(w->h_mid);
   for (hipStream_t s : w->hs)
     if (s) (void)hipStreamDestroy(s);
+  if (w->aux) (void)hipStreamDestroy(w->aux);
+  for (hipEvent_t e : w->aux_ev)
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : w->hev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : w->tev)
@@ -954,7 +960,7 @@ size_t dcf_prg_device_bytes(const dcf_prg* p) {
   for (const Workspace* w : p->all_ws) {
     if (w->d_ctr) b += kCtrBytes;
     b += (size_t)w->dig_levels * 65 + w->kdig_bytes + w->ws_bytes + w->pfx_bytes + w->slab_bytes +
-         w->d_stage_bytes + w->mkey_bytes + w->rows_bytes;
+         w->d_stage_bytes + w->mkey_bytes;
   }
   return b;
 }
@@ -1189,6 +1195,11 @@ static uint64_t mk_keys_per_launch(size_t n_bytes, uint64_t ppk) {
   return std::max<uint64_t>(1, std::min<uint64_t>({1ull << 24, (1ull << 31) / ppk, (1ull << 30) / (8 * n_bytes)}));
 }
 
+size_t dcf_eval_keys_per_launch(size_t n_bytes, size_t points_per_key) {
+  if (n_bytes == 0 || points_per_key == 0) return 0;
+  return (size_t)mk_keys_per_launch(n_bytes, points_per_key);
+}
+
 static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party, const uint8_t* cwb,
                      const uint8_t* s0s, const uint8_t* xs, uint8_t* ys) {
   Workspace* w = L.w;
@@ -1349,14 +1360,6 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     if (multi && ppk >= (1ull << 31)) return fail(DCF_ERR_UNSUPPORTED, "multi-key stream eval: 2^31 points per key or more");
     const uint4* scs = cws;
     const uint8_t* sct = cwt;
-    if (multi) {  // key-major digest of the K keys (kernels_stream.h)
-      if (int rc = grow(&w->d_kdig, &w->kdig_bytes, (size_t)num_keys * n * 33, st)) return rc;
-      hipLaunchKernelGGL(k_cw_keymajor, dim3((unsigned)((num_keys + 15) / 16)), dim3(256), 0, st, cws, cwv, cwt,
-                         (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig, w->d_kdig + (size_t)num_keys * n * 32);
-      HIP_TRY(hipGetLastError());
-      scs = (const uint4*)w->d_kdig;
-      sct = w->d_kdig + (size_t)num_keys * n * 32;
-    }
     PrefixTable pf{nullptr, 0u};
     if (multi && c.prefix_levels != 0 && n > kMkPfxLevels && ppk >= 32 && num_keys <= (1ull << (31 - kMkPfxLevels))) {
       // per-key top trees (k_mk_prefix16: 32 rows per key); no room -> walk from the root (same bytes)
@@ -1375,14 +1378,37 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
         }
       }
       if (w->pfx_bytes >= need) {
-        hipLaunchKernelGGL(k_mk_prefix16<true>,
-                           dim3((unsigned)(((num_keys << kMkPfxRoot) + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           st, p->d_tab, p->rk[0], cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party,
-                           (uint64_t)num_keys, (uint4*)w->d_pfx, p->d_rk0, w->d_ctr);
-        HIP_TRY(hipGetLastError());
         pf = PrefixTable{(const uint4*)w->d_pfx, kMkPfxLevels};
         w->last_prefix = kMkPfxLevels;
       }
+    }
+    if (multi) {
+      // The top trees (k_mk_prefix16: LDS-bound AES, 128 KiB of LDS per workgroup) on the
+      // workspace's second stream while the key-major digest (kernels_stream.h: memory-bound,
+      // 17 KiB per workgroup, so one fits beside a top-tree workgroup on a CU) is written on the
+      // call's stream; the walk waits for both.
+      if (int rc = grow(&w->d_kdig, &w->kdig_bytes, (size_t)num_keys * n * 33, st)) return rc;
+      const bool fork = pf.levels != 0;
+      if (fork) {
+        if (!w->aux) HIP_TRY(hipStreamCreateWithFlags(&w->aux, hipStreamNonBlocking));
+        for (auto& e : w->aux_ev)
+          if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(w->aux_ev[0], st));
+        HIP_TRY(hipStreamWaitEvent(w->aux, w->aux_ev[0], 0));
+        hipLaunchKernelGGL(k_mk_prefix16<true>,
+                           dim3((unsigned)(((num_keys << kMkPfxRoot) + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           w->aux, p->d_tab, p->rk[0], cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party,
+                           (uint64_t)num_keys, (uint4*)w->d_pfx, p->d_rk0, w->d_ctr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(w->aux_ev[1], w->aux));
+      }
+      hipLaunchKernelGGL(k_cw_keymajor, dim3((unsigned)((num_keys + kKmKeys - 1) / kKmKeys), (unsigned)((n + kKmLevs - 1) / kKmLevs)),
+                         dim3(256), 0, st, cws, cwv, cwt, (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig,
+                         w->d_kdig + (size_t)num_keys * n * 32);
+      HIP_TRY(hipGetLastError());
+      if (fork) HIP_TRY(hipStreamWaitEvent(st, w->aux_ev[1], 0));
+      scs = (const uint4*)w->d_kdig;
+      sct = w->d_kdig + (size_t)num_keys * n * 32;
     }
     if (!multi) {
       const uint32_t d = prefix_depth(p, c, n_bytes, num_keys, total);

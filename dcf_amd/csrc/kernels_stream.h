@@ -207,34 +207,39 @@ __device__ __forceinline__ void stream_next_word(StreamLane<NS, XREG, MULTI>& L,
   }
 }
 
-// Key-major CW digest for the multi-key stream engine: one workgroup per 16 keys
-// stages their 8N levels through LDS so both the level-major reads (16 keys x 16 B
-// per row) and the key-major writes (4 KiB per key) are contiguous.
+// Key-major CW digest for the multi-key stream engine, tiled: a workgroup transposes 32 keys x
+// 16 levels through 17 KiB of LDS — per level 512 B contiguous reads of cw_s and of cw_v, per key
+// 512 B contiguous writes of dig and 16 B of dig_t.  Small enough to share a CU with a
+// k_mk_prefix16 workgroup (128 KiB), which runs beside it on a second stream.  A key's LDS row is
+// padded to 33 uint4 so the transposing writes spread over the banks.
+constexpr uint32_t kKmKeys = 32, kKmLevs = 16;
 __global__ __launch_bounds__(256) void k_cw_keymajor(const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
                                                      const uint8_t* __restrict__ cw_t, const uint32_t nlev,
                                                      const uint64_t num_keys, uint4* __restrict__ dig,
                                                      uint8_t* __restrict__ dig_t) {
-  __shared__ uint4 sh[16 * 256 * 2];  // [key][level][s|v], nlev <= 256
-  __shared__ uint8_t sht[16 * 256];
-  const uint64_t k0 = (uint64_t)blockIdx.x * 16;
-  const uint32_t nk = (uint32_t)min<uint64_t>(16, num_keys - k0);
-  for (uint32_t it = threadIdx.x; it < nlev * 16; it += blockDim.x) {
-    const uint32_t l = it >> 4, kk = it & 15u;
-    if (kk < nk) {
-      const uint64_t src = (uint64_t)l * num_keys + k0 + kk;
-      sh[(kk * 256 + l) * 2] = cw_s[src];
-      sh[(kk * 256 + l) * 2 + 1] = cw_v[src];
-      sht[kk * 256 + l] = cw_t[src];
+  constexpr uint32_t RW = 2 * kKmLevs + 1;  // uint4 per key row
+  __shared__ uint4 sh[kKmKeys * RW];
+  __shared__ uint8_t sht[kKmKeys * kKmLevs];
+  const uint64_t k0 = (uint64_t)blockIdx.x * kKmKeys;
+  const uint32_t l0 = blockIdx.y * kKmLevs;
+  const uint32_t nk = (uint32_t)min<uint64_t>(kKmKeys, num_keys - k0), nl = min(kKmLevs, nlev - l0);
+  for (uint32_t it = threadIdx.x; it < kKmKeys * kKmLevs; it += blockDim.x) {
+    const uint32_t l = it / kKmKeys, kk = it % kKmKeys;
+    if (kk < nk && l < nl) {
+      const uint64_t src = (uint64_t)(l0 + l) * num_keys + k0 + kk;
+      sh[kk * RW + 2 * l] = cw_s[src];
+      sh[kk * RW + 2 * l + 1] = cw_v[src];
+      sht[kk * kKmLevs + l] = cw_t[src];
     }
   }
   __syncthreads();
-  for (uint32_t it = threadIdx.x; it < nk * nlev * 2; it += blockDim.x) {
-    const uint32_t kk = it / (nlev * 2), r = it % (nlev * 2);
-    dig[(k0 + kk) * nlev * 2 + r] = sh[kk * 512 + r];
+  for (uint32_t it = threadIdx.x; it < kKmKeys * 2 * kKmLevs; it += blockDim.x) {
+    const uint32_t kk = it / (2 * kKmLevs), r = it % (2 * kKmLevs);
+    if (kk < nk && r < 2 * nl) dig[(k0 + kk) * nlev * 2 + 2 * l0 + r] = sh[kk * RW + r];
   }
-  for (uint32_t it = threadIdx.x; it < nk * nlev; it += blockDim.x) {
-    const uint32_t kk = it / nlev, l = it % nlev;
-    dig_t[(k0 + kk) * nlev + l] = sht[kk * 256 + l];
+  for (uint32_t it = threadIdx.x; it < kKmKeys * kKmLevs; it += blockDim.x) {
+    const uint32_t kk = it / kKmLevs, l = it % kKmLevs;
+    if (kk < nk && l < nl) dig_t[(k0 + kk) * nlev + l0 + l] = sht[kk * kKmLevs + l];
   }
 }
 

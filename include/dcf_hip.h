@@ -147,6 +147,11 @@ int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 int dcf_prg_set_prefix_levels(dcf_prg* prg, int levels);
 /* The prefix depth D a dcf_eval* call of this shape would use (0 = none). */
 int dcf_eval_prefix_levels(const dcf_prg* prg, size_t n_bytes, size_t num_keys, size_t points_per_key);
+/* Keys per kernel launch of a LAMBDA = 16 multi-key stream eval (dcf_eval_multikey_device and
+ * the host entry points with several keys): min(2^24, 2^31 / points_per_key, 2^30 / 8N), at
+ * least 1 — the engine's point, work and CW-digest-row indices are 32-bit, so a larger call runs
+ * as consecutive launches over whole keys.  Pure arithmetic (no device access). */
+size_t dcf_eval_keys_per_launch(size_t n_bytes, size_t points_per_key);
 /* Cap on the device memory the AUTOMATIC prefix depth may allocate (table + build
  * buffers, which stay resident on the prg until it is freed): the auto depth is lowered
  * until they fit, and no table is built below depth 8.  0 = no cap (the default: up to

@@ -31,6 +31,7 @@ extern "C" {
     pub fn dcf_prg_set_eval_mode(prg: *mut DcfPrg, mode: c_int) -> c_int;
     pub fn dcf_prg_set_prefix_levels(prg: *mut DcfPrg, levels: c_int) -> c_int;
     pub fn dcf_eval_prefix_levels(prg: *const DcfPrg, n_bytes: usize, num_keys: usize, points_per_key: usize) -> c_int;
+    pub fn dcf_eval_keys_per_launch(n_bytes: usize, points_per_key: usize) -> usize;
     pub fn dcf_prg_set_prefix_max_bytes(prg: *mut DcfPrg, max_bytes: usize) -> c_int;
     pub fn dcf_prg_device_bytes(prg: *const DcfPrg) -> usize;
     pub fn dcf_prg_host_pinned_bytes(prg: *const DcfPrg) -> usize;

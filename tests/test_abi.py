@@ -54,6 +54,21 @@ def test_version_and_layout_helpers(hip_lib):
     assert hip_lib.dcf_cwb_bytes(16, 16, 1) == 4240
 
 
+def test_multikey_launch_split_keeps_indices_32_bit(hip_lib):
+    """the multi-key stream engine's point, work-unit and CW-digest-row indices are
+    32-bit (kernels_stream.h StreamLane::ci / pt), so each launch holds at most
+    min(2^24, 2^31 / P, 2^30 / 8N) keys: 2 * (key * 8N + level + 1) and key * P stay below 2^31."""
+    assert hip_lib.dcf_eval_keys_per_launch(0, 64) == 0 and hip_lib.dcf_eval_keys_per_launch(16, 0) == 0
+    for nb in (1, 4, 16, 17, 32, 64, 159):
+        for ppk in (1, 32, 64, 255, 256, 4096, 1 << 20, 1 << 30, (1 << 31) + 5):
+            kpl = hip_lib.dcf_eval_keys_per_launch(nb, ppk)
+            n = 8 * nb
+            assert kpl == max(1, min(1 << 24, (1 << 31) // ppk, (1 << 30) // n)), (nb, ppk)
+            if kpl > 1:
+                assert 2 * (kpl * n) <= 1 << 31 and kpl * ppk <= 1 << 31
+    assert hip_lib.dcf_eval_keys_per_launch(32, 1) == (1 << 30) // 256  # N = 32: 4 Mi keys, not 2^24
+
+
 def test_argument_validation_without_gpu(hip_lib):
     h = ctypes.c_void_p()
     keys = b"\x00" * (32 * 18)

@@ -182,6 +182,41 @@ def test_host_call_after_device_call_without_sync(dcf):
     assert np.array_equal(yb[:500], O.eval_(P, 1, kbo, kb.s0s[1], xh[:500], nthreads=CPU_THREADS))
 
 
+def test_multikey_back_to_back_streams(dcf):
+    """Multi-key evals queued on two streams with no synchronization between them: the second call
+    reuses the first's workspace (LIFO pool), whose per-key top trees it rebuilds on the workspace's
+    second stream — that build must wait for the first call's walk (fork / join events)."""
+    import torch
+    rng = np.random.default_rng(41)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
+    d = dcf.DcfImpl(16, 16, prg)
+    K, Pp = 3000, 64
+    sets = []
+    for j in range(2):
+        alpha, beta, s0, s1 = (rng.integers(0, 256, (K, w), dtype=np.uint8) for w in (16, 16, 16, 16))
+        cwb = d.gen_batch_device(_T(alpha.tobytes()).view(K, 16), _T(beta.tobytes()).view(K, 16),
+                                 _T(s0.tobytes()).view(K, 16), _T(s1.tobytes()).view(K, 16), dcf.BoundState(j))
+        xs = torch.from_numpy(rng.integers(0, 256, (K * Pp, 16), dtype=np.uint8)).cuda()
+        sets.append((alpha, beta, s0, s1, cwb, xs))
+    refs = []
+    for alpha, beta, s0, s1, cwb, xs in sets:
+        refs.append(d.eval_multikey_device(False, cwb, _T(s0.tobytes()).view(K, 16), xs, Pp))
+        torch.cuda.synchronize()
+    got = []
+    for (alpha, beta, s0, s1, cwb, xs), st in zip(sets, (torch.cuda.Stream(), torch.cuda.Stream())):
+        with torch.cuda.stream(st):
+            got.append(d.eval_multikey_device(False, cwb, _T(s0.tobytes()).view(K, 16), xs, Pp))
+    torch.cuda.synchronize()
+    for j, (alpha, beta, s0, s1, cwb, xs) in enumerate(sets):
+        assert torch.equal(got[j], refs[j]), j
+        for key in (0, K // 2, K - 1):
+            ok = O.gen(P, alpha[key].tobytes(), beta[key].tobytes(), s0[key].tobytes(), s1[key].tobytes(), j)
+            sl = slice(key * Pp, (key + 1) * Pp)
+            want = O.eval_(P, 0, ok, s0[key].tobytes(), xs[sl].cpu().numpy())
+            assert np.array_equal(refs[j][sl].cpu().numpy(), want), (j, key)
+
+
 def test_phase_timing(dcf):
     import torch
     rng = np.random.default_rng(3)
