@@ -651,7 +651,7 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
 // ppk <= kWideBatchPpk (larger keys amortise their own launches: eval_wide per key).  No shared
 // prefix; the lockstep head (DCF_EVAL_TTABLE) and the MMO PRG keep the per-key path.
 constexpr uint64_t kWideBatchPpk = 32768;
-constexpr uint64_t kWideBatchKeys = 8192;  // keys per pass: tail grid rows (keys x ranges) < 65536
+constexpr uint64_t kWideBatchKeys = 4096;  // keys per pass: tail grid rows (keys x <= 8 ranges) <= 32768
 int eval_wide_batch(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t ppk, int party,
                     const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nlev = (uint32_t)(8 * n_bytes);
