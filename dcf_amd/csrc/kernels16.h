@@ -436,7 +436,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
   const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
   const uint32_t npw[4] = {np.x, np.y, np.z, np.w};
   const bool last = lev + 1 == nlev;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint32_t unit = fd_unit(nparents);
   for (uint64_t base = next_unit_base_n(ctr, ~0ull, unit); base < nparents;
        base = next_unit_base_n(ctr, base, unit)) {

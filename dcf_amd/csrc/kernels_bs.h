@@ -366,7 +366,6 @@ __global__ __launch_bounds__((MEM ? 16 : kHybridWaves) * 64) void k_eval16_hybri
     const uint4* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
     const uint64_t m, const uint32_t n_tt, uint32_t* __restrict__ ctr, uint4* __restrict__ slabs,
     const uint4* __restrict__ km, uint4* __restrict__ ys) {
-  constexpr int kWaves = MEM ? 16 : kHybridWaves;
   constexpr int kXlSlots = MEM ? 15 : kHybridWaves;  // LDS budget: 128 KiB tables + 2 KiB per bitsliced wave
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint32_t xl_all[kXlSlots][32 * 16];

@@ -37,7 +37,7 @@ __device__ __forceinline__ void bs_eval_batch_pf(const uint4* __restrict__ km, c
                                                  const PrefixTable& pf) {
   const uint32_t lane = threadIdx.x & 63u, c = lane & 3u, quad = lane >> 2;
   const uint64_t p0 = p_base + (uint64_t)quad * kBsPoints;
-  const uint32_t nlev = 8u * nbytes, nchunk = nbytes >> 2, D = pf.levels;
+  const uint32_t nchunk = nbytes >> 2, D = pf.levels;
   const uint4* __restrict__ kmc = km + 8 * c;
   uint4* __restrict__ vp = slab + lane;
   uint4* __restrict__ sp = slab + 512 + lane;
