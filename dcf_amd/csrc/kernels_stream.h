@@ -122,31 +122,19 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
 
 // Give every lane whose stream i is free (`mine`) a new point, or retire the
 // stream when the counter is exhausted.  Called in wave-uniform control flow.
-#ifndef DCF_XPF
-#define DCF_XPF 1
-#endif
-// XPF (single key, 4-byte x, x in registers: C2's instance): a wave loads the x words of a whole
-// unit when it claims it (one coalesced load per lane per 64 points, ux[k] = x of point
-// ubase + 64 k + lane), and a refill hands each new point its word by ds_bpermute — so a point's
-// start waits only for its table-row gather, not for an x load followed by the gather.
-template <int NBC>
-constexpr bool kStreamXpf = DCF_XPF && NBC == 4 && kStreamUnit == 256;
-
 template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit, bool PFX = false, int NBC = 0>
 __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint32_t& unext,
                                               uint32_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
                                               uint32_t nunits, uint32_t total, const uint4* __restrict__ s0s,
                                               const uint4 s0v, uint32_t party, const uint8_t* __restrict__ xs,
-                                              uint32_t nbytes, uint64_t ppk, const PrefixTable& pf,
-                                              uint32_t (&ux)[4], uint32_t& ubase) {
+                                              uint32_t nbytes, uint64_t ppk, const PrefixTable& pf) {
   // Single key, x width fixed: the loop only hands out point indices and the stream state is
   // written once after it, so it is not a loop-carried value (no copies of it per pass; the
   // multi-key and runtime-width instances spill VGPRs that way and start streams in the loop).
   uint64_t need = __ballot(mine);
   constexpr bool ONCE = !MULTI && NBC != 0;
-  constexpr bool XPF = ONCE && XREG && UNIT == 256 && kStreamXpf<NBC>;
   if (ONCE) {
-    uint32_t pnew = 0, px = 0;
+    uint32_t pnew = 0;
     bool got = false;
     while (need) {
       if (unext >= uend && !exhausted) {
@@ -156,29 +144,12 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
         } else {
           unext = u * UNIT;
           uend = min(unext + UNIT, total);
-          if (XPF) {  // the unit's x words (clamped past the end)
-            const uint32_t* xw = reinterpret_cast<const uint32_t*>(xs);
-            const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) ux[k] = xw[min(unext + 64u * k + lane, total - 1u)];
-            ubase = unext;
-          }
         }
       }
       if (exhausted && unext >= uend) break;
       const uint32_t rank = lane_rank(need);
       const bool take = mine && rank < uend - unext;
       pnew = take ? unext + rank : pnew;
-      if (XPF) {  // point unext + rank's word: lane (idx & 63) of ux[idx >> 6], idx >> 6 in {k0, k0 + 1}
-        const uint32_t off = unext - ubase, k0 = off >> 6, idx = off + rank;
-        const uint32_t k1 = min(k0 + 1u, 3u);
-        const uint32_t a0 = k0 == 0u ? ux[0] : (k0 == 1u ? ux[1] : (k0 == 2u ? ux[2] : ux[3]));
-        const uint32_t a1 = k1 == 1u ? ux[1] : (k1 == 2u ? ux[2] : ux[3]);
-        const uint32_t src = (idx & 63u) << 2;
-        const uint32_t v0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)a0);
-        const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)a1);
-        px = take ? ((idx >> 6) == k0 ? v0 : v1) : px;
-      }
       got = got || take;
       const uint64_t taken = __ballot(take);
       unext += (uint32_t)__popcll(taken);
@@ -186,12 +157,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
       mine = mine && !take;
     }
     if (got) {
-      if (XPF) {
-        L.xw[i][0] = px;
-        stream_start<NS, XREG, MULTI, PFX, NBC, true>(L, i, pnew, s0s, s0v, party, xs, nbytes, ppk, pf);
-      } else {
-        stream_start<NS, XREG, MULTI, PFX, NBC>(L, i, pnew, s0s, s0v, party, xs, nbytes, ppk, pf);
-      }
+      stream_start<NS, XREG, MULTI, PFX, NBC>(L, i, pnew, s0s, s0v, party, xs, nbytes, ppk, pf);
     } else if (mine) {  // nothing left: the stream retires
       L.alive[i] = false;
       L.ci[i] = 0;  // keep the idle stream's CW loads in bounds
@@ -297,7 +263,6 @@ __device__ __forceinline__ void stream_run(
   bool exhausted = false;
   const uint4 s0v = s0s[0];
   StreamLane<NS, XREG, MULTI> L;
-  uint32_t ux[4] = {0u, 0u, 0u, 0u}, ubase = 0u;  // XPF: the current unit's x words (stream_refill)
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     L.fresh[i] = false;
@@ -310,7 +275,7 @@ __device__ __forceinline__ void stream_run(
 #pragma unroll
   for (int i = 0; i < NS; ++i)
     stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, true, unext, uend, exhausted, ctr, nunits, total32, s0s,
-                                                  s0v, party, xs, nbytes, ppk, pf, ux, ubase);
+                                                  s0v, party, xs, nbytes, ppk, pf);
 
   uint64_t nblk = 0;  // AES blocks this wave encrypts for live streams (wave-uniform)
   for (;;) {
@@ -464,7 +429,7 @@ __device__ __forceinline__ void stream_run(
       }
       if (__ballot(done))
         stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total32, s0s,
-                                                  s0v, party, xs, nbytes, ppk, pf, ux, ubase);
+                                                  s0v, party, xs, nbytes, ppk, pf);
     }
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
