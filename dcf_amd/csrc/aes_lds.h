@@ -198,9 +198,13 @@ __device__ __forceinline__ uint4 lds_load16(uint32_t a) {
 // NB independent AES-NR encryptions, each under the round keys at LDS byte address ka[b]
 // (+16 per round: the offset rides in the ds_read_b128 immediate, no address VALU).
 // PRE: the caller has XORed round key 0 into st already (into its own input XOR).
-template <int NR, int NB, bool PRE>
+// KR > 0: rounds 1 .. KR - 1 take their key from registers instead (rkr[r][c][j]: word j of round r
+// of cipher c, c = 1 where the lane's mask hm[b] is all ones), one 3-input pick per word instead of
+// a ds_read_b128 (round 0 is the caller's, PRE).
+template <int NR, int NB, bool PRE, int KR = 0>
 __device__ __forceinline__ void aes_tt_lka(uint32_t (&st)[NB][4], const uint32_t (&ka)[NB], const uint32_t* lds,
-                                           uint32_t lc) {
+                                           uint32_t lc, const uint32_t (*rkr)[2][4] = nullptr,
+                                           const uint32_t* hm = nullptr) {
   if (!PRE) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -213,8 +217,14 @@ __device__ __forceinline__ void aes_tt_lka(uint32_t (&st)[NB][4], const uint32_t
     uint32_t o[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const uint4 k = lds_load16(ka[b] + 16u * r);
-      const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+      uint32_t kw[4];
+      if (r < KR) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kw[j] = __builtin_amdgcn_bitop3_b32(hm[b], rkr[r][1][j], rkr[r][0][j], 0xCA);
+      } else {
+        const uint4 k = lds_load16(ka[b] + 16u * r);
+        kw[0] = k.x; kw[1] = k.y; kw[2] = k.z; kw[3] = k.w;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (r < NR) {

@@ -181,6 +181,20 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   lds_fill_tables(lds, tab);  // its barrier also publishes rks
   DCF_CLK(1, 0);
   const uint32_t rks_a = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)rks;  // LDS byte address
+  // Rounds 0 .. KR - 1 of both schedules in registers (32 VGPRs, lane-picked per block: one
+  // 3-input pick per word), the rest read per lane from LDS.  C4 A/B r04j (2 runs each, same box):
+  // KR = 4 33.99-34.15 ms vs 34.24-34.36 with every key from LDS, KR = 2 no change, KR = 6 spills.
+  constexpr int KR = 4;
+  uint32_t rkr[KR > 0 ? KR : 1][2][4];
+#pragma unroll
+  for (int r = 0; r < KR; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint4 k = rk2[c * 15 + r];
+      rkr[r][c][0] = k.x; rkr[r][c][1] = k.y; rkr[r][c][2] = k.z; rkr[r][c][3] = k.w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(rkr[r][c][j]));
+    }
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
   const uint64_t nunits = (count + kWideUnit - 1) / kWideUnit;
@@ -228,7 +242,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     // Block of this step: B (ph 0), then A (ph 1, left) or D (ph 1, right), C (ph 2).  The
     // lane's 16-byte half (sel) stays live: d = E(sel ^ inv) ^ sel ^ inv is one 3-input XOR.
     uint32_t st[NS][4], sel[NS][4], inv[NS];
-    uint32_t ka[NS];
+    uint32_t ka[NS], hmk[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const uint32_t xb = L.cur[i] >> 31, ph = L.ph[i];
@@ -240,16 +254,23 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       uint32_t kb = rks_a + 368u * hi;
       asm volatile("" : "+v"(kb));
       ka[i] = kb & 0x3FFFFu;
-      const uint4 k0 = lds_load16(ka[i]);
       const uint32_t hm = 0u - hi;
-      const uint32_t k0w[4] = {k0.x, k0.y, k0.z, k0.w};
+      hmk[i] = hm;
+      uint32_t k0w[4];
+      if (KR > 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k0w[j] = pick(hm, rkr[0][1][j], rkr[0][0][j]);
+      } else {
+        const uint4 k0 = lds_load16(ka[i]);
+        k0w[0] = k0.x; k0w[1] = k0.y; k0w[2] = k0.z; k0w[3] = k0.w;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         sel[i][j] = pick(hm, L.s[i][4 + j], L.s[i][j]);
         st[i][j] = xor3(sel[i][j], inv[i], k0w[j]);  // round key 0 folded in
       }
     }
-    aes_tt_lka<14, NS, true>(st, ka, lds, lc);
+    aes_tt_lka<14, NS, true, KR>(st, ka, lds, lc, rkr, hmk);
 #pragma unroll
     for (int i = 0; i < NS; ++i)
       asm volatile("" : "+v"(cs[i][0].x), "+v"(cs[i][0].y), "+v"(cs[i][0].z), "+v"(cs[i][0].w), "+v"(cs[i][1].x),
