@@ -165,7 +165,7 @@ __global__ void k_cw_digest(const uint8_t* __restrict__ cw_s, const uint8_t* __r
 // Key `key` of a num_keys-key CWB; count <= 2^22 points per launch.  MK (batched keys): the
 // launch's points are keys key .. key + count / ppk - 1, ppk points each (point p: key p / ppk),
 // dig / dig_t / s0p hold those keys back to back, no shared prefix.
-template <int NS, bool MASK_HEAD, bool XREG, bool MK, int WG = kBlock>
+template <int NS, bool MASK_HEAD, bool XREG, bool MK, int WG = kBlock, int KR = 4>
 __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
     const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
     const uint8_t* __restrict__ dig_t, const uint8_t* __restrict__ cw_np1,
@@ -181,10 +181,11 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   lds_fill_tables(lds, tab);  // its barrier also publishes rks
   DCF_CLK(1, 0);
   const uint32_t rks_a = (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)rks;  // LDS byte address
-  // Rounds 0 .. KR - 1 of both schedules in registers (32 VGPRs, lane-picked per block: one
-  // 3-input pick per word), the rest read per lane from LDS.  C4 A/B r04j (2 runs each, same box):
-  // KR = 4 33.99-34.15 ms vs 34.24-34.36 with every key from LDS, KR = 2 no change, KR = 6 spills.
-  constexpr int KR = 4;
+  // Rounds 0 .. KR - 1 of both schedules in registers (8 VGPRs per round, lane-picked per block:
+  // one 3-input pick per word), the rest read per lane from LDS.  C4 A/B r04j (2 runs each, same
+  // box): KR = 4 33.99-34.15 ms vs 34.24-34.36 with every key from LDS, KR = 2 no change, KR = 6
+  // spills.  More rounds at 8 waves per CU (512-thread workgroups, 2 streams per lane, up to all
+  // 15 rounds in registers) ran 36.4-37.7 vs 31.8-32.0 ms (r04l): the head needs the 16 waves.
   uint32_t rkr[KR > 0 ? KR : 1][2][4];
 #pragma unroll
   for (int r = 0; r < KR; ++r)
