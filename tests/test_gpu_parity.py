@@ -430,12 +430,14 @@ def test_wide_gen_batch_and_multikey(dcf):
 
 
 @pytest.mark.parametrize("lam,nb,K,P", [(32, 2, 9, 5), (64, 3, 40, 17), (96, 2, 12, 33), (128, 16, 70, 64),
-                                         (256, 5, 300, 8), (128, 40, 20, 30), (96, 3, 4, 9000), (128, 4, 3, 40000)])
+                                         (256, 5, 300, 8), (128, 40, 20, 30), (96, 3, 4, 9000), (32, 2, 5000, 8),
+                                         (128, 4, 3, 40000)])
 def test_wide_multikey_batched_vs_oracle(dcf, lam, nb, K, P):
-    """LAMBDA >= 32 multi-key eval: keys with <= 32768 points go through one batched head / tail
-    pass (per-point key, per-workgroup key tables; the 4-bit tail at LAMBDA = 96 — with 9000 points
-    per key, three tail ranges per key — and at N = 40, the paired-slot tail at 128 / 256); 40000
-    points per key takes the per-key path.  Both parties reconstruct."""
+    """LAMBDA >= 32 multi-key eval: keys with <= 32768 points go through batched head / tail
+    passes of up to 4096 keys (per-point key, per-workgroup key tables; the 4-bit tail at
+    LAMBDA = 96 — with 9000 points per key, three tail ranges per key — and at N = 40, the
+    paired-slot tail at 128 / 256; 5000 keys take two passes); 40000 points per key takes the
+    per-key path.  Both parties reconstruct."""
     import torch
     rng = np.random.default_rng(lam * 31 + K)
     keys = [rng.bytes(32) for _ in range(18)]
