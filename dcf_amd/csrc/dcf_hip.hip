@@ -250,7 +250,11 @@ struct Lease {
 
 constexpr int kPrefixNoMem = -100;            // build_prefix: table allocation failed (internal)
 constexpr uint64_t kWideChunk = 1ull << 22;   // points per head/tail pass (t-vector scratch 256 MiB at N <= 31)
-constexpr size_t kWideMaxN = 159;             // LAMBDA >= 32 eval: N <= 159 (see eval_wide)
+// Points per LAMBDA >= 32 head/tail pass for t-vectors of tw words: kWideChunk up to N = 31 (16
+// words), fewer for longer t-sequences so the scratch stays ~256 MiB.
+uint64_t wide_chunk_points(uint32_t tw) {
+  return std::max<uint64_t>(65536, kWideChunk * 16 / std::max<uint32_t>(tw, 16u));
+}
 constexpr uint64_t kGenChunk = 4096;          // keys per wide-gen launch (scratch 3*LAMBDA per key)
 constexpr uint32_t kTailPts = 4096;          // points per tail workgroup (one table build each)
 
@@ -495,14 +499,14 @@ int try_prefix(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, int party
 
 // Tails over cnt points of cnt / ppk consecutive keys key, key + 1, ... (ppk points each, s0: their
 // s0s back to back; one key: ppk = cnt); grid rows = keys x ranges per key.
-template <int TW, int NCH = 0>
+template <int TW, int NCH = 0, bool ACC = false>
 int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
                 uint32_t lam, uint64_t K, uint64_t key, const uint32_t* tvec, uint64_t cnt, uint8_t* ys,
-                hipStream_t st, uint64_t ppk) {
+                hipStream_t st, uint64_t ppk, uint32_t c0 = 0, uint32_t ncp = 0) {
   static_assert(TW == 32 || TW == 64 || TW == 128 || TW == 256, "tile width");
-  const uint32_t nch = (nlev + 1 + 3) / 4;
-  const size_t lds = (size_t)nch * 16 * TW;
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail<TW, NCH>),
+  if (ncp == 0) ncp = (nlev + 1 + 3) / 4;
+  const size_t lds = (size_t)ncp * 16 * TW;
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail<TW, NCH, ACC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // Points per workgroup: each workgroup builds its tile's tables once, then streams its
   // kTailPts points (r02i A/B on C4: 41.1-41.3 ms vs 41.7-42.3 with ranges sized to 1, 2 or 4
@@ -510,9 +514,26 @@ int launch_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, cons
   const uint64_t tiles = (lam + TW - 1) / TW;
   const uint64_t rpk = (ppk + kTailPts - 1) / kTailPts;
   const dim3 grid((unsigned)tiles, (unsigned)((cnt / ppk) * rpk));
-  hipLaunchKernelGGL((k_eval_wide_tail<TW, NCH>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key, tvec,
-                     cnt, kTailPts, ys, t_words(nlev), ppk, (uint32_t)rpk);
+  hipLaunchKernelGGL((k_eval_wide_tail<TW, NCH, ACC>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K,
+                     key, tvec, cnt, kTailPts, ys, t_words(nlev), ppk, (uint32_t)rpk, c0, ncp);
   HIP_TRY(hipGetLastError());
+  return DCF_OK;
+}
+
+// More chunks than one 32-byte-tile table set holds (N >= 160): passes of kTailPassChunks chunks,
+// each after the first adding its rows' share to the y the previous pass wrote.
+constexpr uint32_t kTailPassChunks = 320;  // 320 x 16 entries x 32 B = 160 KiB
+int launch_tail_passes(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
+                       uint32_t lam, uint64_t K, uint64_t key, const uint32_t* tvec, uint64_t cnt, uint8_t* ys,
+                       hipStream_t st, uint64_t ppk) {
+  const uint32_t nch = (nlev + 1 + 3) / 4;
+  for (uint32_t c0 = 0; c0 < nch; c0 += kTailPassChunks) {
+    const uint32_t ncp = std::min(kTailPassChunks, nch - c0);
+    const int rc = c0 == 0 ? launch_tail<32>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk, 0, ncp)
+                           : launch_tail<32, 0, true>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk,
+                                                      c0, ncp);
+    if (rc) return rc;
+  }
   return DCF_OK;
 }
 
@@ -570,7 +591,8 @@ int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const u
   if (nch <= 40) return launch_tail<256>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
   if (nch <= 80) return launch_tail<128>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
   if (nch <= 160) return launch_tail<64>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
-  return launch_tail<32>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
+  if (nch <= kTailPassChunks) return launch_tail<32>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
+  return launch_tail_passes(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, ppk);
 }
 
 // Dcf::eval at LAMBDA >= 32 for key `key` of a K-key CWB (see kernels_wide.h).
@@ -578,16 +600,15 @@ int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const u
 int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
               const uint8_t* s0, const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nlev = (uint32_t)(8 * n_bytes);
-  // the 4-bit tail's tables: (8N + 1) / 4 chunks x 16 entries x 32-byte tiles <= 160 KiB
-  if (n_bytes > kWideMaxN) return fail(DCF_ERR_UNSUPPORTED, "LAMBDA >= 32 eval supports N <= 159");
   const size_t n = 8 * n_bytes;
   const uint8_t* cws = cwb;
   const uint8_t* cwv = cwb + n * K * lam;
   const uint8_t* cwt = cwb + 2 * n * K * lam;
   const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
-  const uint64_t chunk = m < kWideChunk ? m : kWideChunk;
   const uint32_t tw = t_words(nlev);  // t-vector words per point
-  const size_t tvb = (chunk * tw * 4 + 255) & ~(size_t)255;
+  const uint64_t chunk = std::min<uint64_t>(m, wide_chunk_points(tw));
+  // + 256 B: a multi-pass tail's t loads run up to 64 B past the last row (never used)
+  const size_t tvb = ((chunk * tw * 4 + 255) & ~(size_t)255) + 256;
   int rc = ensure_ws(w, tvb, st);
   if (rc) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
@@ -655,15 +676,14 @@ constexpr uint64_t kWideBatchKeys = 4096;  // keys per pass: tail grid rows (key
 int eval_wide_batch(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t ppk, int party,
                     const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nlev = (uint32_t)(8 * n_bytes);
-  if (n_bytes > kWideMaxN) return fail(DCF_ERR_UNSUPPORTED, "LAMBDA >= 32 eval supports N <= 159");
   const size_t n = 8 * n_bytes;
   const uint8_t* cws = cwb;
   const uint8_t* cwv = cwb + n * K * lam;
   const uint8_t* cwt = cwb + 2 * n * K * lam;
   const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
-  const uint64_t kp = std::max<uint64_t>(1, std::min<uint64_t>({K, kWideChunk / ppk, kWideBatchKeys}));
   const uint32_t tw = t_words(nlev);
-  const size_t tvb = (kp * ppk * tw * 4 + 255) & ~(size_t)255;
+  const uint64_t kp = std::max<uint64_t>(1, std::min<uint64_t>({K, wide_chunk_points(tw) / ppk, kWideBatchKeys}));
+  const size_t tvb = ((kp * ppk * tw * 4 + 255) & ~(size_t)255) + 256;
   if (int rc = ensure_ws(w, tvb, st)) return rc;
   if (w->dig_levels < kp * nlev) {
     size_t have = (size_t)w->dig_levels * 65;
@@ -709,14 +729,14 @@ int eval_wide_batch(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64
 int eval_mmo_wide(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t key, int party, const uint8_t* cwb,
                   const uint8_t* s0, const uint8_t* xs, uint64_t m, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nb = lam / 16u;
-  if (n_bytes > 31) return fail(DCF_ERR_UNSUPPORTED, "MMO eval at LAMBDA >= 32 supports N <= 31");
   const size_t n = 8 * n_bytes;
   const uint8_t* cws = cwb;
   const uint8_t* cwv = cwb + n * K * lam;
   const uint8_t* cwt = cwb + 2 * n * K * lam;
   const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
-  const uint64_t chunk = m < kWideChunk ? m : kWideChunk;
-  if (int rc = ensure_ws(w, chunk * kMmoTWords * 4, st)) return rc;
+  const uint32_t tw = mmo_t_words((uint32_t)n);
+  const uint64_t chunk = std::min<uint64_t>(m, wide_chunk_points(2 * tw));
+  if (int rc = ensure_ws(w, chunk * tw * 4, st)) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = std::min<uint64_t>(chunk, m - off);
@@ -927,7 +947,7 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   const bool small = total < (uint64_t)p->cus * kBlock * 2;
   if (p->kind == 1 && p->lambda > 16) return 0;  // MMO at LAMBDA >= 32: no shared prefix (head/tail per block)
   if (p->kind == 1) return small && c.prefix_levels < 0 ? 0 : (int)prefix_depth(p, c, n_bytes, num_keys, total);
-  if (p->lambda > 16) return n_bytes > kWideMaxN ? 0 : (int)wide_prefix_depth(p, c, n_bytes, points_per_key);
+  if (p->lambda > 16) return (int)wide_prefix_depth(p, c, n_bytes, points_per_key);
   if (c.mode == DCF_EVAL_AUTO && small) return num_keys == 1 ? (int)small_prefix_depth(p, c, n_bytes) : 0;
   if (c.mode != DCF_EVAL_AUTO && c.mode != DCF_EVAL_STREAM && c.mode != DCF_EVAL_STREAM_HYBRID) return 0;
   return (int)prefix_depth(p, c, n_bytes, num_keys, total);

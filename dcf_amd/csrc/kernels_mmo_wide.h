@@ -24,7 +24,8 @@
 
 namespace {
 
-constexpr uint32_t kMmoTWords = 8;  // t-vector words per point (t_0..t_n, n = 8N <= 248)
+// t-vector words per point: t_0 .. t_n (n = 8N) at bit r & 31 of word r >> 5
+__host__ __device__ constexpr uint32_t mmo_t_words(uint32_t nlev) { return (nlev + 32u) / 32u; }
 
 __device__ __forceinline__ uint32_t mmo_xbit(const uint8_t* __restrict__ x, uint32_t lev) {
   return (x[lev >> 3] >> (7u - (lev & 7u))) & 1u;  // Msb0 (lib.rs:181)
@@ -44,6 +45,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mmo_wide_eval(
   lds_fill_tables(lds, tab);
   const uint32_t lc = lane_const();
   const uint32_t nb = lam / 16u, nlev = 8u * nbytes, lane = threadIdx.x & 63u;
+  const uint32_t twn = mmo_t_words(nlev);
   const uint64_t groups = (count + 63) / 64;
   const uint64_t jn = HEAD ? 1 : nb - 1;  // blocks per point group handled by this kernel
   const uint64_t items = groups * jn;
@@ -59,7 +61,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mmo_wide_eval(
     uint32_t s[4] = {sv.x, sv.y, sv.z, sv.w}, v[4] = {0u, 0u, 0u, 0u};
     // t-vector word of bits 32w..32w+31 (t_r at bit r & 31): HEAD accumulates and stores
     // each word when complete, the tail streams them in (wave-uniform level: L1 hits)
-    uint32_t tw = HEAD ? party : tvec[pp * kMmoTWords];  // t_0 (lib.rs:169)
+    uint32_t tw = HEAD ? party : tvec[pp * twn];  // t_0 (lib.rs:169)
     uint32_t t = party;
     const uint32_t mlast = (j == nb - 1) ? kMaskLast : 0xFFFFFFFFu;
     for (uint32_t lev = 0; lev < nlev; ++lev) {
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mmo_wide_eval(
         tn = ((st[0][0] ^ s[0]) & 1u) ^ (t & (ct >> xb) & 1u);  // t' = t_side ^ t & cw.t_side (lib.rs:179-180)
       } else {
         const uint32_t r = lev + 1u;
-        if ((r & 31u) == 0u) tw = tvec[pp * kMmoTWords + (r >> 5)];
+        if ((r & 31u) == 0u) tw = tvec[pp * twn + (r >> 5)];
         tn = (tw >> (r & 31u)) & 1u;
       }
 #pragma unroll
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mmo_wide_eval(
       if (HEAD) {
         const uint32_t r = lev + 1u;
         if ((r & 31u) == 0u) {  // word (r >> 5) - 1 complete
-          if (live) tvec[p * kMmoTWords + (r >> 5) - 1u] = tw;
+          if (live) tvec[p * twn + (r >> 5) - 1u] = tw;
           tw = 0u;
         }
         tw |= tn << (r & 31u);
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mmo_wide_eval(
       *reinterpret_cast<uint4*>(ys + p * lam + 16ull * j) =  // y = v ^ s ^ t*cw_np1 (lib.rs:192)
           make_uint4(v[0] ^ s[0] ^ (tm & np.x), v[1] ^ s[1] ^ (tm & np.y), v[2] ^ s[2] ^ (tm & np.z),
                      v[3] ^ s[3] ^ (tm & np.w));
-      if (HEAD) tvec[p * kMmoTWords + (nlev >> 5)] = tw;  // the word holding t_n
+      if (HEAD) tvec[p * twn + (nlev >> 5)] = tw;  // the word holding t_n
     }
   }
 }

@@ -278,8 +278,11 @@ __device__ __forceinline__ void tail_store(uint8_t* ys, uint64_t pw, uint32_t pi
 // point, each owns one 16-byte piece.  LDS: G[chunk][nibble][LP] uint4,
 // G[c][e] = XOR of W rows 4c+k over the set bits k of e.  All LP lanes of a
 // point read one contiguous TW-byte entry -> conflict-free ds_read_b128.
+// A launch covers chunks [c0, c0 + ncp) (ncp <= what the LDS holds; c0 % 16 == 0): when
+// the t-sequence has more chunks than one table set holds (N >= 160 at 32-byte tiles), the
+// host runs passes and ACC launches start from the y the previous pass wrote instead of s0.
 // ------------------------------------------------------------------------
-template <int TW, int NCH = 0>
+template <int TW, int NCH = 0, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __restrict__ cw_s,
                                                             const uint8_t* __restrict__ cw_v,
                                                             const uint8_t* __restrict__ cw_np1,
@@ -288,15 +291,17 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
                                                             const uint64_t key0, const uint32_t* __restrict__ tvec,
                                                             const uint64_t count, const uint32_t pts_per_block,
                                                             uint8_t* __restrict__ ys, const uint32_t tw,
-                                                            const uint64_t ppk, const uint32_t rpk) {
+                                                            const uint64_t ppk, const uint32_t rpk,
+                                                            const uint32_t c0, const uint32_t ncp) {
   constexpr int LP = TW / 16;
+  const uint32_t cb = ACC ? c0 : 0u;  // first chunk of this pass
   // Row blockIdx.y of the grid = range rr of key kk of the launch's keys (ppk points each, rpk
   // ranges per key; one key: ppk = count, rpk = gridDim.y)
   const uint32_t kk = blockIdx.y / rpk, rr = blockIdx.y % rpk;
   const uint64_t key = key0 + kk;
   extern __shared__ uint4 G[];
   if (TW == 256 && (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)G != 0u) __builtin_trap();
-  const uint32_t nrows = nlev + 1, nch = (nrows + 3) >> 2;
+  const uint32_t nch = ncp;
   // Tiles are aligned to TW bytes of the output row (tile 0's first 32 bytes belong to
   // the head and are skipped): unaligned 256-byte pieces split cache lines between
   // neighbouring tiles and measured 20 % slower HBM writes.
@@ -307,7 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
     const uint32_t qq = it % LP, c = it / LP;
     uint4 w[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = w_row_piece(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, 4 * c + k, byte0 + 16 * qq);
+    for (int k = 0; k < 4; ++k) w[k] = w_row_piece(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, 4 * (cb + c) + k, byte0 + 16 * qq);
     uint4* dst = G + (c * 16) * LP + qq;
     uint4 e[16];
     e[0] = make_uint4(0u, 0u, 0u, 0u);
@@ -337,9 +342,16 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
   // clamped instead of guarded, and the y store below is unconditional too: with no
   // branch around any vector-memory instruction the compiler counts vmcnt exactly and
   // waits for the t-vector loads only, never for an older non-temporal y store.
-  const uint4* tv4 = reinterpret_cast<const uint4*>(tvec);
+  const uint4* tv4 = reinterpret_cast<const uint4*>(tvec) + cb / 16u;  // this pass's t words
   const uint32_t tw4 = tw / 4u;
   uint64_t p = p0 + threadIdx.x / LP;
+  // ACC: the point's y piece so far (dead lanes and past-the-end points read a clamped, unused piece)
+  auto ycur = [&](uint64_t pp) -> uint4 {
+    if (!ACC) return cst;
+    pp = min<uint64_t>(pp, p1 - 1);
+    const uint4 v = *reinterpret_cast<const uint4*>(ys + pp * lam + (lane_live ? off : 32u));
+    return lane_live ? v : make_uint4(0u, 0u, 0u, 0u);
+  };
   uint4 ta[4], tb[4];
   tail_load_t(ta, tv4, p, p1, tw4);
   tail_load_t(tb, tv4, p + pstep, p1, tw4);
@@ -351,14 +363,14 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
   for (;;) {
     if (p >= p1) break;
     {
-      const uint4 y = tail_piece<TW, LP, NCH>(ta, cst, gb, G, q, nch16, nrem, tv4 + tw4 * min<uint64_t>(p, p1 - 1));
+      const uint4 y = tail_piece<TW, LP, NCH>(ta, ycur(p), gb, G, q, nch16, nrem, tv4 + tw4 * min<uint64_t>(p, p1 - 1));
       tail_load_t(ta, tv4, p + 2 * pstep, p1, tw4);
       tail_store<LP>(ys, p - pin, pin, lam, off, lane_live ? 0u : dead, y);
     }
     p += pstep;
     if (p >= p1) break;
     {
-      const uint4 y = tail_piece<TW, LP, NCH>(tb, cst, gb, G, q, nch16, nrem, tv4 + tw4 * min<uint64_t>(p, p1 - 1));
+      const uint4 y = tail_piece<TW, LP, NCH>(tb, ycur(p), gb, G, q, nch16, nrem, tv4 + tw4 * min<uint64_t>(p, p1 - 1));
       tail_load_t(tb, tv4, p + 2 * pstep, p1, tw4);
       tail_store<LP>(ys, p - pin, pin, lam, off, lane_live ? 0u : dead, y);
     }

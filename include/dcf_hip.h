@@ -112,8 +112,8 @@ int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int 
  *   MMO" at LAMBDA >= 32), t_L / t_R = Lsb0 bit 0 of byte 0 of s_L / s_R, then bit 0
  *   of byte LAMBDA-1 cleared in all four outputs (the Hirose convention of prg.rs:63-68).
  * keys: cipher_n * 16 bytes, cipher_n >= 4 * lambda / 16 (else DCF_ERR_CIPHER_N).
- * Every gen / eval / prg entry point below accepts either PRG (LAMBDA >= 32: N <= 31,
- * no shared-prefix table). */
+ * Every gen / eval / prg entry point below accepts either PRG (LAMBDA >= 32: no
+ * shared-prefix table). */
 int dcf_mmo_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int device, dcf_prg** out);
 
 /* 0 = Aes256HirosePrg, 1 = Aes128MatyasMeyerOseasPrg, -1 = null. */

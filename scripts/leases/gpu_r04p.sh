@@ -1,0 +1,8 @@
+# r04p: GPU suite + smoke on the tree after the tail A/Bs (reverted code, new tail2 layout cases).
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r04p; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log

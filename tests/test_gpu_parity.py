@@ -433,13 +433,13 @@ def test_wide_gen_batch_and_multikey(dcf):
 
 @pytest.mark.parametrize("lam,nb,K,P", [(32, 2, 9, 5), (64, 3, 40, 17), (96, 2, 12, 33), (128, 16, 70, 64),
                                          (256, 5, 300, 8), (128, 40, 20, 30), (96, 3, 4, 9000), (32, 2, 5000, 8),
-                                         (128, 4, 3, 40000)])
+                                         (128, 4, 3, 40000), (64, 170, 4, 9)])
 def test_wide_multikey_batched_vs_oracle(dcf, lam, nb, K, P):
     """LAMBDA >= 32 multi-key eval: keys with <= 32768 points go through batched head / tail
     passes of up to 4096 keys (per-point key, per-workgroup key tables; the 4-bit tail at
     LAMBDA = 96 — with 9000 points per key, three tail ranges per key — and at N = 40, the
-    paired-slot tail at 128 / 256; 5000 keys take two passes); 40000 points per key takes the
-    per-key path.  Both parties reconstruct."""
+    paired-slot tail at 128 / 256; 5000 keys take two passes; N = 170, two tail passes over the
+    t-sequence); 40000 points per key takes the per-key path.  Both parties reconstruct."""
     import torch
     rng = np.random.default_rng(lam * 31 + K)
     keys = [rng.bytes(32) for _ in range(18)]
@@ -675,18 +675,35 @@ def test_wide_large_n_vs_oracle(dcf, nb, lam, m, mode):
         assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), b
 
 
-def test_wide_beyond_largest_n_refused(dcf):
-    """N = 160 at LAMBDA >= 32 is refused with DCF_ERR_UNSUPPORTED (-7) rather than evaluated wrong
-    (the 4-bit tail's tables of 32-byte tiles would exceed the LDS)."""
-    lam, nb = 128, 160
-    rng = np.random.default_rng(0x160)
+@pytest.mark.parametrize("nb,lam,m,mode", [(160, 128, 96, 0), (161, 64, 70, 1), (200, 256, 40, 0),
+                                             (401, 128, 33, 0)])
+def test_wide_n_past_one_table_set_vs_oracle(dcf, nb, lam, m, mode):
+    """N >= 160 at LAMBDA >= 32: the t-sequence has more 4-row chunks (> 320) than one set of
+    32-byte-tile tables holds in the LDS, so the tail runs in passes of 320 chunks, each after the
+    first adding its rows' share to the y the previous pass wrote (N = 401: three passes, the last
+    with 3 chunks).  Both parties vs the oracle, alpha and a neighbour among the points."""
+    rng = np.random.default_rng(0x160 + nb + lam)
     keys = [rng.bytes(32) for _ in range(18)]
-    d = dcf.DcfImpl(nb, lam, dcf.Aes256HirosePrg(keys, lam))
-    s0, s1 = rng.bytes(lam), rng.bytes(lam)
-    k = d.gen(dcf.CmpFn(rng.bytes(nb), rng.bytes(lam)), [s0, s1], dcf.BoundState.LtBeta)
-    with pytest.raises(dcf.DcfError) as e:
-        d.eval(False, dcf.Share([s0], k.cws, k.cw_np1), _rand(rng, (8, nb)))
-    assert e.value.code == -7
+    prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    prg.set_eval_mode(mode)
+    d = dcf.DcfImpl(nb, lam, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+    ok = O.gen(P, alpha, beta, s0, s1, 0)
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
+    xs = _rand(rng, (m, nb))
+    xs[0] = np.frombuffer(alpha, np.uint8)
+    xs[1] = xs[0]
+    xs[1, -1] ^= 1
+    ys = []
+    for b, s in ((0, s0), (1, s1)):
+        got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
+        assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), b
+        ys.append(got)
+    rec = ys[0] ^ ys[1]
+    a = int.from_bytes(alpha, "big")
+    for i in range(m):
+        on = int.from_bytes(xs[i].tobytes(), "big") < a
+        assert rec[i].tobytes() == (beta if on else bytes(lam)), i
 
 
 @pytest.mark.parametrize("nb,m", [(16, 3000), (4, 70_000), (16, 100_000), (2, 1000)])

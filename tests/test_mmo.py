@@ -227,11 +227,13 @@ def test_gpu_mmo_wide_prg_vs_oracle(dcf, lam):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("lam,nb,m", [(32, 2, 300), (48, 3, 200), (64, 16, 130), (512, 4, 100), (16384, 16, 70),
-                                      (32, 1, 256), (96, 5, 65)])
+                                      (32, 1, 256), (96, 5, 65), (64, 31, 70), (48, 32, 70), (64, 40, 65),
+                                      (32, 100, 40)])
 def test_gpu_mmo_wide_gen_eval_vs_oracle(dcf, lam, nb, m):
     """gen + eval of both parties and both bounds at LAMBDA >= 32 (head over block 0, tail over
     the others) bit for bit with the oracle, and the reconstruction y0 ^ y1 = beta [x < alpha]
-    (LtBeta) / [x > alpha] (GtBeta) on every point (parity unpinned by the reference)."""
+    (LtBeta) / [x > alpha] (GtBeta) on every point (parity unpinned by the reference).  N >= 32:
+    the t-vector passes 8 words (t_0 .. t_n, n + 1 > 256 bits)."""
     rng, keys = _mmo_keys(lam, lam * 3 + nb)
     prg, P = dcf.Aes128MatyasMeyerOseasPrg(keys, lam), O.OracleMmoPrg(keys, lam)
     d = dcf.DcfImpl(nb, lam, prg)
