@@ -706,6 +706,44 @@ def test_wide_n_past_one_table_set_vs_oracle(dcf, nb, lam, m, mode):
         assert rec[i].tobytes() == (beta if on else bytes(lam)), i
 
 
+@pytest.mark.parametrize("kind,lam,nb", [(0, 16, 16), (0, 128, 16), (0, 64, 200), (1, 16, 4), (1, 64, 40)])
+def test_empty_batches_every_path(dcf, kind, lam, nb):
+    """Empty inputs are no-ops on every entry point, both PRGs, LAMBDA = 16 and >= 32 (the
+    reference's eval maps an empty xs to an empty ys, lib.rs:163-204): host eval of 0 points,
+    device eval of 0 points, batched gen of 0 keys, multi-key eval of 0 keys and of K keys x 0
+    points; a following non-empty eval on the same prg is still exact."""
+    import torch
+    rng = np.random.default_rng(kind * 1000 + lam + nb)
+    if kind == 0:
+        keys = [rng.bytes(32) for _ in range(18)]
+        prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
+    else:
+        keys = [rng.bytes(16) for _ in range(4 * lam // 16)]
+        prg, P = dcf.Aes128MatyasMeyerOseasPrg(keys, lam), O.OracleMmoPrg(keys, lam)
+    d = dcf.DcfImpl(nb, lam, prg)
+    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(lam), rng.bytes(lam), rng.bytes(lam)
+    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState.LtBeta)
+    assert d.eval(False, dcf.Share([s0], k.cws, k.cw_np1), np.zeros((0, nb), np.uint8)).shape == (0, lam)
+    dev = "cuda"
+    cwb = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, nb, lam), np.uint8).copy()).to(dev)
+    s0d = torch.from_numpy(np.frombuffer(s0, np.uint8).copy()).to(dev)
+    assert d.eval_device(False, cwb, s0d, torch.empty((0, nb), dtype=torch.uint8, device=dev)).shape == (0, lam)
+    e = lambda *sh: torch.empty(sh, dtype=torch.uint8, device=dev)  # noqa: E731
+    g0 = d.gen_batch_device(e(0, nb), e(0, lam), e(0, lam), e(0, lam), dcf.BoundState.LtBeta)
+    assert g0.numel() == dcf.cwb_bytes(nb, lam, 0)
+    assert d.eval_multikey_device(False, g0, e(0, lam), e(0, nb), 5).shape == (0, lam)
+    K = 3
+    r = lambda *sh: torch.from_numpy(rng.integers(0, 256, sh, dtype=np.uint8)).to(dev)  # noqa: E731
+    cwk = d.gen_batch_device(r(K, nb), r(K, lam), r(K, lam), r(K, lam), dcf.BoundState.GtBeta)
+    assert d.eval_multikey_device(True, cwk, r(K, lam), e(0, nb), 0).shape == (0, lam)
+    torch.cuda.synchronize()
+    ok = O.gen(P, alpha, beta, s0, s1, 0)
+    xs = _rand(rng, (70, nb))
+    xs[0] = np.frombuffer(alpha, np.uint8)
+    got = d.eval(False, dcf.Share([s0], k.cws, k.cw_np1), xs)
+    assert np.array_equal(got, O.eval_(P, 0, ok, s0, xs, nthreads=8))
+
+
 @pytest.mark.parametrize("nb,m", [(16, 3000), (4, 70_000), (16, 100_000), (2, 1000)])
 def test_host_mid_path_vs_device_and_oracle(dcf, nb, m):
     """Auto mode, host buffers, a batch in the small-batch kernels' range: dcf_eval reads x from and
