@@ -253,7 +253,7 @@ constexpr uint64_t kWideChunk = 1ull << 22;   // points per head/tail pass (t-ve
 // Points per LAMBDA >= 32 head/tail pass for t-vectors of tw words: kWideChunk up to N = 31 (16
 // words), fewer for longer t-sequences so the scratch stays ~256 MiB.
 uint64_t wide_chunk_points(uint32_t tw) {
-  return std::max<uint64_t>(65536, kWideChunk * 16 / std::max<uint32_t>(tw, 16u));
+  return std::max<uint64_t>(16384, kWideChunk * 16 / std::max<uint32_t>(tw, 16u));
 }
 constexpr uint64_t kGenChunk = 4096;          // keys per wide-gen launch (scratch 3*LAMBDA per key)
 constexpr uint32_t kTailPts = 4096;          // points per tail workgroup (one table build each)
