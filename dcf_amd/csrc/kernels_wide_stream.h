@@ -467,6 +467,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_wpfx_build(
   __shared__ uint4 root[5];
   if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
   lds_fill_tables(lds, tab);
+  DCF_CLK(6, 0);  // (diagnostic builds; slots 6 / 7 are k_prefix_build16's at LAMBDA = 16) after the fill
   const uint32_t lc = lane_const();
   const uint32_t w = blockIdx.x;
   const uint64_t R5 = 5ull * region_nodes;
@@ -488,9 +489,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_wpfx_build(
       for (int q = 0; q < 5; ++q) root[q] = nd[q];
   }
   __syncthreads();
+  DCF_CLK(6, 1);  // root path done
   for (uint32_t lev = S; lev < D; ++lev) {
     const uint32_t np = 1u << (lev - S);
     const bool last = lev + 1u == D;
+    if (lev + 3u == D) DCF_CLK(7, 0);  // the last three levels start
     uint4* out = last ? table + 5ull * ((uint64_t)w << (D - S)) : Y;
     // whole waves stay in the loop (uniform AES); lanes past np compute a copy of node np - 1
     for (uint32_t g = threadIdx.x; g - (threadIdx.x & 63u) < np; g += blockDim.x) {
@@ -514,6 +517,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_wpfx_build(
     X = Y;
     Y = tmp;
   }
+  DCF_CLK(7, 1);
 }
 
 }  // namespace
