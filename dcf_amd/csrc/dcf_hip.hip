@@ -553,12 +553,17 @@ int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, con
   const size_t lds = L::lds_bytes();
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  // One workgroup per CU: the batch split into cus / tiles ranges, so the tiles of a range build
-  // their tables once and walk its points together (the rows being written at any time stay
-  // few), at least 32768 points per workgroup (C4 A/B: 34.36-34.38 ms vs 34.78-35.01 with
-  // 32768-point ranges; 4096-point ranges 37.8-38.0).
+  // One workgroup per CU at a time, kTail2Rounds rounds of them: the batch split into
+  // rounds x cus / tiles ranges, so the tiles of a range build their tables once and walk its
+  // points together (the rows being written at any time stay few), at least 32768 points per
+  // workgroup.  Several rounds let the dispatcher even out the CUs' speeds (one round: the last
+  // workgroup ended ~1 ms after the first, profiles/r04b_c4_timeline_dynamic_tail.json).  C4 A/B
+  // (r04t / r04u, 3 alternating runs per box): rounds 1 / 2 / 4 / 8 32.33-32.53 / 32.46-32.73 /
+  // 32.28-32.43 / 32.16-32.27 ms; on a second box 8 / 16 / 32 / 64 (= 32768-point ranges)
+  // 33.08-33.12 / 33.12-33.41 / 33.24-33.28 / 33.69-33.99 ms.
   // Several keys (ppk < cnt): each key's points are ranges of their own (its own tables).
-  const uint64_t ranges = std::max<uint64_t>(1, (uint64_t)cus / tiles);
+  constexpr uint64_t kTail2Rounds = 8;
+  const uint64_t ranges = std::max<uint64_t>(1, (uint64_t)cus * kTail2Rounds / tiles);
   const uint64_t per = std::max<uint64_t>(32768, (((cnt + ranges - 1) / ranges) + 255) & ~(uint64_t)255);
   const uint64_t rpk = (ppk + per - 1) / per;
   const dim3 grid((unsigned)tiles, (unsigned)((cnt / ppk) * rpk));

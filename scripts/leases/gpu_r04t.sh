@@ -1,0 +1,9 @@
+# r04t: C4 tail2 workgroup rounds (ranges per tile = rounds x CUs / tiles): 1 (default, one round
+# of 256 workgroups), 2, 4, 8 — three alternating same-box runs each.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r04t; mkdir -p $O
+for rep in 1 2 3; do for v in tr1 tr2 tr4 tr8; do
+  DCF_HIP_LIB=$PWD/dcf_amd/libdcf_hip_$v.so timeout -k 10 300 python bench.py --workload c4 --steps 10 --warmup 3 --no-cpu --no-compare > $O/c4_${v}_$rep.json 2> $O/c4_${v}_$rep.err || { tail -20 $O/c4_${v}_$rep.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/c4_${v}_$rep.json')); r=d['roofline']; print('c4 $v', round(d['value']/1e6,2), round(d['ms_per_step'],3), round(r['frac'],4))"
+done; done
