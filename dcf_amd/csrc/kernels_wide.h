@@ -410,19 +410,26 @@ struct Tail2Layout {
 
 // Old nibble t-vector (row r at byte r >> 2, bit r & 3; words 0 .. nlev >> 4 valid) -> chunk
 // bytes of Tail2Layout<R6, R5>, in place (bytes [0, 32) of each 64-byte row).  One thread
-// per point: 36 of 64 bytes read, 32 written.
+// per point: the row's first 16-byte pieces the layout's rows need read whole (unwritten
+// words hold rows past t_n, cleared below), 32 bytes written.
 template <int R6, int R5>
 __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, const uint64_t count) {
   using L = Tail2Layout<R6, R5>;
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= count) return;
   uint32_t* row = tvec + p * kTWords;
-  const uint32_t nw = (nlev >> 4) + 1u;  // nibble words written by the head
+  constexpr uint32_t NQ = (L::rows() + 63u) / 64u;  // 16-byte pieces holding rows 0 .. rows() - 1
+  uint32_t wv[4 * NQ];
+#pragma unroll
+  for (uint32_t q = 0; q < NQ; ++q) {
+    const uint4 t = reinterpret_cast<const uint4*>(row)[q];
+    wv[4 * q] = t.x; wv[4 * q + 1] = t.y; wv[4 * q + 2] = t.z; wv[4 * q + 3] = t.w;
+  }
   uint32_t pk[6] = {0u, 0u, 0u, 0u, 0u, 0u};  // rows as a plain bit string, row r = bit r
 #pragma unroll
-  for (uint32_t j = 0; j < 12; ++j) {
-    if (j < nw && 16u * j < L::rows()) {
-      uint32_t x = row[j] & 0x0F0F0F0Fu;
+  for (uint32_t j = 0; j < 4 * NQ; ++j) {
+    if (16u * j < L::rows()) {
+      uint32_t x = wv[j] & 0x0F0F0F0Fu;
       x = (x | (x >> 4)) & 0x00FF00FFu;
       x = (x | (x >> 8)) & 0x0000FFFFu;
       pk[j >> 1] |= x << (16u * (j & 1u));
