@@ -1428,7 +1428,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
         HIP_TRY(hipEventRecord(w->aux_ev[1], w->aux));
       }
       hipLaunchKernelGGL(k_cw_keymajor, dim3((unsigned)((num_keys + kKmKeys - 1) / kKmKeys), (unsigned)((n + kKmLevs - 1) / kKmLevs)),
-                         dim3(256), 0, st, cws, cwv, cwt, (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig,
+                         dim3(kKmThreads), 0, st, cws, cwv, cwt, (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig,
                          w->d_kdig + (size_t)num_keys * n * 32);
       HIP_TRY(hipGetLastError());
       if (fork) HIP_TRY(hipStreamWaitEvent(st, w->aux_ev[1], 0));
