@@ -1,0 +1,15 @@
+# r04z5: last tree of the round (tail rounds, t-vector repack, digest): GPU suite, smoke, C3 (driver command) and C4 lines, C4 trace.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r04z5; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_c3.json 2> $O/bench_c3.err || { tail -20 $O/bench_c3.err; exit 1; }
+python -c "import json; d=json.load(open('$O/bench_c3.json')); r=d['roofline']; print('c3', round(d['value']/1e6,1), round(r['frac'],4), d['ms_per_step'])"
+timeout -k 10 500 python bench.py --workload c4 --steps 10 --warmup 3 > $O/bench_c4.json 2> $O/bench_c4.err || { tail -20 $O/bench_c4.err; exit 1; }
+python -c "import json; d=json.load(open('$O/bench_c4.json')); r=d['roofline']; print('c4', d['value'], r['frac'], d['ms_per_step'])"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace_c4 -o trace -- python3 bench.py --workload c4 --steps 5 --warmup 2 --no-cpu > $O/bench_trace_c4.json 2> $O/bench_trace_c4.err || { tail -20 $O/bench_trace_c4.err; exit 1; }
+python scripts/trace_summary.py $O/trace_c4 --tail 12 > $O/prof_c4.md && rm -rf $O/trace_c4
+head -9 $O/prof_c4.md
