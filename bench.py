@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -43,21 +44,11 @@ LDS_LOOKUPS = CUS * 32 * CLK_HZ      # ds_read_b32: 64 lanes per 2 LDS cycles pe
 VALU_OPS = CUS * 128 * CLK_HZ        # 4 SIMD-32 per CU, wave64 op every 2 cycles per SIMD
 TT_LDS_PER_BLOCK = 14 * 16           # T-table AES-256: 16 lookups per round
 TT_VALU_PER_BLOCK = 370              # 1 v_perm per lookup + 2 v_bitop3 per column + DCF share
-BS_VALU_PER_BLOCK = 800              # bitsliced: 453 VALU per lane-round / 8 blocks per lane, + last round, ARK, DCF
 PEAK_TT_BLOCKS = LDS_LOOKUPS / TT_LDS_PER_BLOCK  # ~87.8 G blocks/s: T-table alone is LDS-bound
 
 
-def hybrid_peak() -> float:
-    """Best blocks/s with both engines on every CU: the T-table engine takes the whole
-    LDS issue rate, the bitsliced engine the VALU it leaves (a 2-resource LP)."""
-    b_tt = PEAK_TT_BLOCKS
-    valu_left = VALU_OPS - b_tt * TT_VALU_PER_BLOCK
-    return b_tt + max(0.0, valu_left) / BS_VALU_PER_BLOCK
-
-
-ENGINE = {0: "stream", 1: "ttable", 2: "bitsliced", 3: "hybrid", 4: "stream", 5: "stream-hybrid"}
-KERNEL = {"hybrid": "k_eval16_hybrid", "ttable": "k_eval16_hybrid", "ttable-small": "k_eval16_pair", "bitsliced": "k_eval16_bs",
-          "stream": "k_eval16_stream", "mmo": "k_eval16_mmo", "stream-hybrid": "k_eval16_shybrid"}
+ENGINE = {0: "stream", 1: "ttable", 4: "stream"}
+KERNEL = {"ttable": "k_eval16", "ttable-small": "k_eval16_pair", "stream": "k_eval16_stream", "mmo": "k_eval16_mmo"}
 
 
 # MMO (AES-128, kernels_mmo.h): 10 rounds x 16 lookups + 11 round-key ds_read_b128 (16 lanes/clk) per block
@@ -77,11 +68,7 @@ def measured_ceiling(achieved_blocks_per_s: float) -> dict:
 def engine_peak(engine: str) -> float:
     if engine in ("mmo", "mmo-wide"):
         return PEAK_MMO_BLOCKS
-    if engine in ("ttable", "ttable-small", "stream"):
-        return PEAK_TT_BLOCKS
-    if engine == "bitsliced":
-        return VALU_OPS / BS_VALU_PER_BLOCK
-    return hybrid_peak()
+    return PEAK_TT_BLOCKS
 
 
 def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels: int = 0):
@@ -189,6 +176,39 @@ def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, cmd, env=None, poll_s: float = 0.2) -> int:
+    """`--gpus N` (N > 1) without a launcher (WORLD_SIZE unset): start N fresh rank processes
+    running `cmd` with the environment torch.distributed.run would give them (RANK, LOCAL_RANK,
+    WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR = 127.0.0.1, a free MASTER_PORT), one per GPU
+    (each rank takes device = LOCAL_RANK in dist_setup), and wait for them.  This process never
+    touches the GPU and replaces itself with nothing: the ranks are children (fork + exec of a
+    process with no HIP state).  Rank 0's stdout is this process's stdout, so the one JSON line
+    reaches the caller unchanged.  When a rank fails, the others are ended (their own PIDs) and
+    the exit status is the first failure's (128 + signal for a killed rank)."""
+    base = dict(os.environ if env is None else env)
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR=base.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        procs.append(subprocess.Popen(list(cmd), env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(poll_s)
+    return rc
 
 
 def pg() -> bool:
@@ -374,10 +394,6 @@ def run_eval(args, world, rank):
         keys = [rng.bytes(32) for _ in range(2 if lam == 16 else 2048)]
         prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
     prg.set_eval_mode(args.eval_mode)
-    if args.hybrid_split is not None:
-        prg.set_hybrid_split(args.hybrid_split, args.hybrid_mem)
-    if args.shy_mask is not None:
-        prg.set_stream_hybrid(int(args.shy_mask, 0), args.shy_prio)
     prg.set_prefix_levels(args.prefix)
     pfx = prg.eval_prefix_levels(nb, 1, m)  # shared-prefix depth this eval uses (0 = none)
     d = dcf_amd.DcfImpl(nb, lam, prg)
@@ -424,12 +440,15 @@ def run_eval(args, world, rank):
     total_evals = global_points * args.steps * parties
     value = total_evals / wall
     check = slice_check(d, cwb, s0, ys, nb, lam, args, world, rank) if args.check else None
+    abi_check = None
+    if rank == 0 and (world > 1 or args.abi_check):
+        prg_cls = dcf_amd.Aes128MatyasMeyerOseasPrg if args.prg == "mmo" else dcf_amd.Aes256HirosePrg
+        abi_check = multi_gpu_abi_check(keys, nb, lam, prg_cls, d, cwb, s0,
+                                        points=min(1 << 20, max(1, (1 << 30) // (lam * 8))))
     bpe = blocks_per_eval(nb, lam)
     if args.prg == "mmo" and lam > 16:
         bpe = 4 * 8 * nb * (lam // 16)  # the MMO PRG's full output per level: 4 outputs x LAMBDA/16 blocks
     engine = ENGINE[args.eval_mode] if lam == 16 else "ttable"
-    if engine in ("hybrid", "bitsliced", "stream-hybrid") and nb > 16:
-        engine = "ttable"
     if args.prg == "mmo":
         engine = "mmo"
     elif args.eval_mode == 0 and lam == 16 and m < CUS * 1024 * 2:
@@ -456,7 +475,7 @@ def run_eval(args, world, rank):
     elif lam > 16:
         # LAMBDA >= 32: the stream head encrypts B, A (left) or B, D, C (right) per level, and the
         # tail writes LAMBDA - 32 output bytes per eval: time bound = AES (LDS) + output (HBM write).
-        engine = "stream-head" if args.eval_mode != 1 else "ttable"
+        engine = "stream-head"
         if engine == "stream-head":
             # below a shared prefix of pfx levels (k_wpfx_build: 4 blocks per parent node); the
             # walk's blocks are counted by the kernel (B reuse after a right step at t = 0 skips
@@ -488,7 +507,7 @@ def run_eval(args, world, rank):
         "aes_blocks_per_s_reference_count": value * bpe,
         "aes_blocks_per_s_executed": value * exec_bpe,
         "roofline": wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine) if (lam > 16 and engine != "mmo-wide") else {
-            "bound": "lds" if engine in ("ttable", "ttable-small", "stream", "mmo", "mmo-wide") else ("valu" if engine == "bitsliced" else "lds+valu"),
+            "bound": "lds",
             "kernel": kernel, "engine": engine,
             "achieved": per_gpu_blocks / 1e9, "peak": peak / 1e9, "unit": "G AES-128 blocks/s" if engine.startswith("mmo") else "G AES-256 blocks/s",
             "frac": per_gpu_blocks / peak, "traffic": traffic, "traffic_source": traffic_src,
@@ -505,9 +524,7 @@ def run_eval(args, world, rank):
                     "aes_blocks_per_s_reference_count above uses the reference count (2 per level; the kernels skip "
                     "unused A blocks, reused B blocks and the shared prefix, so it exceeds the LDS peak), "
                     "aes_blocks_per_s_executed the blocks actually encrypted.  Peak per GPU at 2.4 GHz: T-table "
-                    "engines LDS-bound (32 ds_read_b32 lookups/clk/CU, 224 per block), bitsliced VALU-bound "
-                    "(128 lane-ops/clk/CU, ~800 per block); hybrid = LDS-saturating T-table + bitsliced on "
-                    "the VALU left over (DESIGN.md section 4)",
+                    "engines LDS-bound (32 ds_read_b32 lookups/clk/CU, 224 per block; DESIGN.md section 4)",
         },
     }
     if lam > 16 and engine != "mmo-wide":
@@ -516,6 +533,8 @@ def run_eval(args, world, rank):
             kernel, m, nb, lam, pfx, m * (nb + lam))
     if check is not None:
         out["slice_check"] = check
+    if abi_check is not None:
+        out["multi_gpu_abi_check"] = abi_check
     out["phases"] = {"table_ms": table_ms, "walk_ms": walk_ms, "prefix_levels": depth,
                      "note": "rank 0, one untimed eval with phase events (dcf_prg_set_phase_timing)"}
     if pg():
@@ -546,11 +565,16 @@ def run_eval(args, world, rank):
 
 
 def ys_digest(ys: torch.Tensor) -> int:
-    """Order-sensitive 64-bit digest of an output slice (row-weighted byte sums)."""
-    y = ys.to(torch.int64)
-    w = torch.arange(1, ys.shape[0] + 1, device=ys.device, dtype=torch.int64).unsqueeze(1)
+    """Order-sensitive 64-bit digest of an output slice (row-weighted byte sums), in chunks of
+    rows so the int64 temporaries stay small."""
     c = torch.arange(1, ys.shape[1] + 1, device=ys.device, dtype=torch.int64)
-    return int(((y * w).sum() + (y.sum(0) * c).sum()).item())
+    tot = torch.zeros((), dtype=torch.int64, device=ys.device)
+    step = max(1, (1 << 24) // max(1, ys.shape[1]))
+    for off in range(0, ys.shape[0], step):
+        y = ys[off:off + step].to(torch.int64)
+        w = torch.arange(off + 1, off + y.shape[0] + 1, device=ys.device, dtype=torch.int64).unsqueeze(1)
+        tot += (y * w).sum() + (y.sum(0) * c).sum()
+    return int(tot.item())
 
 
 def slice_check(d, cwb, s0, ys, nb, lam, args, world, rank):
@@ -572,6 +596,78 @@ def slice_check(d, cwb, s0, ys, nb, lam, args, world, rank):
     return {"ranks": world, "slices_match": all(ok), "per_rank": ok}
 
 
+def multi_gpu_abi_check(keys, nb, lam, prg_cls, d, cwb, s0, points: int = 1 << 20):
+    """N > 1, rank 0, after timing: one dcf_eval_multi_gpu_device call (the one-process
+    multi-GPU C ABI) over every visible device (at least 2 prgs: on a one-GPU box both sit on
+    device 0), slices gathered into one buffer on device 0 — hipMemcpyPeerAsync over xGMI for
+    every slice on another device — and compared byte for byte with rank 0's own
+    dcf_eval_device over the same points.  Never raises: a failure is recorded in the line."""
+    t0 = time.perf_counter()
+    ndev = torch.cuda.device_count()
+    G = max(2, min(ndev, 8))
+    devs = [g % ndev for g in range(G)]
+    rec = {"devices": devs, "points": points, "peer_slices": sum(1 for v in devs if v != devs[0])}
+    try:
+        impls = [dcf_amd.DcfImpl(nb, lam, prg_cls(keys, lam, device=v)) for v in devs]
+        mg = dcf_amd.MultiGpuDcf(impls)
+        xs = gen_points(points, nb, 0, 0xDCF0004)
+        slices = []
+        for g, v in enumerate(devs):
+            st, cnt = dcf_amd.point_slice(points, G, g)
+            slices.append(xs[st:st + cnt].to(torch.device("cuda", v)).contiguous())
+        gather = torch.empty((points, lam), dtype=torch.uint8, device=xs.device)
+        cwb_h = cwb.cpu().numpy().tobytes()
+        ys_sl = mg.eval_device(False, cwb_h, s0.cpu().numpy().tobytes(), slices, gather=gather)
+        ref = d.eval_device(False, cwb, s0, xs)
+        torch.cuda.synchronize()
+        rows = [dcf_amd.point_slice(points, G, g) for g in range(G)]
+        rec["slices_match"] = all(torch.equal(ys_sl[g].to(xs.device), ref[st:st + c]) for g, (st, c) in enumerate(rows))
+        rec["gather_matches"] = bool(torch.equal(gather, ref))
+        rec["ok"] = rec["slices_match"] and rec["gather_matches"]
+    except Exception as e:  # noqa: BLE001 — recorded, the line still prints
+        rec["ok"] = False
+        rec["error"] = f"{type(e).__name__}: {e}"
+    rec["ms"] = (time.perf_counter() - t0) * 1e3
+    rec["note"] = ("dcf_eval_multi_gpu_device over the devices listed (prgs from the same keys), gather on device "
+                   "0; peer_slices = slices copied from another device (hipMemcpyPeerAsync, dcf_hip.hip); compared "
+                   "with dcf_eval_device on rank 0; untimed, after the timed region")
+    return rec
+
+
+def c5_inputs(K: int, kstart: int, nb: int, lam: int, P: int):
+    """C5 keys [kstart, kstart + K): alpha, beta, both root seeds and P points per key, drawn on
+    device from a generator keyed by the slice start (any rank can regenerate any slice)."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5 * 1000003 + kstart)
+    rnd = lambda *s: torch.randint(0, 256, s, dtype=torch.uint8, device="cuda", generator=g)  # noqa: E731
+    alpha, beta, s0, s1 = rnd(K, nb), rnd(K, lam), rnd(K, lam), rnd(K, lam)
+    return alpha, beta, s0, s1, rnd(K * P, nb)
+
+
+def c5_check(d, cwb, y0, y1, args, world, rank, nb, lam, P):
+    """Multi-rank self-check of C5: every rank's (CWB, party-0 and party-1 outputs) digests go
+    to rank 0, which regenerates each rank's keys and points, runs batched gen and both
+    parties' multi-key eval itself, and compares."""
+    mine = [ys_digest(cwb.view(-1, 16)), ys_digest(y0), ys_digest(y1)]
+    digs = [mine]
+    if pg():
+        digs = [None] * world
+        dist.all_gather_object(digs, mine)
+    if rank != 0:
+        return None
+    ok = []
+    for r in range(world):
+        st, K = (point_slice(args.keys, world, r) if args.scaling == "strong" else weak_slice(args.keys, r))
+        alpha, beta, s0, s1, xs = c5_inputs(K, st, nb, lam, P)
+        cw = d.gen_batch_device(alpha, beta, s0, s1, dcf_amd.BoundState.LtBeta,
+                                torch.zeros(dcf_amd.cwb_bytes(nb, lam, K), dtype=torch.uint8, device="cuda"))
+        a = d.eval_multikey_device(False, cw, s0, xs, P)
+        b = d.eval_multikey_device(True, cw, s1, xs, P)
+        torch.cuda.synchronize()
+        ok.append([ys_digest(cw.view(-1, 16)), ys_digest(a), ys_digest(b)] == [int(v) for v in digs[r]])
+    return {"ranks": world, "slices_match": all(ok), "per_rank": ok}
+
+
 def run_c5(args, world, rank):
     """C5: K independent keys x 64 points: batched gen + eval of both parties per step.
     Strong scaling by default: the 2^20 keys are split over the ranks (dcf_point_slice)."""
@@ -586,12 +682,9 @@ def run_c5(args, world, rank):
     keys = [rng.bytes(32) for _ in range(2)]
     prg = dcf_amd.Aes256HirosePrg(keys, lam, device=torch.cuda.current_device())
     d = dcf_amd.DcfImpl(nb, lam, prg)
-    g = torch.Generator(device="cuda")
-    g.manual_seed(5 * 1000003 + kstart)
-    rnd = lambda *s: torch.randint(0, 256, s, dtype=torch.uint8, device="cuda", generator=g)  # noqa: E731
-    alpha, beta, s0, s1 = rnd(K, nb), rnd(K, lam), rnd(K, lam), rnd(K, lam)
-    xs = rnd(K * P, nb)
-    cwb = torch.empty(dcf_amd.cwb_bytes(nb, lam, K), dtype=torch.uint8, device="cuda")
+    alpha, beta, s0, s1, xs = c5_inputs(K, kstart, nb, lam, P)
+    # zeroed: gen writes every key byte, the padding before cw_np1 stays 0 (c5_check digests it all)
+    cwb = torch.zeros(dcf_amd.cwb_bytes(nb, lam, K), dtype=torch.uint8, device="cuda")
     y0 = torch.empty((K * P, lam), dtype=torch.uint8, device="cuda")
     y1 = torch.empty_like(y0)
     stream = torch.cuda.current_stream()
@@ -669,6 +762,10 @@ def run_c5(args, world, rank):
                                        "kernel_ms": step_s * 1e3, "gen_ms": phase[0] * 1e3,
                                        "eval_ms": (phase[1] + phase[2]) * 1e3})
         out["per_rank"] = per_rank_summary(recs, args.steps)
+    if args.check:
+        chk = c5_check(d, cwb, y0, y1, args, world, rank, nb, lam, P)
+        if chk is not None:
+            out["slice_check"] = chk
     if rank == 0 and world == 1 and not args.no_cpu:  # cpu_baseline: rank 0 at N=1 only
         out["cpu_baseline"] = c5_cpu_baseline(keys, nb, lam, alpha, beta, s0, s1, xs, cwb, y0, y1, K, P,
                                               args.cpu_seconds)
@@ -901,7 +998,31 @@ def json_stdout():
 
 
 def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: this process starts the N ranks itself and exits with their status
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     out_stream = json_stdout()
+    world, rank, _ = dist_setup(args.gpus, args.dist_backend, args.force_dist)
+    if args.workload == "lat":
+        out = run_latency(args, world, rank)
+    elif args.workload == "c5":
+        out = run_c5(args, world, rank)
+    elif args.workload == "fd":
+        out = run_fd(args, world, rank)
+    else:
+        out = run_eval(args, world, rank)
+    if args.workload not in ("fd", "lat") and (args.workload != "c3" or args.prg != "hirose"):
+        out["metric"] = (f"DCF evals/sec, workload {args.workload.upper()}, {args.prg} PRG "
+                         "(not the BASELINE.json headline config)")
+    if rank == 0:
+        print(json.dumps(out), file=out_stream, flush=True)
+    if pg():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -912,16 +1033,13 @@ def main():
     ap.add_argument("--n-bytes", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--eval-mode", type=int, default=0, help="AES engine: 0 auto, 1 T-table, 2 bitsliced, 3 hybrid, 4 stream")
+    ap.add_argument("--eval-mode", type=int, default=0, choices=[0, 1, 4],
+                    help="LAMBDA = 16 AES engine: 0 auto, 1 lockstep T-table, 4 stream")
     ap.add_argument("--prg", default="hirose", choices=["hirose", "mmo"],
                     help="hirose: the reference's Aes256HirosePrg; mmo: Aes128MatyasMeyerOseasPrg (lambda = 16)")
     ap.add_argument("--prefix", type=int, default=-1,
                     help="shared-prefix table depth for single-key eval: -1 auto (library default), 0 off")
     ap.add_argument("--no-compare", action="store_true", help="skip the no-prefix comparison timing")
-    ap.add_argument("--hybrid-split", type=int, default=None, help="hybrid: T-table waves per workgroup")
-    ap.add_argument("--shy-mask", default=None, help="stream-hybrid (eval mode 5): stream-wave mask, e.g. 0x7777")
-    ap.add_argument("--shy-prio", type=int, default=0, help="stream-hybrid: 1 = stream waves at raised priority")
-    ap.add_argument("--hybrid-mem", type=int, default=1, help="hybrid: 1 = 16 waves + scratch slabs, 0 = 12 waves")
     ap.add_argument("--scaling", default=None, choices=["strong", "weak"],
                     help="strong: the workload's points (C5: keys) are split over the ranks (default for c3, c5); "
                          "weak: every rank gets the full count (default otherwise)")
@@ -934,7 +1052,9 @@ def main():
                          "timing all-reduce run as at N > 1)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, rank 0 re-evaluates every rank's slice and compares output digests")
-    args = ap.parse_args()
+    ap.add_argument("--abi-check", action="store_true",
+                    help="run multi_gpu_abi_check at N = 1 too (always on at N > 1 for c1-c4)")
+    args = ap.parse_args(argv)
     if args.scaling is None:
         args.scaling = "strong" if args.workload in ("c3", "c5") else "weak"
     args.lam = 16
@@ -953,23 +1073,7 @@ def main():
     else:
         args.n_bytes = args.n_bytes or 16
         args.points = args.points or (1 << 28)
-    world, rank, _ = dist_setup(args.gpus, args.dist_backend, args.force_dist)
-    if args.workload == "lat":
-        out = run_latency(args, world, rank)
-    elif args.workload == "c5":
-        out = run_c5(args, world, rank)
-    elif args.workload == "fd":
-        out = run_fd(args, world, rank)
-    else:
-        out = run_eval(args, world, rank)
-    if args.workload not in ("fd", "lat") and (args.workload != "c3" or args.prg != "hirose"):
-        out["metric"] = (f"DCF evals/sec, workload {args.workload.upper()}, {args.prg} PRG "
-                         "(not the BASELINE.json headline config)")
-    if rank == 0:
-        print(json.dumps(out), file=out_stream, flush=True)
-    if pg():
-        dist.barrier()
-        dist.destroy_process_group()
+    return args
 
 
 if __name__ == "__main__":

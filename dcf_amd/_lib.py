@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DCF_HIP_LIB") or os.path.join(_HERE, "libdcf_hip.so")
 
 DCF_OK = 0
-EVAL_AUTO, EVAL_TTABLE, EVAL_BITSLICED, EVAL_HYBRID, EVAL_STREAM = 0, 1, 2, 3, 4
+EVAL_AUTO, EVAL_TTABLE, EVAL_STREAM = 0, 1, 4
 ERRORS = {
     -1: "DCF_ERR_ARG",
     -2: "DCF_ERR_LAMBDA",
@@ -28,7 +28,7 @@ ERRORS = {
 # Every symbol the header declares (tests check the library exports all of them).
 EXPORTS = [
     "dcf_version", "dcf_last_error", "dcf_hirose_prg_new", "dcf_mmo_prg_new", "dcf_prg_kind", "dcf_prg_free", "dcf_prg_lambda", "dcf_prg_set_eval_mode",
-    "dcf_prg_set_hybrid_split", "dcf_prg_set_stream_hybrid", "dcf_prg_last_eval_blocks", "dcf_prg_set_prefix_levels", "dcf_eval_prefix_levels",
+    "dcf_prg_last_eval_blocks", "dcf_prg_set_prefix_levels", "dcf_eval_prefix_levels",
     "dcf_eval_keys_per_launch", "dcf_cwb_bytes", "dcf_cwb_np1_offset", "dcf_gen", "dcf_eval", "dcf_prg_gen",
     "dcf_gen_batch_device", "dcf_eval_device", "dcf_eval_multikey_device", "dcf_eval_full_domain_device",
     "dcf_share_bincode_bytes", "dcf_share_to_bincode", "dcf_share_from_bincode",
@@ -73,8 +73,6 @@ def load(path: str = LIB_PATH):
         "dcf_prg_free": ([vp], None),
         "dcf_prg_lambda": ([vp], sz),
         "dcf_prg_set_eval_mode": ([vp, i], i),
-        "dcf_prg_set_hybrid_split": ([vp, i, i], i),
-        "dcf_prg_set_stream_hybrid": ([vp, ctypes.c_uint, i], i),
         "dcf_prg_last_eval_blocks": ([vp, ctypes.POINTER(ctypes.c_uint64)], i),
         "dcf_prg_set_prefix_levels": ([vp, i], i),
         "dcf_eval_prefix_levels": ([vp, sz, sz, sz], i),

@@ -36,12 +36,10 @@
 #include "kernels16.h"
 #include "kernels_lat.h"
 #include "kernels_wide.h"
-#include "kernels_bs.h"
 #include "kernels_stream.h"
 #include "kernels_mmo.h"
 #include "kernels_mmo_wide.h"
 #include "kernels_wide_stream.h"
-#include "kernels_shybrid.h"
 
 namespace {
 
@@ -114,8 +112,6 @@ struct Workspace {
   uint32_t dig_levels = 0;
   uint8_t* d_kdig = nullptr;  // LAMBDA = 16 multi-key stream eval: key-major CW digest
   size_t kdig_bytes = 0;
-  void* d_slabs = nullptr;    // per-wave s/v slabs of the hybrid kernels (MEM variant)
-  size_t slab_bytes = 0;
   uint8_t* d_pfx = nullptr;   // shared-prefix table + its build buffers / per-key top trees
   size_t pfx_bytes = 0;
   uint8_t* d_mkey = nullptr;  // dcf_eval_multi_gpu_device: this device's copy of the key (CWB + s0)
@@ -159,15 +155,10 @@ struct dcf_prg {
   uint4* d_rk2 = nullptr;     // LAMBDA >= 32 stream head: AES-256 schedules of ciphers 0 and 17
   uint4* d_rk0 = nullptr;     // LAMBDA = 16 stream eval: AES-256 schedule of cipher 0 (15 x 16 B)
   uint32_t* d_tab = nullptr;  // T0..T3 (4 KiB) on the device
-  uint4* d_km = nullptr;      // bitsliced round-key masks of cipher 0 (15 x 4 x 8 uint4)
   std::vector<uint8_t> key_blob;  // the PRG keys as given (multi-GPU calls check every prg holds the same)
   // Settings (read once per call; atomics so a setter racing a call is not a data race).
   std::atomic<int> eval_mode{DCF_EVAL_AUTO};
   std::atomic<int> prefix_levels{-1};     // shared-prefix table depth: -1 auto, 0 off
-  std::atomic<int> hybrid_tt_waves{13};   // T-table waves per hybrid workgroup (r01 sweep: 13 of 16 best)
-  std::atomic<int> hybrid_mem{1};         // 1: 16-wave workgroups with s/v slabs; 0: 12 waves, s/v in registers
-  std::atomic<uint32_t> shy_mask{0x7777}; // stream-hybrid: stream waves (bit w = wave w)
-  std::atomic<int> shy_prio{0};           // stream-hybrid: raise the stream waves' issue priority
   std::atomic<size_t> prefix_cap{0};      // dcf_prg_set_prefix_max_bytes (0 = none)
   std::atomic<int> timing{0};             // dcf_prg_set_phase_timing
   // Workspace pool (see Workspace).
@@ -181,14 +172,12 @@ namespace {
 // The prg's settings as one call sees them: read once, when the call leases its workspace (the
 // setters may race a call; no decision inside a call reads a setting twice).
 struct Cfg {
-  int mode, prefix_levels, hyb_tt, hyb_mem, shy_prio;
-  uint32_t shy_mask;
+  int mode, prefix_levels;
   size_t prefix_cap;
   bool timing;
 };
 Cfg snapshot(const dcf_prg* p) {
-  return Cfg{p->eval_mode.load(), p->prefix_levels.load(), p->hybrid_tt_waves.load(), p->hybrid_mem.load(),
-             p->shy_prio.load(), p->shy_mask.load(), p->prefix_cap.load(), p->timing.load() != 0};
+  return Cfg{p->eval_mode.load(), p->prefix_levels.load(), p->prefix_cap.load(), p->timing.load() != 0};
 }
 
 // A workspace leased for one call.  `st` is the stream the call's device work is queued on
@@ -367,7 +356,7 @@ uint32_t small_prefix_depth(const dcf_prg* p, const Cfg& c, size_t n_bytes) {
 // Auto: log2(m) - 1, at most 22 (two 336 MB node buffers at 2^22), none below 8.
 constexpr uint32_t kWidePrefixMax = 22;
 uint32_t wide_prefix_depth(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t m) {
-  if (p->lambda <= 16 || p->kind != 0 || c.prefix_levels == 0 || c.mode == DCF_EVAL_TTABLE || m == 0) return 0;
+  if (p->lambda <= 16 || p->kind != 0 || c.prefix_levels == 0 || m == 0) return 0;
   uint32_t d;
   if (c.prefix_levels > 0) {
     d = std::min((uint32_t)c.prefix_levels, 30u);
@@ -618,11 +607,9 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
   if (rc) return rc;
   uint32_t* tvec = reinterpret_cast<uint32_t*>(w->d_ws);
   WidePrefix wpf{nullptr, 0u};
-  const int mode = c.mode;
   for (uint64_t off = 0; off < m; off += chunk) {
     const uint64_t cnt = (m - off < chunk) ? m - off : chunk;
-    const dim3 grid((unsigned)grid_for(cnt, p->cus));
-    if (mode != DCF_EVAL_TTABLE) {  // stream head: 2.5 AES blocks per level instead of 4
+    {  // stream head: 2.5 AES blocks per level instead of 4
       HIP_TRY(hipMemsetAsync(w->d_ctr, 0, 8, st));  // the pass's work counter (the block count stays)
       if (off == 0) {  // CW digest of this key (bytes [0,32) of each level's cw_s / cw_v, and cw_t)
         if (w->dig_levels < nlev) {
@@ -654,14 +641,7 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
       else if (xreg) DCF_WHS(false, true);
       else DCF_WHS(false, false);
 #undef DCF_WHS
-    } else if (lam == 32)
-      hipLaunchKernelGGL(k_eval_wide_head<true>, grid, dim3(kBlock), 0, st, p->d_tab, p->rk[0], p->rk[17], cws, cwv,
-                         cwt, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes, lam, K, key, cnt,
-                         ys + off * lam, tvec, tw);
-    else
-      hipLaunchKernelGGL(k_eval_wide_head<false>, grid, dim3(kBlock), 0, st, p->d_tab, p->rk[0], p->rk[17], cws,
-                         cwv, cwt, np1, s0, (uint32_t)party, xs + off * n_bytes, (uint32_t)n_bytes, lam, K, key, cnt,
-                         ys + off * lam, tvec, tw);
+    }
     HIP_TRY(hipGetLastError());
     if (lam > 32) {
       rc = run_tail(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus, cnt);
@@ -675,9 +655,15 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
 // several keys per pass: one key-major CW digest, one stream-head launch (each point's key =
 // point / ppk) and one tail launch whose workgroups build the tables of their own key.  For
 // ppk <= kWideBatchPpk (larger keys amortise their own launches: eval_wide per key).  No shared
-// prefix; the lockstep head (DCF_EVAL_TTABLE) and the MMO PRG keep the per-key path.
+// prefix; the MMO PRG keeps the per-key path.
 constexpr uint64_t kWideBatchPpk = 32768;
 constexpr uint64_t kWideBatchKeys = 4096;  // keys per pass: tail grid rows (keys x <= 8 ranges) <= 32768
+// The multi-key shapes eval_wide_batch takes: several keys of few points each, Hirose PRG, and no
+// forced prefix depth (a forced depth runs the per-key passes, which build one table per key).
+bool wide_batched(const dcf_prg* p, const Cfg& c, uint64_t num_keys, uint64_t ppk) {
+  return num_keys > 1 && ppk > 0 && p->kind == 0 && ppk <= kWideBatchPpk && c.prefix_levels <= 0;
+}
+
 int eval_wide_batch(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64_t ppk, int party,
                     const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys, hipStream_t st) {
   const uint32_t lam = (uint32_t)p->lambda, nlev = (uint32_t)(8 * n_bytes);
@@ -687,7 +673,10 @@ int eval_wide_batch(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64
   const uint8_t* cwt = cwb + 2 * n * K * lam;
   const uint8_t* np1 = cwb + dcf_cwb_np1_offset(n_bytes, lam, K);
   const uint32_t tw = t_words(nlev);
-  const uint64_t kp = std::max<uint64_t>(1, std::min<uint64_t>({K, wide_chunk_points(tw) / ppk, kWideBatchKeys}));
+  // keys per pass; the digest's uint4 index 4 * (key * nlev + level) and dig_levels are 32-bit
+  const uint64_t kdig = std::max<uint64_t>(1, (0xFFFFFFFFull / 4u) / nlev);
+  const uint64_t kp =
+      std::max<uint64_t>(1, std::min<uint64_t>({K, wide_chunk_points(tw) / ppk, kWideBatchKeys, kdig}));
   const size_t tvb = ((kp * ppk * tw * 4 + 255) & ~(size_t)255) + 256;
   if (int rc = ensure_ws(w, tvb, st)) return rc;
   if (w->dig_levels < kp * nlev) {
@@ -825,15 +814,8 @@ int dcf_hirose_prg_new(const uint8_t* keys, size_t cipher_n, size_t lambda, int 
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     p->cus = prop.multiProcessorCount;
-  // Bitsliced key masks: word e of uint4 (16 r + 4 c + q) = -(bit 4q+e of column c of round key r).
-  std::vector<uint32_t> km(15 * 4 * 8 * 4);
-  for (int r = 0; r < 15; r++)
-    for (int c = 0; c < 4; c++)
-      for (int i = 0; i < 32; i++) km[((r * 4 + c) * 8) * 4 + i] = ((p->rk[0].w[4 * r + c] >> i) & 1u) ? ~0u : 0u;
   hipError_t e = hipMalloc(&p->d_tab, sizeof(g_tab));
   if (e == hipSuccess) e = hipMemcpy(p->d_tab, g_tab, sizeof(g_tab), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&p->d_km, km.size() * 4);
-  if (e == hipSuccess) e = hipMemcpy(p->d_km, km.data(), km.size() * 4, hipMemcpyHostToDevice);
   // device copies of the schedules the kernels read per round: cipher 0 (LAMBDA = 16 stream /
   // pair / table-build kernels) and, at LAMBDA >= 32, ciphers 0 and 17 (the wide stream head)
   if (e == hipSuccess) e = hipMalloc(&p->d_rk0, sizeof(RoundKeys));
@@ -896,7 +878,7 @@ static void free_workspace(Workspace* w) {
     if (s) (void)hipStreamSynchronize(s);
   if (w->aux) (void)hipStreamSynchronize(w->aux);
   if (w->pending) (void)hipEventSynchronize(w->done);  // the last device call's kernels
-  for (void* b : {(void*)w->d_ctr, (void*)w->d_ws, (void*)w->d_dig, (void*)w->d_kdig, w->d_slabs, (void*)w->d_pfx,
+  for (void* b : {(void*)w->d_ctr, (void*)w->d_ws, (void*)w->d_dig, (void*)w->d_kdig, (void*)w->d_pfx,
                   (void*)w->d_mkey, (void*)w->d_stage})
     if (b) (void)hipFree(b);
   if (w->h_stage) (void)hipHostFree(w->h_stage);
@@ -920,7 +902,7 @@ void dcf_prg_free(dcf_prg* p) {
   {
     DeviceGuard dg(p->device);
     for (Workspace* w : p->all_ws) free_workspace(w);
-    for (void* b : {(void*)p->d_tab, (void*)p->d_km, (void*)p->d_rk128, (void*)p->d_rk2, (void*)p->d_rk0})
+    for (void* b : {(void*)p->d_tab, (void*)p->d_rk128, (void*)p->d_rk2, (void*)p->d_rk0})
       if (b) (void)hipFree(b);
   }
   delete p;
@@ -930,7 +912,8 @@ size_t dcf_prg_lambda(const dcf_prg* p) { return p ? p->lambda : 0; }
 
 int dcf_prg_set_eval_mode(dcf_prg* p, int mode) {
   if (!p) return fail(DCF_ERR_ARG, "null prg");
-  if (mode < DCF_EVAL_AUTO || mode > DCF_EVAL_STREAM_HYBRID) return fail(DCF_ERR_ARG, "bad eval mode");
+  if (mode != DCF_EVAL_AUTO && mode != DCF_EVAL_TTABLE && mode != DCF_EVAL_STREAM)
+    return fail(DCF_ERR_ARG, "bad eval mode (DCF_EVAL_AUTO, DCF_EVAL_TTABLE or DCF_EVAL_STREAM)");
   p->eval_mode = mode;
   return DCF_OK;
 }
@@ -952,19 +935,11 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   const bool small = total < (uint64_t)p->cus * kBlock * 2;
   if (p->kind == 1 && p->lambda > 16) return 0;  // MMO at LAMBDA >= 32: no shared prefix (head/tail per block)
   if (p->kind == 1) return small && c.prefix_levels < 0 ? 0 : (int)prefix_depth(p, c, n_bytes, num_keys, total);
-  if (p->lambda > 16) return (int)wide_prefix_depth(p, c, n_bytes, points_per_key);
+  if (p->lambda > 16)  // batched keys (eval_wide_batch) build no table; per-key passes do
+    return wide_batched(p, c, num_keys, points_per_key) ? 0 : (int)wide_prefix_depth(p, c, n_bytes, points_per_key);
   if (c.mode == DCF_EVAL_AUTO && small) return num_keys == 1 ? (int)small_prefix_depth(p, c, n_bytes) : 0;
-  if (c.mode != DCF_EVAL_AUTO && c.mode != DCF_EVAL_STREAM && c.mode != DCF_EVAL_STREAM_HYBRID) return 0;
+  if (c.mode != DCF_EVAL_AUTO && c.mode != DCF_EVAL_STREAM) return 0;
   return (int)prefix_depth(p, c, n_bytes, num_keys, total);
-}
-
-int dcf_prg_set_hybrid_split(dcf_prg* p, int ttable_waves, int slab_variant) {
-  if (!p) return fail(DCF_ERR_ARG, "null prg");
-  if (ttable_waves < 0 || ttable_waves > 16) return fail(DCF_ERR_ARG, "ttable_waves must be in [0, 16]");
-  if (slab_variant != 0 && slab_variant != 1) return fail(DCF_ERR_ARG, "slab_variant must be 0 or 1");
-  p->hybrid_tt_waves = ttable_waves;
-  p->hybrid_mem = slab_variant;
-  return DCF_OK;
 }
 
 int dcf_prg_set_prefix_max_bytes(dcf_prg* p, size_t max_bytes) {
@@ -977,14 +952,13 @@ size_t dcf_prg_device_bytes(const dcf_prg* p) {
   if (!p) return 0;
   size_t b = 0;
   if (p->d_tab) b += sizeof(g_tab);
-  if (p->d_km) b += 15 * 4 * 8 * 16;
   if (p->d_rk128) b += p->rk128_count * 44 * 4;
   if (p->d_rk2) b += 2 * sizeof(RoundKeys);
   if (p->d_rk0) b += sizeof(RoundKeys);
   std::lock_guard<std::mutex> g(const_cast<dcf_prg*>(p)->pool_mu);
   for (const Workspace* w : p->all_ws) {
     if (w->d_ctr) b += kCtrBytes;
-    b += (size_t)w->dig_levels * 65 + w->kdig_bytes + w->ws_bytes + w->pfx_bytes + w->slab_bytes +
+    b += (size_t)w->dig_levels * 65 + w->kdig_bytes + w->ws_bytes + w->pfx_bytes +
          w->d_stage_bytes + w->mkey_bytes;
   }
   return b;
@@ -1014,14 +988,30 @@ static bool ws_idle(const dcf_prg* p, const Workspace* w) {
 int dcf_prg_last_eval_blocks(dcf_prg* p, uint64_t* blocks) {
   if (!p || !blocks) return fail(DCF_ERR_ARG, "null argument");
   *blocks = 0;
+  Workspace* w = nullptr;
+  {  // take the workspace out of the pool (as a lease does), so the drain below holds no lock
+    std::lock_guard<std::mutex> g(p->pool_mu);
+    w = p->last_ws.load();
+    if (!w || !w->d_ctr) return DCF_OK;
+    auto it = std::find(p->free_ws.begin(), p->free_ws.end(), w);
+    if (it == p->free_ws.end()) return fail(DCF_ERR_ARG, "the last eval's workspace is in use by another call");
+    p->free_ws.erase(it);
+  }
+  int rc = DCF_OK;
+  {
+    DeviceGuard dg(p->device);
+    hipError_t e = w->pending ? hipEventSynchronize(w->done) : hipSuccess;
+    if (e == hipSuccess) e = hipMemcpy(blocks, w->d_ctr + 2, sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      rc = fail(DCF_ERR_HIP, std::string("dcf_prg_last_eval_blocks: ") + hipGetErrorString(e));
+    } else {
+      w->pending = false;  // drained
+    }
+  }
   std::lock_guard<std::mutex> g(p->pool_mu);
-  Workspace* w = p->last_ws.load();
-  if (!w || !w->d_ctr) return DCF_OK;
-  if (!ws_idle(p, w)) return fail(DCF_ERR_ARG, "the last eval's workspace is in use by another call");
-  DeviceGuard dg(p->device);
-  if (w->pending) HIP_TRY(hipEventSynchronize(w->done));
-  HIP_TRY(hipMemcpy(blocks, w->d_ctr + 2, sizeof(uint64_t), hipMemcpyDeviceToHost));
-  return DCF_OK;
+  p->free_ws.push_back(w);
+  return rc;
 }
 
 int dcf_prg_set_phase_timing(dcf_prg* p, int on) {
@@ -1061,16 +1051,6 @@ int dcf_prg_trim(dcf_prg* p) {
   return (int)idle.size();
 }
 
-int dcf_prg_set_stream_hybrid(dcf_prg* p, unsigned ttable_wave_mask, int priority) {
-  if (!p) return fail(DCF_ERR_ARG, "null prg");
-  if (ttable_wave_mask > 0xFFFFu || __builtin_popcount(ttable_wave_mask) < 16 - kShybridXlSlots)
-    return fail(DCF_ERR_ARG, "ttable_wave_mask: 16 bits, at least 4 set");
-  if (priority != 0 && priority != 1) return fail(DCF_ERR_ARG, "priority must be 0 or 1");
-  p->shy_mask = ttable_wave_mask;
-  p->shy_prio = priority;
-  return DCF_OK;
-}
-
 // Tiny batches run the latency kernels of kernels_lat.h (one AES column per lane).  Thresholds:
 // scripts/lat_sweep.py / row_threshold.py (DESIGN.md §4 "Latency kernels", profiles/AB_LOG.md).
 constexpr uint64_t kEvalOctMax = 32768;  // points (one key) up to which auto-mode eval runs k_eval16_oct
@@ -1091,17 +1071,6 @@ static bool oct_eval(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t nu
 }
 static bool col_gen(const dcf_prg* p, size_t n_bytes, uint64_t num_keys) {
   return p->kind == 0 && p->lambda == 16 && num_keys <= kGenColMax && 8 * n_bytes <= kColMaxLevels;
-}
-
-// Per-wave scratch slabs (bitsliced v) for every 16-wave workgroup of the hybrid kernels.
-static int ensure_slabs(dcf_prg* p, Workspace* w, hipStream_t st) {
-  const size_t need = (size_t)p->cus * 16 * kSlabUint4 * sizeof(uint4);
-  size_t have = w->slab_bytes;
-  uint8_t* b = (uint8_t*)w->d_slabs;
-  const int rc = grow(&b, &have, need, st);
-  w->d_slabs = b;
-  w->slab_bytes = have;
-  return rc;
 }
 
 static int gen_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, const uint8_t* alpha,
@@ -1128,7 +1097,7 @@ static int gen_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, con
     if (rc) return rc;
     for (uint64_t k0 = 0; k0 < num_keys; k0 += chunk) {
       const uint64_t cnt = (num_keys - k0 < chunk) ? num_keys - k0 : chunk;
-      hipLaunchKernelGGL(k_gen_wide, dim3((unsigned)cnt), dim3(kBlock), 0, st, p->d_tab, p->rk[0], p->rk[17], alpha,
+      hipLaunchKernelGGL(k_gen_wide, dim3((unsigned)cnt), dim3(kBlock), 0, st, p->d_tab, p->d_rk2, alpha,
                          beta, s0_0, s0_1, (uint32_t)bound, (uint32_t)n_bytes, (uint64_t)num_keys, k0, (uint32_t)lam,
                          cws, cwv, cwt, np1, w->d_ws);
       HIP_TRY(hipGetLastError());
@@ -1234,7 +1203,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
   const size_t n = 8 * n_bytes, lam = p->lambda;
   if (lam > 16) {  // head/tail pipeline: keys with few points batched, else per key
     phase_mark(p, L, 1);
-    if (num_keys > 1 && ppk > 0 && p->kind == 0 && c.mode != DCF_EVAL_TTABLE && ppk <= kWideBatchPpk)
+    if (wide_batched(p, c, num_keys, ppk))
       return eval_wide_batch(p, w, n_bytes, num_keys, ppk, party, cwb, s0s, xs, ys, st);
     for (uint64_t k = 0; k < num_keys; ++k) {
       int rc = p->kind == 1 ? eval_mmo_wide(p, w, n_bytes, num_keys, k, party, cwb, s0s + k * lam,
@@ -1273,7 +1242,6 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     HIP_TRY(hipGetLastError());
     return DCF_OK;
   }
-  const bool bs_ok = (num_keys == 1 && n_bytes <= 16);
   int mode = c.mode;
   if (oct_eval(p, c, n_bytes, num_keys, total) && total <= kEvalRowMax) {
     // The smallest batches: 32 lanes per point, one table lookup per lane and AES round
@@ -1300,7 +1268,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
   // pass: 8N passes) beats the stream engine (~12N passes); it runs on a lane pair per point
   // (k_eval16_pair: the even lane encrypts A, the odd lane B), spread over every CU with
   // workgroups just big enough (C1).  Larger batches: the stream engine, single key or many
-  // (C3: 407 M evals/s vs 353 M hybrid, 332 M lockstep T-table; C5 with the key-major digest).
+  // (C3 r01: 407 M evals/s vs 332 M lockstep T-table; C5 with the key-major digest).  DCF_EVAL_TTABLE
+  // forces the lockstep walk (k_eval16: A and B every level), which auto takes for many keys at N > 32.
   if (mode == DCF_EVAL_AUTO && total < (uint64_t)p->cus * kBlock * 2) {
     PrefixTable spf{nullptr, 0u};
     if (num_keys == 1) {
@@ -1330,56 +1299,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
   if (mode == DCF_EVAL_AUTO) mode = (num_keys == 1 || n_bytes <= 32) ? DCF_EVAL_STREAM : DCF_EVAL_TTABLE;
   if (mode == DCF_EVAL_STREAM && num_keys > 1 && n_bytes > 32)
     return fail(DCF_ERR_UNSUPPORTED, "multi-key stream eval: N <= 32");
-  // Single-key T-table eval also runs in the hybrid kernel, with every wave on
-  // the T-table engine: its 512-point work units measured 13 % faster than
-  // k_eval16<0>'s grid-stride loop (r01 sweep, 331.7 vs 292 M evals/s).
-  const bool tt_single = (mode == DCF_EVAL_TTABLE && bs_ok);
-  if (mode == DCF_EVAL_HYBRID || tt_single) {
-    if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "hybrid eval: single key, N <= 16");
-    const bool mem = tt_single || c.hyb_mem != 0;
-    const int waves = mem ? 16 : kHybridWaves;
-    int ntt = tt_single ? 16 : c.hyb_tt;
-    if (mem && ntt < 1) ntt = 1;  // 15 LDS x-slots for bitsliced waves
-    if (ntt > waves) ntt = waves;
-    const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
-    uint64_t blocks = (units + waves - 1) / waves;
-    if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
-    if (int rc = ensure_slabs(p, w, st)) return rc;
-    uint4* slabs = reinterpret_cast<uint4*>(w->d_slabs);
-    phase_mark(p, L, 1);
-    const dim3 g((unsigned)blocks), b((unsigned)(waves * 64));
-#define DCF_HYB(XA, MEM)                                                                                   \
-  hipLaunchKernelGGL((k_eval16_hybrid<XA, MEM>), g, b, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,       \
-                     (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, (uint32_t)ntt, \
-                     w->d_ctr, slabs, p->d_km, (uint4*)ys)
-    const bool xa = n_bytes % 4 == 0;
-    if (xa && mem) DCF_HYB(true, true);
-    else if (xa) DCF_HYB(true, false);
-    else if (mem) DCF_HYB(false, true);
-    else DCF_HYB(false, false);
-#undef DCF_HYB
-  } else if (mode == DCF_EVAL_STREAM_HYBRID) {
-    if (!(num_keys == 1 && n_bytes % 4 == 0 && n_bytes <= 16))
-      return fail(DCF_ERR_UNSUPPORTED, "stream-hybrid eval: single key, N % 4 == 0, N <= 16");
-    const uint64_t units = (total + kWavePoints - 1) / kWavePoints;
-    if (total >= (1ull << 31)) return fail(DCF_ERR_UNSUPPORTED, "stream-hybrid eval: 2^31 points or more");
-    int rc = ensure_slabs(p, w, st);
-    if (rc) return rc;
-    PrefixTable pf{nullptr, 0u};
-    const uint32_t d = prefix_depth(p, c, n_bytes, num_keys, total);
-    if (d) {
-      rc = try_prefix(p, c, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &pf, st);
-      if (rc) return rc;
-      w->last_prefix = pf.levels;
-    }
-    phase_mark(p, L, 1);
-    uint64_t blocks = (units + 15) / 16;
-    if (blocks > (uint64_t)p->cus) blocks = (uint64_t)p->cus;
-    hipLaunchKernelGGL(k_eval16_shybrid, dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,
-                       (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, w->d_ctr,
-                       (uint4*)ys, pf, c.shy_mask, (uint32_t)c.shy_prio, reinterpret_cast<uint4*>(w->d_slabs), p->d_km,
-                       p->d_rk0);
-  } else if (mode == DCF_EVAL_STREAM) {
+  if (mode == DCF_EVAL_STREAM) {
     constexpr int NS = 2;  // streams per lane
     const bool xreg = n_bytes % 4 == 0 && n_bytes <= 16, multi = num_keys > 1;
     if (multi && ppk >= (1ull << 31)) return fail(DCF_ERR_UNSUPPORTED, "multi-key stream eval: 2^31 points per key or more");
@@ -1414,24 +1334,40 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       // call's stream; the walk waits for both.
       if (int rc = grow(&w->d_kdig, &w->kdig_bytes, (size_t)num_keys * n * 33, st)) return rc;
       const bool fork = pf.levels != 0;
+      // Once the top trees are queued on aux, every exit from this block — the normal one and an
+      // error return — joins aux into the call's stream (the walk and the lease's `done` event must
+      // cover them: the next user of this workspace overwrites d_pfx / d_ctr); if the join cannot
+      // be queued, aux is drained on the host instead.
+      struct AuxJoin {
+        Workspace* w;
+        hipStream_t st;
+        bool armed = false;
+        ~AuxJoin() {
+          if (!armed) return;
+          if (hipEventRecord(w->aux_ev[1], w->aux) != hipSuccess || hipStreamWaitEvent(st, w->aux_ev[1], 0) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipStreamSynchronize(w->aux);
+          }
+        }
+      } join{w, st};
       if (fork) {
         if (!w->aux) HIP_TRY(hipStreamCreateWithFlags(&w->aux, hipStreamNonBlocking));
         for (auto& e : w->aux_ev)
           if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(w->aux_ev[0], st));
         HIP_TRY(hipStreamWaitEvent(w->aux, w->aux_ev[0], 0));
+        join.armed = true;
         hipLaunchKernelGGL(k_mk_prefix16<true>,
                            dim3((unsigned)(((num_keys << kMkPfxRoot) + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            w->aux, p->d_tab, p->rk[0], cws, cwv, cwt, (const uint4*)s0s, (uint32_t)party,
                            (uint64_t)num_keys, (uint4*)w->d_pfx, p->d_rk0, w->d_ctr);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(w->aux_ev[1], w->aux));
       }
       hipLaunchKernelGGL(k_cw_keymajor, dim3((unsigned)((num_keys + kKmKeys - 1) / kKmKeys), (unsigned)((n + kKmLevs - 1) / kKmLevs)),
                          dim3(kKmThreads), 0, st, cws, cwv, cwt, (uint32_t)n, (uint64_t)num_keys, (uint4*)w->d_kdig,
                          w->d_kdig + (size_t)num_keys * n * 32);
       HIP_TRY(hipGetLastError());
-      if (fork) HIP_TRY(hipStreamWaitEvent(st, w->aux_ev[1], 0));
+      // (the join runs here, as `join` leaves scope: the walk below waits for the top trees)
       scs = (const uint4*)w->d_kdig;
       sct = w->d_kdig + (size_t)num_keys * n * 32;
     }
@@ -1491,21 +1427,6 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
 #undef DCF_STREAM
       HIP_TRY(hipGetLastError());
     }
-  } else if (mode == DCF_EVAL_BITSLICED) {
-    if (!bs_ok) return fail(DCF_ERR_UNSUPPORTED, "bitsliced eval: single key, N <= 16");
-    if (int rc = ensure_slabs(p, w, st)) return rc;  // cus x 16 wave slabs: one per resident wave
-    phase_mark(p, L, 1);
-    const uint64_t waves = (total + kWavePoints - 1) / kWavePoints;
-    uint64_t blocks = (waves + 3) / 4;
-    const uint64_t cap = (uint64_t)p->cus * 4;  // 4 workgroups of 4 waves per CU (<= 128 VGPRs)
-    if (blocks > cap) blocks = cap;
-    uint4* slabs = reinterpret_cast<uint4*>(w->d_slabs);
-    if (n_bytes % 4 == 0)
-      hipLaunchKernelGGL(k_eval16_bs<true>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
-                         (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, slabs, (uint4*)ys);
-    else
-      hipLaunchKernelGGL(k_eval16_bs<false>, dim3((unsigned)blocks), dim3(256), 0, st, p->d_km, cws, cwv, cwt, np1,
-                         (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)total, slabs, (uint4*)ys);
   } else {  // lockstep T-table, 64-point units from the work counter
     if ((total + 63) / 64 > 0xFFFFFFFFull) return fail(DCF_ERR_UNSUPPORTED, "more than 2^32 64-point units");
     phase_mark(p, L, 1);
@@ -1799,7 +1720,7 @@ static int host_prg_gen(dcf_prg* p, Lease& L, const uint8_t* seeds, size_t m, ui
                        (const uint4*)d, (uint64_t)m, d + so);
   else
     hipLaunchKernelGGL(k_prg_wide, dim3((unsigned)std::min<uint64_t>((m * (lam / 16) + 255) / 256, 65535)),
-                       dim3(256), 0, sc, p->d_tab, p->rk[0], p->rk[17], (const uint8_t*)d, (uint64_t)m, (uint32_t)lam,
+                       dim3(256), 0, sc, p->d_tab, p->d_rk2, (const uint8_t*)d, (uint64_t)m, (uint32_t)lam,
                        d + so);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(h + so, d + so, m * row, hipMemcpyDeviceToHost, sc));

@@ -17,7 +17,7 @@ namespace {
 //   L = ((A^s)&M, (B^~s)&M, lsb(A^s)[0]),  R = (s&M, ~s&M, lsb(B^~s)[0])
 // ------------------------------------------------------------------------
 // One point, one lane: returns y for point gg of key `key` (the whole
-// lib.rs:166-193 closure).  Used by k_eval16 and by the hybrid kernel.
+// lib.rs:166-193 closure).  Used by k_eval16.
 __device__ __forceinline__ uint4 tt_eval_one(const uint32_t* lds, uint32_t lc, const RoundKeys& rk,
                                              const uint4* __restrict__ cw_s, const uint4* __restrict__ cw_v,
                                              const uint8_t* __restrict__ cw_t, const uint4 np, const uint4 sv,

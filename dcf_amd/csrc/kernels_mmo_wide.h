@@ -181,16 +181,25 @@ __global__ __launch_bounds__(kBlock, 1) void k_mmo_wide_gen(
         t0 = w & 1u; t1 = (w >> 1) & 1u; tlcw = (w >> 2) & 1u; trcw = (w >> 3) & 1u;
         tl0 = tr0 = tl1 = tr1 = 0u;
       }
-      const uint32_t lose = a ? 0u : 2u, keep = a ? 2u : 0u;  // output index of the lose / keep side's s
+      // the lose side is left (outputs 0, 1) when alpha_i = 1, right (2, 3) otherwise: picked by a
+      // select per word (a runtime index into o[][][] would put the array on the stack)
       const uint32_t m0 = 0u - t0, m1 = 0u - t1;
       uint32_t scw[4], vcw[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        scw[q] = o[0][lose][q] ^ o[1][lose][q];                                      // lib.rs:112
-        vcw[q] = o[0][lose + 1][q] ^ o[1][lose + 1][q] ^ va[q] ^ (bm & bw[q]);       // lib.rs:113-125
-        va[q] ^= o[0][keep + 1][q] ^ o[1][keep + 1][q] ^ vcw[q];                     // lib.rs:126-129
-        s[0][q] = o[0][keep][q] ^ (m0 & scw[q]);                                     // lib.rs:139-148
-        s[1][q] = o[1][keep][q] ^ (m1 & scw[q]);
+        uint32_t ls[2], lv[2], ks[2], kv[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          ls[p] = a ? o[p][0][q] : o[p][2][q];
+          lv[p] = a ? o[p][1][q] : o[p][3][q];
+          ks[p] = a ? o[p][2][q] : o[p][0][q];
+          kv[p] = a ? o[p][3][q] : o[p][1][q];
+        }
+        scw[q] = ls[0] ^ ls[1];                             // lib.rs:112
+        vcw[q] = lv[0] ^ lv[1] ^ va[q] ^ (bm & bw[q]);      // lib.rs:113-125
+        va[q] ^= kv[0] ^ kv[1] ^ vcw[q];                    // lib.rs:126-129
+        s[0][q] = ks[0] ^ (m0 & scw[q]);                    // lib.rs:139-148
+        s[1][q] = ks[1] ^ (m1 & scw[q]);
       }
       if (live) {
         const uint64_t ci = ((uint64_t)lev * num_keys + k) * lam + 16ull * j;

@@ -1,5 +1,5 @@
 // kernels_stream.h — LAMBDA = 16 eval with per-lane AES block scheduling.
-// Included by dcf_hip.hip only (after kernels_bs.h: reuses dequeue_unit).
+// Included by dcf_hip.hip only.
 //
 // At LAMBDA = 16 one level of the GGM walk (lib.rs:174-189 over prg.rs:42-73)
 // needs AES_K0(~s) = B on every step but AES_K0(s) = A only on a LEFT step:
@@ -31,6 +31,14 @@
 #include "kernels16.h"
 
 namespace {
+
+// One work unit from a global counter (reset by the host before the launch), taken by lane 0
+// of the wave and broadcast: the wave's streams (and the LAMBDA >= 32 head's) share it.
+__device__ __forceinline__ uint32_t dequeue_unit(uint32_t* ctr) {
+  uint32_t u = 0;
+  if ((threadIdx.x & 63u) == 0) u = atomicAdd(ctr, 1u);
+  return __builtin_amdgcn_readfirstlane(u);
+}
 
 constexpr uint32_t kStreamUnit = 256;  // points per refill of a wave
 // Round keys: the single-key engine reads them per round from the device copy of the schedule

@@ -17,9 +17,9 @@
 //   c   = s0
 // except bit 0 of byte LAMBDA-1, which the PRG clears every level:
 //   W_l.bit = cw_v[l].bit ^ (l == n ? cw_s[l].bit : 0),  W_{n+1}.bit = np1.bit,  c.bit = 0.
-// Eval = k_eval_wide_head (AES walk over bytes [0,32), one lane per point,
-// emits y[0:32) and T) + k_eval_wide_tail (y[32:LAMBDA) as a GF(2)
-// combination of W rows, four-Russians tables of 4 rows in LDS).
+// Eval = k_eval_wide_head_stream (kernels_wide_stream.h: AES walk over bytes [0,32),
+// emits y[0:32) and T) + k_eval_wide_tail / k_eval_wide_tail2 (y[32:LAMBDA) as a GF(2)
+// combination of W rows, four-Russians tables in LDS).
 // tests/test_gpu_parity.py checks the result bit for bit against the oracle,
 // which runs the reference algorithm literally.
 #pragma once
@@ -42,16 +42,27 @@ __device__ __forceinline__ void load_tab4(uint32_t* t4, const uint32_t* __restri
   __syncthreads();
 }
 
-// AES-256 for a few lanes: plain T-table reads from a 4 KiB LDS copy.
-__device__ __forceinline__ void aes256_small(uint32_t (&w)[4], const RoundKeys& rk, const uint32_t* t4) {
+// The schedules of ciphers 0 and 17 (p->d_rk2: 2 x 15 round keys) into LDS, 60 words each: a
+// lane picks its cipher by a pointer, not by selecting between two by-value kernel arguments (which
+// put both 240-byte schedules on the stack: 484 B of scratch per lane, r04).
+__device__ __forceinline__ void load_rk2(uint32_t (*rks)[60], const uint4* __restrict__ rk2) {
+  if (threadIdx.x < 30) {
+    const uint4 k = rk2[threadIdx.x];
+    uint32_t* o = &rks[threadIdx.x / 15][4 * (threadIdx.x % 15)];
+    o[0] = k.x; o[1] = k.y; o[2] = k.z; o[3] = k.w;
+  }
+}
+
+// AES-256 for a few lanes: plain T-table reads from a 4 KiB LDS copy; rk: 60 round-key words (LDS).
+__device__ __forceinline__ void aes256_small(uint32_t (&w)[4], const uint32_t* rk, const uint32_t* t4) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) w[j] ^= rk.w[j];
+  for (int j = 0; j < 4; ++j) w[j] ^= rk[j];
   for (int r = 1; r < 14; ++r) {
     uint32_t o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       o[j] = t4[w[j] & 0xff] ^ t4[256 + ((w[(j + 1) & 3] >> 8) & 0xff)] ^
-             t4[512 + ((w[(j + 2) & 3] >> 16) & 0xff)] ^ t4[768 + (w[(j + 3) & 3] >> 24)] ^ rk.w[4 * r + j];
+             t4[512 + ((w[(j + 2) & 3] >> 16) & 0xff)] ^ t4[768 + (w[(j + 3) & 3] >> 24)] ^ rk[4 * r + j];
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[j] = o[j];
   }
@@ -60,107 +71,9 @@ __device__ __forceinline__ void aes256_small(uint32_t (&w)[4], const RoundKeys& 
   for (int j = 0; j < 4; ++j)
     o[j] = (t4[512 + (w[j] & 0xff)] & 0xffu) ^ (t4[768 + ((w[(j + 1) & 3] >> 8) & 0xff)] & 0xff00u) ^
            (t4[(w[(j + 2) & 3] >> 16) & 0xff] & 0xff0000u) ^ (t4[256 + (w[(j + 3) & 3] >> 24)] & 0xff000000u) ^
-           rk.w[56 + j];
+           rk[56 + j];
 #pragma unroll
   for (int j = 0; j < 4; ++j) w[j] = o[j];
-}
-
-// ------------------------------------------------------------------------
-// Head: one lane per point; bytes [0,32) of s and v, plus the t-vector.
-// MASK_HEAD: LAMBDA == 32, byte 31 is the last byte (cleared bit lives here).
-// ------------------------------------------------------------------------
-template <bool MASK_HEAD>
-__global__ __launch_bounds__(kBlock, 1) void k_eval_wide_head(
-    const uint32_t* __restrict__ tab, const RoundKeys rk0, const RoundKeys rk17, const uint8_t* __restrict__ cw_s,
-    const uint8_t* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint8_t* __restrict__ cw_np1,
-    const uint8_t* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
-    const uint32_t lam, const uint64_t num_keys, const uint64_t key, const uint64_t count, uint8_t* __restrict__ ys,
-    uint32_t* __restrict__ tvec, const uint32_t tw) {
-  // Key `key` of a num_keys-key CWB: row l of cw_s / cw_v at (l * num_keys + key) * lam.
-  __shared__ uint32_t lds[kLdsWords];
-  lds_fill_tables(lds, tab);
-  const uint32_t lc = lane_const();
-  const uint32_t nlev = 8u * nbytes;
-  const uint32_t nchunk = (nbytes + 3u) >> 2;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint32_t mlast = MASK_HEAD ? kMaskLast : 0xFFFFFFFFu;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < count; base += stride) {
-    const uint64_t g = base + (threadIdx.x & 63u);
-    const bool live = g < count;
-    const uint64_t gg = live ? g : count - 1;
-    uint32_t s[8], v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      s[j] = reinterpret_cast<const uint32_t*>(s0)[j];
-      v[j] = 0u;
-    }
-    uint32_t t = party;
-    uint32_t tacc = party, r = 1;  // t_r goes to bit (r & 3) of byte r >> 2
-    uint32_t* trow = tvec + gg * tw;
-    const uint8_t* x = xs + gg * nbytes;
-    uint32_t lev = 0;
-    for (uint32_t c = 0; c < nchunk; ++c) {
-      uint32_t cur = load_bits32(x, c, nbytes);
-      const uint32_t lend = min(32u, nlev - 32u * c);
-      for (uint32_t b = 0; b < lend; ++b, ++lev) {
-        uint32_t e0[2][4], e1[2][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          e0[0][j] = s[j];
-          e0[1][j] = ~s[j];
-          e1[0][j] = s[4 + j];
-          e1[1][j] = ~s[4 + j];
-        }
-        aes256_tt<2>(e0, rk0, lds, lc);   // A, B
-        aes256_tt<2>(e1, rk17, lds, lc);  // C, D
-        const uint64_t ro = ((uint64_t)lev * num_keys + key) * lam;
-        const uint4* cs4 = reinterpret_cast<const uint4*>(cw_s + ro);
-        const uint4* cv4 = reinterpret_cast<const uint4*>(cw_v + ro);
-        const uint4 cs0 = cs4[0], cs1 = cs4[1], cv0 = cv4[0], cv1 = cv4[1];
-        const uint32_t csw[8] = {cs0.x, cs0.y, cs0.z, cs0.w, cs1.x, cs1.y, cs1.z, cs1.w};
-        const uint32_t cvw[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
-        const uint32_t ct = cw_t[(uint64_t)lev * num_keys + key];
-        const uint32_t xb = cur >> 31;
-        cur <<= 1;
-        const uint32_t L = xb - 1u;  // all ones when going left
-        const uint32_t R = ~L;
-        const uint32_t tm = 0u - t;
-        const uint32_t tl = (e0[0][0] ^ s[0]) & 1u;
-        const uint32_t tr = (e0[1][0] ^ ~s[0]) & 1u;
-        const uint32_t tn = (xb ? tr : tl) ^ (t & (ct >> xb) & 1u);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {  // bytes [0,16): AES only on the left branch
-          v[j] ^= ((~s[j]) ^ (e0[1][j] & L)) ^ (tm & cvw[j]);
-          s[j] = (s[j] ^ (e0[0][j] & L)) ^ (tm & csw[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {  // bytes [16,32): AES only on the right branch
-          const uint32_t msk = (j == 3) ? mlast : 0xFFFFFFFFu;
-          v[4 + j] ^= (((~s[4 + j]) ^ (e1[1][j] & R)) & msk) ^ (tm & cvw[4 + j]);
-          s[4 + j] = ((s[4 + j] ^ (e1[0][j] & R)) & msk) ^ (tm & csw[4 + j]);
-        }
-        t = tn;
-        tacc |= t << (8u * ((r >> 2) & 3u) + (r & 3u));
-        if ((r & 15u) == 15u) {
-          if (live) trow[r >> 4] = tacc;
-          tacc = 0;
-        }
-        ++r;
-      }
-    }
-    if (live) {
-      if ((r & 15u) != 0) trow[r >> 4] = tacc;
-      const uint32_t tm = 0u - t;
-      const uint4* np4 = reinterpret_cast<const uint4*>(cw_np1 + key * lam);
-      const uint4 n0 = np4[0], n1 = np4[1];
-      const uint32_t nw[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
-      uint4* y4 = reinterpret_cast<uint4*>(ys + gg * lam);
-      y4[0] = make_uint4(v[0] ^ s[0] ^ (tm & nw[0]), v[1] ^ s[1] ^ (tm & nw[1]), v[2] ^ s[2] ^ (tm & nw[2]),
-                         v[3] ^ s[3] ^ (tm & nw[3]));
-      y4[1] = make_uint4(v[4] ^ s[4] ^ (tm & nw[4]), v[5] ^ s[5] ^ (tm & nw[5]), v[6] ^ s[6] ^ (tm & nw[6]),
-                         v[7] ^ s[7] ^ (tm & nw[7]));
-    }
-  }
 }
 
 // W row r (coefficient t_r), 16 bytes at byte offset `off` (>= 32), see file header.
@@ -660,7 +573,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
 // Per level 8 AES blocks (E0/E17 on s_p and ~s_p, p = 0, 1) by lanes 0..7.
 // ------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_gen_wide(
-    const uint32_t* __restrict__ tab, const RoundKeys rk0, const RoundKeys rk17, const uint8_t* __restrict__ alpha,
+    const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint8_t* __restrict__ alpha,
     const uint8_t* __restrict__ beta, const uint8_t* __restrict__ s0_0, const uint8_t* __restrict__ s0_1,
     const uint32_t bound, const uint32_t nbytes, const uint64_t num_keys, const uint64_t key_base, const uint32_t lam,
     uint8_t* __restrict__ cw_s, uint8_t* __restrict__ cw_v, uint8_t* __restrict__ cw_t, uint8_t* __restrict__ cw_np1,
@@ -668,7 +581,9 @@ __global__ __launch_bounds__(kBlock) void k_gen_wide(
   __shared__ uint32_t t4[1024];
   __shared__ uint32_t head[2][2][8];  // [buffer][party][word]: s_p bytes [0,32)
   __shared__ uint32_t eo[2][4][4];    // [party][A,B,C,D][word]
-  load_tab4(t4, tab);
+  __shared__ uint32_t rks[2][60];     // ciphers 0 and 17
+  load_rk2(rks, rk2);
+  load_tab4(t4, tab);  // its barrier publishes rks
   const uint64_t k = key_base + blockIdx.x;
   const uint32_t npieces = lam / 16, nlev = 8u * nbytes;
   uint4* w_s0 = reinterpret_cast<uint4*>(ws + (uint64_t)blockIdx.x * 3 * lam);
@@ -700,7 +615,7 @@ __global__ __launch_bounds__(kBlock) void k_gen_wide(
         const uint32_t sw = head[buf][p][4 * hi + j];
         w[j] = (which & 1u) ? ~sw : sw;
       }
-      aes256_small(w, hi ? rk17 : rk0, t4);
+      aes256_small(w, rks[hi], t4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) eo[p][which][j] = w[j];
     }
@@ -767,10 +682,12 @@ __global__ __launch_bounds__(kBlock) void k_gen_wide(
 }
 
 // PRG test hook at LAMBDA >= 32: one thread per (seed, 16-byte piece).
-__global__ __launch_bounds__(256) void k_prg_wide(const uint32_t* __restrict__ tab, const RoundKeys rk0,
-                                                  const RoundKeys rk17, const uint8_t* __restrict__ seeds,
+__global__ __launch_bounds__(256) void k_prg_wide(const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2,
+                                                  const uint8_t* __restrict__ seeds,
                                                   const uint64_t m, const uint32_t lam, uint8_t* __restrict__ out) {
   __shared__ uint32_t t4[1024];
+  __shared__ uint32_t rks[2][60];  // ciphers 0 and 17
+  load_rk2(rks, rk2);
   load_tab4(t4, tab);
   const uint32_t npieces = lam / 16;
   const uint64_t total = m * npieces;
@@ -788,8 +705,8 @@ __global__ __launch_bounds__(256) void k_prg_wide(const uint32_t* __restrict__ t
       e[1][j] = ~s[j];
     }
     if (q < 2) {
-      aes256_small(e[0], q ? rk17 : rk0, t4);
-      aes256_small(e[1], q ? rk17 : rk0, t4);
+      aes256_small(e[0], rks[q], t4);
+      aes256_small(e[1], rks[q], t4);
     }
     uint32_t o[4][4];
 #pragma unroll

@@ -11,8 +11,7 @@
 // per lane: the schedules of ciphers 0 and 17 sit in LDS beside the T-tables and
 // each round reads the lane's key with one ds_read_b128 (as kernels_mmo.h does;
 // key words in SGPRs would need a v_mov per use for the per-lane select).
-// Outputs (y[0:32) and the t-vector for the tail) are identical to
-// k_eval_wide_head's.
+// Outputs: y[0:32) and the t-vector for the tail (kernels_wide.h).
 #pragma once
 
 #include "aes_lds.h"
@@ -331,7 +330,7 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
       L.ph[i] = mB ? 1u : (mD ? 2u : 0u);
       const bool reuse = ru != 0u && L.lev[i] + adv != nlev;
       L.ph[i] = reuse ? 1u : L.ph[i];  // the next level starts at A / D
-      // t-vector: row r = lev + 1 gets t_r (byte r >> 2, bit r & 3), as k_eval_wide_head writes it
+      // t-vector: row r = lev + 1 gets t_r (byte r >> 2, bit r & 3), the layout the tail reads
       const uint32_t r = L.lev[i] + adv;
       L.tacc[i] |= (am & L.t[i]) << (8u * ((r >> 2) & 3u) + (r & 3u));
       uint32_t* trow = tvec + (uint64_t)L.pt[i] * tw;

@@ -173,8 +173,8 @@ class Aes256HirosePrg:
         return self._h
 
     def set_eval_mode(self, mode: int) -> None:
-        """AES engine for LAMBDA = 16 eval: 0 auto, 1 LDS T-table, 2 VALU bitsliced, 3 hybrid,
-        4 stream (LDS T-table, per-lane block scheduling), 5 stream + bitsliced waves."""
+        """AES engine for LAMBDA = 16 eval: 0 auto, 1 lockstep LDS T-table, 4 stream (LDS T-table,
+        per-lane block scheduling).  Identical bytes for every mode (dcf_prg_set_eval_mode)."""
         check(_lib.load().dcf_prg_set_eval_mode(self._h, int(mode)))
 
     def set_prefix_levels(self, levels: int) -> None:
@@ -196,17 +196,6 @@ class Aes256HirosePrg:
         if r < 0:
             check(r)
         return r
-
-    def set_hybrid_split(self, ttable_waves: int, slab_variant: int = 1) -> None:
-        """Hybrid engine: T-table waves per workgroup (rest bitsliced); slab_variant 1 = 16-wave
-        workgroups with bitsliced state in scratch slabs, 0 = 12 waves with state in registers."""
-        check(_lib.load().dcf_prg_set_hybrid_split(self._h, int(ttable_waves), int(slab_variant)))
-
-    def set_stream_hybrid(self, ttable_wave_mask: int, priority: int = 0) -> None:
-        """Stream-hybrid engine (mode 5): bit w of the mask = wave w of the 16-wave workgroup
-        runs the stream T-table engine, clear = bitsliced (waves w and w + 4 share a SIMD);
-        priority 1 raises the stream waves' issue priority.  Output bytes are identical."""
-        check(_lib.load().dcf_prg_set_stream_hybrid(self._h, int(ttable_wave_mask), int(priority)))
 
     def last_eval_blocks(self) -> int:
         """AES blocks the last stream-engine eval encrypted for live points, counted on the

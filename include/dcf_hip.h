@@ -81,13 +81,12 @@ extern "C" {
 #define DCF_BOUND_LT_BETA 0
 #define DCF_BOUND_GT_BETA 1
 
-/* AES engine for LAMBDA = 16 eval (dcf_prg_set_eval_mode); results are identical. */
-#define DCF_EVAL_AUTO 0      /* library's choice: STREAM for one key, TTABLE for many */
-#define DCF_EVAL_TTABLE 1    /* LDS T-table AES, one lane per point */
-#define DCF_EVAL_BITSLICED 2 /* VALU bitsliced AES, 32 points per lane quad (single key, N <= 16) */
-#define DCF_EVAL_HYBRID 3    /* both engines side by side on every CU (single key, N <= 16) */
+/* AES engine for LAMBDA = 16 eval (dcf_prg_set_eval_mode); results are identical.  Values 2, 3
+ * and 5 (bitsliced, hybrid and stream-hybrid engines, rounds 1-4) are retired: every A/B measured
+ * them slower than the stream engine (profiles/AB_LOG.md), and setting them returns DCF_ERR_ARG. */
+#define DCF_EVAL_AUTO 0      /* library's choice: STREAM for one key or N <= 32, TTABLE for many keys at N > 32 */
+#define DCF_EVAL_TTABLE 1    /* LDS T-table AES, lockstep walk (A and B every level), one lane per point */
 #define DCF_EVAL_STREAM 4    /* LDS T-table AES, per-lane block scheduling: a right step encrypts B only */
-#define DCF_EVAL_STREAM_HYBRID 5 /* STREAM waves + bitsliced waves on every CU (single key, N % 4 == 0, N <= 16) */
 
 /* Opaque: an Aes256HirosePrg (prg.rs:22-24) whose AES-256 schedules live on one
  * device, i.e. `DcfImpl::new(Aes256HirosePrg::new(keys))` (lib.rs:74, prg.rs:27). */
@@ -122,8 +121,9 @@ int dcf_prg_kind(const dcf_prg* prg);
 void dcf_prg_free(dcf_prg* prg);
 size_t dcf_prg_lambda(const dcf_prg* prg);
 
-/* Select the AES engine used by eval at LAMBDA = 16 (DCF_EVAL_*).  Tuning and
- * test knob only: every engine returns identical bytes. */
+/* Select the AES engine used by eval at LAMBDA = 16 (DCF_EVAL_AUTO / _TTABLE / _STREAM; the
+ * LAMBDA >= 32 head and the MMO PRG have one engine each and ignore it).  Tuning and test knob
+ * only: every engine returns identical bytes. */
 int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 
 /* Shared prefix for single-key eval at LAMBDA = 16 (Hirose PRG: stream engine, and the
@@ -172,24 +172,8 @@ int dcf_prg_workspaces(const dcf_prg* prg);
  * of workspaces freed. */
 int dcf_prg_trim(dcf_prg* prg);
 
-/* Hybrid engine tuning (results are identical for every setting):
- *   slab_variant 1: 16-wave workgroups; slab_variant 0: 12-wave workgroups (the bitsliced
- *                  waves keep their s / v state in per-wave scratch slabs either way);
- *   ttable_waves:  waves per workgroup running the T-table engine (the rest
- *                  run the bitsliced engine; clamped to [1, 16] / [0, 12]). */
-int dcf_prg_set_hybrid_split(dcf_prg* prg, int ttable_waves, int slab_variant);
-
-/* DCF_EVAL_STREAM_HYBRID tuning (results are identical for every setting):
- *   ttable_wave_mask: bit w set = wave w of the 16-wave workgroup runs the stream
- *                     T-table engine, clear = the bitsliced engine; waves w and
- *                     w + 4 share a SIMD (at least 4 bits set);
- *   priority:         1 = stream waves issue at raised priority (s_setprio).
- * A DCF_EVAL_STREAM_HYBRID eval takes fewer than 2^31 points per call (DCF_ERR_UNSUPPORTED
- * otherwise; the default stream engine splits larger batches into launches itself). */
-int dcf_prg_set_stream_hybrid(dcf_prg* prg, unsigned ttable_wave_mask, int priority);
-
 /* AES blocks the last eval call on this prg (the last one to return, from any thread)
- * encrypted for live points (LAMBDA = 16: DCF_EVAL_STREAM / _STREAM_HYBRID's stream waves;
+ * encrypted for live points (LAMBDA = 16: the DCF_EVAL_STREAM engine;
  * LAMBDA >= 32: the stream head over all of the call's keys and passes; not counting a
  * shared-prefix table build, except the multi-key per-key top trees, whose blocks are
  * included), counted on the device; 0 for engines that do not count.

@@ -1,7 +1,7 @@
 //! Raw bindings of include/dcf_hip.h (every entry point; same order as the header).
 //! tests/test_rust_ffi.py (in the repo's Python suite) checks names and arities against
 //! the header, since this container has no Rust toolchain.
-use std::os::raw::{c_char, c_int, c_uint, c_void};
+use std::os::raw::{c_char, c_int, c_void};
 
 #[repr(C)]
 pub struct DcfPrg {
@@ -37,8 +37,6 @@ extern "C" {
     pub fn dcf_prg_host_pinned_bytes(prg: *const DcfPrg) -> usize;
     pub fn dcf_prg_workspaces(prg: *const DcfPrg) -> c_int;
     pub fn dcf_prg_trim(prg: *mut DcfPrg) -> c_int;
-    pub fn dcf_prg_set_hybrid_split(prg: *mut DcfPrg, ttable_waves: c_int, slab_variant: c_int) -> c_int;
-    pub fn dcf_prg_set_stream_hybrid(prg: *mut DcfPrg, ttable_wave_mask: c_uint, priority: c_int) -> c_int;
     pub fn dcf_prg_last_eval_blocks(prg: *mut DcfPrg, blocks: *mut u64) -> c_int;
     pub fn dcf_prg_set_phase_timing(prg: *mut DcfPrg, on: c_int) -> c_int;
     pub fn dcf_prg_last_eval_phases(prg: *mut DcfPrg, prep_ms: *mut f32, walk_ms: *mut f32,

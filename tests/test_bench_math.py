@@ -27,8 +27,7 @@ def test_peaks(bench):
     assert bench.PEAK_TT_BLOCKS == pytest.approx(256 * 32 * 2.4e9 / 224)
     assert bench.engine_peak("stream") == bench.PEAK_TT_BLOCKS
     assert bench.engine_peak("mmo") == pytest.approx(256 * 2.4e9 / (160 / 32 + 11 / 16))
-    # hybrid: T-table saturates the LDS, bitsliced uses the VALU left over
-    assert bench.hybrid_peak() > bench.PEAK_TT_BLOCKS
+    assert bench.engine_peak("ttable") == bench.engine_peak("ttable-small") == bench.PEAK_TT_BLOCKS
 
 
 def test_wide_roofline_bound(bench):

@@ -114,13 +114,11 @@ def test_reference_reconstruction_kat(dcf, bound):
         assert y0[2].tobytes() != bytes(16) and y1[2].tobytes() != bytes(16)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1, 4])
 @pytest.mark.parametrize("nb", [1, 2, 3, 4, 5, 7, 8, 12, 16, 17, 32])
 def test_eval_random_vs_oracle(dcf, nb, mode):
-    """mode 1 = LDS T-table engine, 2 = VALU bitsliced engine, 3 = hybrid (2 and 3: N <= 16 only),
-    4 = T-table with per-lane block scheduling (stream engine)."""
-    if mode in (2, 3) and nb > 16:
-        pytest.skip("bitsliced engine covers N <= 16")
+    """mode 0 = auto, 1 = lockstep LDS T-table engine (k_eval16, also for one key), 4 = T-table
+    with per-lane block scheduling (stream engine)."""
     rng = np.random.default_rng(100 + nb)
     keys = [rng.bytes(32) for _ in range(2)]
     prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
@@ -196,7 +194,7 @@ def test_eval_length_mismatch_is_error(dcf):
         d.eval(False, dcf.Share(k.s0s, k.cws[:127], k.cw_np1), REF_ALPHAS)  # lib.rs:165
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [1, 4])
 @pytest.mark.parametrize("nb,m", [(16, 1 << 20), (4, (1 << 20) + 37)])
 def test_eval_device_large_sample_and_reconstruction(dcf, nb, m, mode):
     """Large batch on device: bit-exact on a sample vs the oracle, and the
@@ -404,7 +402,9 @@ def test_wide_prefix_vs_oracle(dcf, lam, nb, depth, m):
         for b, s in ((0, s0), (1, s1)):
             got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
             assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, depth, b, bound)
-    prg.set_eval_mode(1)  # the lockstep head takes no table
+    prg.set_eval_mode(1)  # LAMBDA >= 32 has one head engine: the setting changes nothing
+    assert prg.eval_prefix_levels(nb, 1, m) == min(depth, 30, 8 * nb - 1)
+    prg.set_prefix_levels(0)
     assert prg.eval_prefix_levels(nb, 1, m) == 0
 
 
@@ -460,27 +460,16 @@ def test_wide_multikey_batched_vs_oracle(dcf, lam, nb, K, P):
         assert np.array_equal(y0h[sl], O.eval_(Po, 0, ok, s0[key].tobytes(), xs[sl], nthreads=8)), key
         assert np.array_equal(y1h[sl], O.eval_(Po, 1, ok, s1[key].tobytes(), xs[sl], nthreads=8)), key
     assert not (y0h[::P] ^ y1h[::P]).any()  # f(alpha) = 0 for every key
-
-
-@pytest.mark.parametrize("split,variant", [(0, 0), (6, 0), (12, 0), (1, 1), (8, 1), (15, 1), (16, 1)])
-def test_hybrid_splits_identical(dcf, split, variant):
-    """Every T-table/bitsliced wave split of the hybrid engine returns the same bytes."""
-    import torch
-    rng = np.random.default_rng(split)
-    keys = [rng.bytes(32) for _ in range(2)]
-    prg = dcf.Aes256HirosePrg(keys, 16)
-    d = dcf.DcfImpl(16, 16, prg)
-    k = d.gen(dcf.CmpFn(rng.bytes(16), rng.bytes(16)), [rng.bytes(16), rng.bytes(16)], dcf.BoundState.GtBeta)
-    cwb = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, 16, 16), np.uint8).copy()).cuda()
-    s0 = torch.from_numpy(np.frombuffer(k.s0s[0], np.uint8).copy()).cuda()
-    xs = torch.from_numpy(_rand(rng, (300_001, 16))).cuda()
-    prg.set_eval_mode(1)
-    ref = d.eval_device(False, cwb, s0, xs)
-    prg.set_eval_mode(3)
-    prg.set_hybrid_split(split, variant)
-    got = d.eval_device(False, cwb, s0, xs)
-    torch.cuda.synchronize()
-    assert torch.equal(ref, got)
+    # the batched passes build no shared-prefix table, and the depth hook says so;
+    # a forced depth sends the keys through the per-key path, which builds one per key
+    want = 0 if P <= 32768 else min(P.bit_length() - 2, 22, 8 * nb - 1)
+    assert prg.eval_prefix_levels(nb, K, P) == (want if want >= 8 else 0)
+    if K <= 40 and P < 32768 and 8 * nb > 6:
+        prg.set_prefix_levels(6)
+        assert prg.eval_prefix_levels(nb, K, P) == 6
+        y0f = d.eval_multikey_device(False, cwb, T(s0), T(xs), P)
+        torch.cuda.synchronize()
+        assert np.array_equal(y0f.cpu().numpy(), y0h)
 
 
 @pytest.mark.parametrize("nb", [1, 4, 5, 8, 16, 17, 32])
@@ -522,56 +511,17 @@ def test_stream_b_reuse_vs_oracle(dcf, nb, prefix):
                 assert blocks > 0.5 * (8 * nb * m + zeros)
 
 
-@pytest.mark.parametrize("nb,prefix,mask,prio", [(16, -1, 0x7777, 0), (16, -1, 0x3333, 1), (16, 0, 0xEEEE, 0),
-                                                   (16, 13, 0xFFF0, 1), (4, -1, 0x7777, 0), (4, 23, 0x5555, 0),
-                                                   (8, 1, 0x7777, 1), (12, 0, 0x0F0F, 0)])
-def test_stream_hybrid_vs_oracle(dcf, nb, prefix, mask, prio):
-    """Stream-hybrid engine (mode 5: stream T-table waves + bitsliced waves, both below
-    the shared prefix): bit-exact with the oracle on a sample and with the stream
-    engine on a batch large enough that both roles take units (300k points), for
-    several wave masks, depths (auto, forced, off) and N (4, 8, 12, 16)."""
-    import torch
-    rng = np.random.default_rng(0x5E + nb * 7 + mask)
-    keys = [rng.bytes(32) for _ in range(2)]
-    prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
-    d = dcf.DcfImpl(nb, 16, prg)
-    alpha, beta, s0, s1 = rng.bytes(nb), rng.bytes(16), rng.bytes(16), rng.bytes(16)
-    bound = int(rng.integers(0, 2))
-    k = d.gen(dcf.CmpFn(alpha, beta), [s0, s1], dcf.BoundState(bound))
-    ok = O.gen(P, alpha, beta, s0, s1, bound)
-    m = 300_001
-    xs_h = _rand(rng, (m, nb))
-    a = np.frombuffer(alpha, np.uint8)
-    xs_h[0] = a
-    xs_h[1:200] = a
-    xs_h[1:200, -1] = rng.integers(0, 256, 199, dtype=np.uint8)
-    cwb = torch.from_numpy(np.frombuffer(dcf.share_to_cwb(k, nb, 16), np.uint8).copy()).cuda()
-    xs = torch.from_numpy(xs_h).cuda()
-    prg.set_prefix_levels(prefix)
-    for b, s in ((0, s0), (1, s1)):
-        sd = torch.from_numpy(np.frombuffer(s, np.uint8).copy()).cuda()
-        prg.set_eval_mode(4)
-        ref = d.eval_device(bool(b), cwb, sd, xs)
-        prg.set_eval_mode(5)
-        prg.set_stream_hybrid(mask, prio)
-        got = d.eval_device(bool(b), cwb, sd, xs)
-        torch.cuda.synchronize()
-        assert torch.equal(ref, got), (nb, prefix, hex(mask), b)
-        idx = np.r_[0:3000, m - 3000:m]
-        want = O.eval_(P, b, ok, s, xs_h[idx], nthreads=8)
-        assert np.array_equal(got.cpu().numpy()[idx], want), (nb, prefix, hex(mask), b)
-
-
-def test_stream_hybrid_rejects(dcf):
-    prg = dcf.Aes256HirosePrg([bytes(32)] * 2, 16)
-    for mask in (0x0007, 0x10000):
-        with pytest.raises(dcf.DcfError):
-            prg.set_stream_hybrid(mask, 0)
-    prg.set_eval_mode(5)
-    d = dcf.DcfImpl(3, 16, prg)  # N % 4 != 0: not served by this engine
-    k = d.gen(dcf.CmpFn(bytes(3), bytes(16)), [bytes(16), bytes(16)], dcf.BoundState.LtBeta)
-    with pytest.raises(dcf.DcfError):
-        d.eval(False, k, np.zeros((10, 3), np.uint8))
+def test_retired_eval_modes_rejected(dcf):
+    """Modes 2, 3 and 5 (bitsliced, hybrid, stream-hybrid; retired in round 5 after losing every
+    A/B) are refused with DCF_ERR_ARG, and the prg keeps its engine."""
+    prg = dcf.Aes256HirosePrg(REF_KEYS, 16)
+    for mode in (2, 3, 5, 6, -1):
+        with pytest.raises(dcf.DcfError) as e:
+            prg.set_eval_mode(mode)
+        assert e.value.code == -1
+    for mode in (0, 1, 4):
+        prg.set_eval_mode(mode)
+    assert not hasattr(prg, "set_hybrid_split") and not hasattr(prg, "set_stream_hybrid")
 
 
 def test_error_codes_on_device(dcf):
