@@ -15,6 +15,8 @@
 #pragma once
 
 #include "aes_lds.h"
+#include "kernels_lat.h"     // dpp<>
+#include "kernels_stream.h"  // dequeue_unit
 
 namespace {
 
@@ -380,81 +382,113 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
   DCF_CLK(1, 1);
 }
 
-// One wide prefix node (80 B: s[0:32) | v[0:32) | {t, t-vector word 0, partial word, 0})
-// at depth `lev` -> its two children, bytes [0,32) of the walk exactly as
-// k_eval_wide_head_stream updates them: A = E0(s_lo), B = E0(~s_lo) (left),
-// C = E17(s_hi), D = E17(~s_hi) (right), all four blocks.  rks: the LDS copies of the
-// schedules of ciphers 0 (rks[0..15)) and 17 (rks[23..38)).
+// One wide prefix node (80 B: s[0:32) | v[0:32) | {t, t-vector word 0, partial word, 0}) at depth
+// `lev` -> its two children, bytes [0,32) of the walk exactly as k_eval_wide_head_stream updates
+// them, on a lane QUAD: lane q encrypts one of the node's four blocks — A = E0(s_lo), B = E0(~s_lo),
+// C = E17(s_hi), D = E17(~s_hi) for q = 0..3 — and writes the child pieces its block decides:
+//   q = 0: left s_lo = A ^ s_lo ^ t cs_lo            right s_lo = s_lo ^ t cs_lo
+//   q = 1: left v_lo = v_lo ^ B ^ ~s_lo ^ t cv_lo    right v_lo = v_lo ^ ~s_lo ^ t cv_lo
+//   q = 2: right s_hi = (C ^ s_hi) & M ^ t cs_hi     left s_hi = s_hi & M ^ t cs_hi           + left's word 4
+//   q = 3: right v_hi = v_hi ^ (D ^ ~s_hi) & M ^ t cv_hi   left v_hi = v_hi ^ ~s_hi & M ^ t cv_hi   + right's word 4
+// (prg.rs:57-68 under the diagonal zip; M clears bit 0 of byte 31 when LAMBDA == 32), t_L = lsb(A ^ s)[0]
+// ^ t cw.tl from lane 0 and t_R = lsb(B ^ ~s)[0] ^ t cw.tr from lane 1, broadcast over the quad
+// (lib.rs:177-180).  One block per lane instead of four: a level's latency is one AES chain, and no
+// lane holds more than a node piece (the four-block form held 2 x 5 uint4 of children and spilled
+// to 176 B of scratch).  Must run in uniform control flow (DPP): whole waves, quads past the level's
+// nodes compute a copy and skip the stores.  rks_a: LDS byte address of the schedules (cipher 0 at
+// slot 0, cipher 17 at slot 23); node / piece pointers may be LDS or global.
+struct WpfxQuad {
+  uint32_t q, lo, in_piece, v_piece, cw_piece, ka;
+  __device__ __forceinline__ void init(uint32_t rks_a) {
+    q = threadIdx.x & 3u;
+    lo = (q >> 1) == 0u;                 // bytes [0,16): blocks A, B (cipher 0)
+    in_piece = q >> 1;                   // s_lo / s_hi
+    v_piece = 2u + (q >> 1);             // v_lo / v_hi
+    cw_piece = (q & 1u) ? 2u + (q >> 1) : (q >> 1);  // digest row: cs_lo, cs_hi, cv_lo, cv_hi = 0, 1, 2, 3
+    ka = rks_a + (lo ? 0u : 368u);
+  }
+  // the pieces of node `n` (LDS or global) this lane reads: its AES input half, its v half, word 4
+  __device__ __forceinline__ void load(const uint4* n, uint4& sp, uint4& vp, uint4& e) const {
+    sp = n[in_piece];
+    vp = n[v_piece];
+    e = n[4];
+  }
+};
+
 template <bool MASK_HEAD>
-__device__ __forceinline__ void wpfx_children(const uint32_t* lds, uint32_t lc, const uint4* rks,
-                                              const uint4* __restrict__ dig, const uint8_t* __restrict__ dig_t,
-                                              uint32_t lev, const uint4 (&in)[5], uint4 (&ol)[5], uint4 (&orr)[5]) {
-  const uint32_t mlast = MASK_HEAD ? kMaskLast : 0xFFFFFFFFu;
-  const uint4* d4 = dig + 4u * lev;
-  const uint4 cs0 = d4[0], cs1 = d4[1], cv0 = d4[2], cv1 = d4[3];
+__device__ __forceinline__ void wpfx_quad_children(const uint32_t* lds, uint32_t lc, const WpfxQuad& Q,
+                                                   const uint4* __restrict__ dig, const uint8_t* __restrict__ dig_t,
+                                                   uint32_t lev, const uint4 sp, const uint4 vp, const uint4 e,
+                                                   bool store, uint4* left, uint4* right) {
+  const uint32_t q = Q.q;
+  const uint4 cw = dig[4u * lev + Q.cw_piece];
   const uint32_t ct = dig_t[lev];
-  const uint32_t csw[8] = {cs0.x, cs0.y, cs0.z, cs0.w, cs1.x, cs1.y, cs1.z, cs1.w};
-  const uint32_t cvw[8] = {cv0.x, cv0.y, cv0.z, cv0.w, cv1.x, cv1.y, cv1.z, cv1.w};
-  const uint32_t r = lev + 1u, pos = 8u * ((r >> 2) & 3u) + (r & 3u);
-  const uint4 a0 = in[0], a1 = in[1], b0 = in[2], b1 = in[3], e = in[4];
-  const uint32_t sw[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-  const uint32_t vw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-  uint32_t ab[2][4], cd[2][4];
+  const uint32_t inv = 0u - (q & 1u);
+  const uint32_t s[4] = {sp.x, sp.y, sp.z, sp.w}, v[4] = {vp.x, vp.y, vp.z, vp.w};
+  const uint32_t c[4] = {cw.x, cw.y, cw.z, cw.w};
+  uint32_t st[1][4];
+  const uint32_t ka[1] = {Q.ka};
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    ab[0][j] = sw[j];           // A
-    ab[1][j] = ~sw[j];          // B
-    cd[0][j] = sw[4 + j];       // C
-    cd[1][j] = ~sw[4 + j];      // D
-  }
-  const uint4* rk0[2] = {rks, rks};
-  const uint4* rk17[2] = {rks + 23, rks + 23};
-  aes_tt_lk<14, 2, true>(ab, rk0, lds, lc);
-  aes_tt_lk<14, 2, true>(cd, rk17, lds, lc);
+  for (int j = 0; j < 4; ++j) st[0][j] = s[j] ^ inv;
+  aes_tt_lka<14, 1, false>(st, ka, lds, lc);
   const uint32_t t = e.x, tm = 0u - t;
-  uint32_t sl[8], vl[8], sr[8], vr[8];
+  // d = E(in) ^ in: the PRG output block (prg.rs:57-62); bit 0 of byte 31 masked (hi half, LAMBDA == 32)
+  const uint32_t mlast = (MASK_HEAD && !Q.lo) ? kMaskLast : 0xFFFFFFFFu;
+  uint32_t d[4], keep[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint32_t dA = ab[0][j] ^ sw[j], dB = ab[1][j] ^ ~sw[j];
-    const uint32_t dC = cd[0][j] ^ sw[4 + j], dD = cd[1][j] ^ ~sw[4 + j];
-    const uint32_t msk = (j == 3) ? mlast : 0xFFFFFFFFu;
-    // left: s = (A^s_lo, s_hi & M), v ^= (B^~s_lo, ~s_hi & M)   (prg.rs:57-68 with the diagonal zip)
-    sl[j] = dA ^ (tm & csw[j]);
-    sl[4 + j] = (sw[4 + j] & msk) ^ (tm & csw[4 + j]);
-    vl[j] = vw[j] ^ dB ^ (tm & cvw[j]);
-    vl[4 + j] = vw[4 + j] ^ (~sw[4 + j] & msk) ^ (tm & cvw[4 + j]);
-    // right: s = (s_lo, (C^s_hi) & M), v ^= (~s_lo, (D^~s_hi) & M)
-    sr[j] = sw[j] ^ (tm & csw[j]);
-    sr[4 + j] = (dC & msk) ^ (tm & csw[4 + j]);
-    vr[j] = vw[j] ^ ~sw[j] ^ (tm & cvw[j]);
-    vr[4 + j] = vw[4 + j] ^ (dD & msk) ^ (tm & cvw[4 + j]);
+    const uint32_t m = (j == 3) ? mlast : 0xFFFFFFFFu;
+    d[j] = (st[0][j] ^ s[j] ^ inv) & m;   // A ^ s, B ^ ~s, C ^ s, D ^ ~s
+    keep[j] = (s[j] ^ inv) & m;           // the branch this block does not touch: s or ~s
   }
-  // t_L = lsb(A^s)[0], t_R = lsb(B^~s)[0], each ^ t & its cw.t   (lib.rs:179-180)
-  const uint32_t tl = ((ab[0][0] ^ sw[0]) ^ (t & ct)) & 1u;
-  const uint32_t trr = ((ab[1][0] ^ ~sw[0]) ^ (t & (ct >> 1))) & 1u;
-  uint32_t accl = e.z | (tl << pos), accr = e.z | (trr << pos), w0l = e.y, w0r = e.y;
-  if ((r & 15u) == 15u) {  // word r >> 4 of the t-vector is complete (r < 31: word 0)
-    w0l = accl; w0r = accr;
-    accl = accr = 0u;
+  // t_L (lane 0: lsb of A ^ s), t_R (lane 1: lsb of B ^ ~s), each ^ t & its cw.t bit
+  const uint32_t tb = (d[0] ^ (t & (ct >> (q & 1u)))) & 1u;
+  const uint32_t tl = dpp<kQpBcast0>(tb), tr = dpp<1 | (1 << 2) | (1 << 4) | (1 << 6)>(tb);
+  if (!store) return;
+  // AES'd piece (to the block's branch) and the pass-through piece (to the other branch); the v
+  // lanes (q odd) add v, every piece adds t * its CW piece
+  uint4 pa, pk;
+  {
+    uint32_t a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t base = (q & 1u) ? v[j] : 0u;
+      a[j] = base ^ d[j] ^ (tm & c[j]);
+      b[j] = base ^ keep[j] ^ (tm & c[j]);
+    }
+    pa = make_uint4(a[0], a[1], a[2], a[3]);
+    pk = make_uint4(b[0], b[1], b[2], b[3]);
   }
-  ol[0] = make_uint4(sl[0], sl[1], sl[2], sl[3]);
-  ol[1] = make_uint4(sl[4], sl[5], sl[6], sl[7]);
-  ol[2] = make_uint4(vl[0], vl[1], vl[2], vl[3]);
-  ol[3] = make_uint4(vl[4], vl[5], vl[6], vl[7]);
-  ol[4] = make_uint4(tl, w0l, accl, 0u);
-  orr[0] = make_uint4(sr[0], sr[1], sr[2], sr[3]);
-  orr[1] = make_uint4(sr[4], sr[5], sr[6], sr[7]);
-  orr[2] = make_uint4(vr[0], vr[1], vr[2], vr[3]);
-  orr[3] = make_uint4(vr[4], vr[5], vr[6], vr[7]);
-  orr[4] = make_uint4(trr, w0r, accr, 0u);
+  // A (q 0) and B (q 1) belong to the left child, C (q 2) and D (q 3) to the right one
+  uint4* mine = Q.lo ? left : right;
+  uint4* other = Q.lo ? right : left;
+  const uint32_t piece = (q & 1u) ? Q.v_piece : Q.in_piece;
+  mine[piece] = pa;
+  other[piece] = pk;
+  if (q >= 2u) {  // word 4: t, t-vector word 0, partial word (row r = lev + 1 at bit pos)
+    const uint32_t r = lev + 1u, pos = 8u * ((r >> 2) & 3u) + (r & 3u);
+    const uint32_t tc = (q == 2u) ? tl : tr;
+    uint32_t acc = e.z | (tc << pos), w0 = e.y;
+    if ((r & 15u) == 15u) {  // word r >> 4 of the t-vector is complete (r < 31: word 0)
+      w0 = acc;
+      acc = 0u;
+    }
+    ((q == 2u) ? left : right)[4] = make_uint4(tc, w0, acc, 0u);
+  }
 }
 
 // The whole wide prefix tree of depth D in ONE launch (as k_prefix_build16 at LAMBDA = 16):
-// workgroup w (2^S of them) owns the subtree under node w of level S; wave 0 walks the
-// root path (root = k.s0s[0][0:32), v = 0, t = party, t-vector row 0 = party:
-// lib.rs:167-169), then the workgroup expands its subtree level by level with workgroup
-// barriers only, ping-ponging through its own regions (R = 2^(D-1-S) nodes of 80 B) of
-// two buffers; the last level writes the workgroup's contiguous block of the table.
+// workgroup w (2^S of them) owns the subtree under node w of level S.  One lane quad walks the
+// root path (root = k.s0s[0][0:32), v = 0, t = party, t-vector row 0 = party: lib.rs:167-169);
+// the workgroup then expands its subtree level by level (a quad per node, wpfx_quad_children):
+// while a level has <= kWpfxLdsPar parents its children stay in an LDS node buffer (two barriers
+// per level, no global round trip); wider levels go through the workgroup's regions (R =
+// 2^(D-1-S) nodes of 80 B) of two global buffers, waves claiming 16 nodes at a time from an LDS
+// counter (waves of a workgroup do not progress at one rate); the last level writes the
+// workgroup's contiguous block of the table.  C4 (D = 21): the build went from 0.38 ms with a
+// lone wave's four-block T-table calls on the root path and every level through global memory.
+constexpr uint32_t kWpfxLdsNodes = 384;  // 30 KiB of 80-byte nodes beside the 128 KiB tables
+constexpr uint32_t kWpfxLdsPar = 128;    // parents per level whose children stay in the LDS (256 <= 384)
 template <bool MASK_HEAD>
 __global__ __launch_bounds__(kBlock, 1) void k_wpfx_build(
     const uint32_t* __restrict__ tab, const uint4* __restrict__ rk2, const uint4* __restrict__ dig,
@@ -463,58 +497,79 @@ __global__ __launch_bounds__(kBlock, 1) void k_wpfx_build(
     uint4* __restrict__ table) {
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint4 rks[23 + 15];
-  __shared__ uint4 root[5];
+  __shared__ uint4 nodes[5 * kWpfxLdsNodes];
+  __shared__ uint32_t claim;
   if (threadIdx.x < 30) rks[threadIdx.x < 15 ? threadIdx.x : threadIdx.x + 8] = rk2[threadIdx.x];
-  lds_fill_tables(lds, tab);
+  if (threadIdx.x < 5) {  // the root node (level 0) into LDS slot 0
+    const uint4* s4 = reinterpret_cast<const uint4*>(s0p);
+    nodes[threadIdx.x] = threadIdx.x < 2 ? s4[threadIdx.x]
+                                          : (threadIdx.x < 4 ? make_uint4(0u, 0u, 0u, 0u)
+                                                             : make_uint4(party, 0u, party, 0u));
+  }
+  lds_fill_tables(lds, tab);  // its barrier publishes rks and the root
   DCF_CLK(6, 0);  // (diagnostic builds; slots 6 / 7 are k_prefix_build16's at LAMBDA = 16) after the fill
   const uint32_t lc = lane_const();
-  const uint32_t w = blockIdx.x;
-  const uint64_t R5 = 5ull * region_nodes;
-  uint4* X = buf_a + (uint64_t)w * R5;
-  uint4* Y = buf_b + (uint64_t)w * R5;
-  if (threadIdx.x < 64) {  // wave 0: root -> node w of level S (every lane the same node)
-    const uint4* s4 = reinterpret_cast<const uint4*>(s0p);
-    uint4 nd[5] = {s4[0], s4[1], make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u),
-                   make_uint4(party, 0u, party, 0u)};
+  WpfxQuad Q;
+  Q.init((uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)rks);
+  const uint32_t w = blockIdx.x, g = threadIdx.x >> 2;  // quad g of 256
+  const uint32_t nq = blockDim.x >> 2;
+  if (threadIdx.x < 64) {  // wave 0, quad 0: root -> node w of level S (slot 0 -> slot 0)
     for (uint32_t lev = 0; lev < S; ++lev) {
-      uint4 cl[5], cr[5];
-      wpfx_children<MASK_HEAD>(lds, lc, rks, dig, dig_t, lev, nd, cl, cr);
       const bool right = (w >> (S - 1u - lev)) & 1u;
-#pragma unroll
-      for (int q = 0; q < 5; ++q) nd[q] = right ? cr[q] : cl[q];
+      // children to slots 1 / 2, then the chosen one back to slot 0 (one wave: LDS is in order)
+      uint4 sp, vp, e;
+      Q.load(nodes, sp, vp, e);
+      wpfx_quad_children<MASK_HEAD>(lds, lc, Q, dig, dig_t, lev, sp, vp, e, g == 0u, nodes + 5, nodes + 10);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (threadIdx.x < 5) nodes[threadIdx.x] = nodes[(right ? 10 : 5) + threadIdx.x];
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
-    if (threadIdx.x == 0)
-#pragma unroll
-      for (int q = 0; q < 5; ++q) root[q] = nd[q];
   }
   __syncthreads();
   DCF_CLK(6, 1);  // root path done
-  for (uint32_t lev = S; lev < D; ++lev) {
+  const uint64_t R5 = 5ull * region_nodes;
+  uint4* X = buf_a + (uint64_t)w * R5;
+  uint4* Y = buf_b + (uint64_t)w * R5;
+  uint32_t lev = S;
+  // narrow levels in the LDS: parents in slots [0, np), children to [0, 2 np) after a barrier
+  for (; lev < D && (1u << (lev - S)) <= kWpfxLdsPar; ++lev) {
     const uint32_t np = 1u << (lev - S);
     const bool last = lev + 1u == D;
-    if (lev + 3u == D) DCF_CLK(7, 0);  // the last three levels start
+    const uint32_t j = g < np ? g : np - 1u;
+    uint4 sp, vp, e;
+    Q.load(nodes + 5u * j, sp, vp, e);
+    __syncthreads();  // every parent read before any child overwrites it
+    uint4* out = last ? table + 5ull * ((uint64_t)w << (D - S)) : nodes;
+    if (g - (g & 15u) < np)  // whole waves (uniform DPP); quads past np store nothing
+      wpfx_quad_children<MASK_HEAD>(lds, lc, Q, dig, dig_t, lev, sp, vp, e, g < np, out + 10u * j, out + 10u * j + 5u);
+    __syncthreads();
+  }
+  if (lev == D) return;
+  // wide levels: parents from the LDS (first one) or X, children to Y or the table
+  bool from_lds = true;
+  for (; lev < D; ++lev) {
+    const uint32_t np = 1u << (lev - S);
+    const bool last = lev + 1u == D;
     uint4* out = last ? table + 5ull * ((uint64_t)w << (D - S)) : Y;
-    // whole waves stay in the loop (uniform AES); lanes past np compute a copy of node np - 1
-    for (uint32_t g = threadIdx.x; g - (threadIdx.x & 63u) < np; g += blockDim.x) {
-      const uint32_t j = g < np ? g : np - 1u;
-      uint4 in[5];
-#pragma unroll
-      for (int q = 0; q < 5; ++q) in[q] = lev == S ? root[q] : X[5u * j + q];
-      uint4 cl[5], cr[5];
-      wpfx_children<MASK_HEAD>(lds, lc, rks, dig, dig_t, lev, in, cl, cr);
-      if (g < np) {
-        uint4* o = out + 10u * j;
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
-          o[q] = cl[q];
-          o[5 + q] = cr[q];
-        }
-      }
+    const uint4* in = from_lds ? nodes : X;
+    if (threadIdx.x == 0) claim = 0u;
+    __syncthreads();
+    for (;;) {  // 16 nodes per wave per claim (np is a multiple of 256 here)
+      uint32_t base = 0u;
+      if ((threadIdx.x & 63u) == 0)
+        base = __hip_atomic_fetch_add(&claim, 16u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      base = __builtin_amdgcn_readfirstlane(base);
+      if (base >= np) break;
+      const uint32_t j = base + ((threadIdx.x & 63u) >> 2);
+      uint4 sp, vp, e;
+      Q.load(in + 5u * j, sp, vp, e);
+      wpfx_quad_children<MASK_HEAD>(lds, lc, Q, dig, dig_t, lev, sp, vp, e, true, out + 10u * j, out + 10u * j + 5u);
     }
     __syncthreads();  // the workgroup's children are its next parents
     uint4* tmp = X;
     X = Y;
     Y = tmp;
+    from_lds = false;
   }
   DCF_CLK(7, 1);
 }

@@ -1,8 +1,8 @@
-# r05a: first tree of round 5 (retired bitsliced / hybrid engines, bench.py self-spawn + multi-GPU ABI
+# r05b (r05a with the test fix): first tree of round 5 (retired bitsliced / hybrid engines, bench.py self-spawn + multi-GPU ABI
 # check, C5 N > 1 check, ADVICE r04 fixes, scratch-free wide gen): GPU suite, smoke, C3 and C4 lines.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r05a; mkdir -p $O
+O=gpurun_out/r05b; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }

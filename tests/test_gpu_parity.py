@@ -403,7 +403,7 @@ def test_wide_prefix_vs_oracle(dcf, lam, nb, depth, m):
             got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
             assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, depth, b, bound)
     prg.set_eval_mode(1)  # LAMBDA >= 32 has one head engine: the setting changes nothing
-    assert prg.eval_prefix_levels(nb, 1, m) == min(depth, 30, 8 * nb - 1)
+    assert prg.eval_prefix_levels(nb, 1, m) == want_d
     prg.set_prefix_levels(0)
     assert prg.eval_prefix_levels(nb, 1, m) == 0
 
