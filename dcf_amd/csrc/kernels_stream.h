@@ -477,8 +477,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_stream(
   __shared__ uint32_t lds[kLdsWords];
   lds_fill_tables(lds, tab);
   DCF_CLK(2, 0);
-  stream_run<NS, XREG, MULTI, kStreamUnit, !MULTI, PFX, NBC>(lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs,
-                                                           nbytes, num_keys, ppk, total, ctr, ys, pf);
+  // Round keys: per round from the device copy (GK), except in the multi-key instances with per-key
+  // top trees (C5), which keep them in SGPRs (device-copy keys cost C5 14 %, AB_LOG).  The multi-key
+  // instance without top trees (fewer than 32 points per key, or prefix levels forced off) has the
+  // root-seed start path as well and spilled 45 SGPRs with SGPR keys (r04 resource usage): with x in
+  // registers it takes the device-copy keys (0 spills); with x loaded per word the key look-ahead
+  // registers would spill 2 VGPRs to scratch instead, so it keeps SGPR keys (40 SGPR spills, to VGPR lanes).
+  constexpr bool GK = !MULTI || (!PFX && XREG);
+  stream_run<NS, XREG, MULTI, kStreamUnit, GK, PFX, NBC>(lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs,
+                                                       nbytes, num_keys, ppk, total, ctr, ys, pf);
   DCF_CLK(2, 1);
 }
 
