@@ -116,6 +116,8 @@ struct Workspace {
   size_t pfx_bytes = 0;
   uint8_t* d_mkey = nullptr;  // dcf_eval_multi_gpu_device: this device's copy of the key (CWB + s0)
   size_t mkey_bytes = 0;
+  uint32_t* d_tctr = nullptr; // LAMBDA >= 32 paired-slot tail with LDS-filling tables: per-workgroup block counters
+  size_t tctr_bytes = 0;
   // Host-pointer entry points: three non-blocking streams (copy-in, compute, copy-out), their
   // events and staging (pinned host + device), grown on demand and kept.
   hipStream_t hs[3] = {nullptr, nullptr, nullptr};
@@ -530,17 +532,18 @@ int launch_tail_passes(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np
 // repacked into chunk bytes in place, then the tail runs as launch_tail does.  (8-bit chunks in
 // global memory beside the LDS tables, read through the vector L1 / L2, measured 11-24 % slower on
 // C4: profiles/AB_LOG.md r04d.)
-template <int R6, int R5>
+template <int R6, int R5, int ROW0>
 int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
                  uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
-                 int cus, uint64_t ppk) {
-  using L = Tail2Layout<R6, R5>;
+                 int cus, uint64_t ppk, int party, Workspace* w) {
+  using L = Tail2Layout<R6, R5, ROW0>;
   if (nlev + 1 > L::rows()) return fail(DCF_ERR_UNSUPPORTED, "tail2 layout too small");
   const uint64_t tiles = (lam + 127) / 128;
-  hipLaunchKernelGGL((k_tvec_chunks<R6, R5>), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tvec, nlev, cnt);
+  hipLaunchKernelGGL((k_tvec_chunks<R6, R5, ROW0>), dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, tvec, nlev,
+                     cnt);
   HIP_TRY(hipGetLastError());
   const size_t lds = L::lds_bytes();
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5>),
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eval_wide_tail2<R6, R5, ROW0>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // One workgroup per CU at a time, kTail2Rounds rounds of them: the batch split into
   // rounds x cus / tiles ranges, so the tiles of a range build their tables once and walk its
@@ -556,8 +559,15 @@ int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, con
   const uint64_t per = std::max<uint64_t>(32768, (((cnt + ranges - 1) / ranges) + 255) & ~(uint64_t)255);
   const uint64_t rpk = (ppk + per - 1) / per;
   const dim3 grid((unsigned)tiles, (unsigned)((cnt / ppk) * rpk));
-  hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K, key,
-                     tvec, cnt, (uint32_t)per, ys, ppk, (uint32_t)rpk);
+  uint32_t* gctr = nullptr;
+  if (L::GCTR) {  // one block counter per workgroup (each workgroup resets its own)
+    uint8_t* b = reinterpret_cast<uint8_t*>(w->d_tctr);
+    if (int rc = grow(&b, &w->tctr_bytes, (size_t)grid.x * grid.y * kT2CtrStride * sizeof(uint32_t), st)) return rc;
+    w->d_tctr = reinterpret_cast<uint32_t*>(b);
+    gctr = w->d_tctr;
+  }
+  hipLaunchKernelGGL((k_eval_wide_tail2<R6, R5, ROW0>), grid, dim3(kBlock), lds, st, cws, cwv, np1, s0, nlev, lam, K,
+                     key, tvec, cnt, (uint32_t)per, ys, ppk, (uint32_t)rpk, (uint32_t)party, gctr);
   HIP_TRY(hipGetLastError());
   return DCF_OK;
 }
@@ -567,17 +577,34 @@ int launch_tail2(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, con
 // ppk: points per key (= cnt for one key).
 int run_tail(const uint8_t* cws, const uint8_t* cwv, const uint8_t* np1, const uint8_t* s0, uint32_t nlev,
              uint32_t lam, uint64_t K, uint64_t key, uint32_t* tvec, uint64_t cnt, uint8_t* ys, hipStream_t st,
-             int cus, uint64_t ppk) {
+             int cus, uint64_t ppk, int party, Workspace* w) {
   const uint32_t nrows = nlev + 1, nch = (nrows + 3) / 4;
   if (lam % 128 == 0) {
+    // Paired-slot layouts with row 0 folded into the constant (t_0 = party): the first that covers
+    // rows 1 .. n, in increasing reads per 16 bytes of y (2 (R6 + R5)), used when it beats the
+    // 4-bit tail's ceil((n + 1) / 4).  (r04 layouts, row 0 in the tables: N = 16 took (5, 7), 24 reads.)
 #define DCF_T2(A, B)                                                                               \
-  if (nrows <= Tail2Layout<A, B>::rows() && 2u * (A + B) < nch)                                    \
-    return launch_tail2<A, B>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus, ppk);
-    DCF_T2(1, 0)   // N = 1: 9 rows, 2 reads (4-bit: 3)
-    DCF_T2(1, 1)   // N = 2: 17 rows, 4 reads (5)
-    DCF_T2(2, 1)   // N = 3, 4: 25 / 33 rows, 6 reads (7 / 9)
-    DCF_T2(3, 3)   // N = 6..8: 49..65 rows, 12 reads (13..17)
-    DCF_T2(5, 7)   // N = 12..16: 97..129 rows, 24 reads (25..33)
+  if (nrows <= Tail2Layout<A, B, 1>::rows() && 2u * (A + B) < nch)                                 \
+    return launch_tail2<A, B, 1>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus, ppk, party, w);
+#ifndef DCF_T2_ROW0
+#define DCF_T2_ROW0 1
+#endif
+    if (!DCF_T2_ROW0) {  // A/B knob: the r04 layouts (row 0 in the tables)
+      if (nrows <= Tail2Layout<5, 7>::rows() && nrows > Tail2Layout<3, 3>::rows() && 24u < nch)
+        return launch_tail2<5, 7, 0>(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys, st, cus, ppk, party, w);
+    }
+    DCF_T2(0, 1)   // N = 1: 8 rows, 2 reads (4-bit: 3)
+    DCF_T2(2, 0)   // N = 2, 3: 16 / 24 rows, 4 reads (5 / 7)
+    DCF_T2(1, 2)   // N = 4: 32 rows, 6 reads (9)
+    DCF_T2(4, 0)   // N = 5, 6: 40 / 48 rows, 8 reads (11 / 13)
+    DCF_T2(3, 2)   // N = 7: 56 rows, 10 reads (15)
+    DCF_T2(6, 0)   // N = 8, 9: 64 / 72 rows, 12 reads (17 / 19)
+    DCF_T2(5, 2)   // N = 10: 80 rows, 14 reads (21)
+    DCF_T2(8, 0)   // N = 11, 12: 88 / 96 rows, 16 reads (23 / 25)
+    DCF_T2(7, 2)   // N = 13: 104 rows, 18 reads (27)
+    DCF_T2(10, 0)  // N = 14, 15: 112 / 120 rows, 20 reads (29 / 31), 160 KiB of tables
+    DCF_T2(9, 2)   // N = 16: 128 rows, 22 reads (33), 160 KiB of tables
+    DCF_T2(8, 4)   // N = 17: 136 rows, 24 reads (35), 160 KiB of tables
 #undef DCF_T2
   }
   // 4-bit tail: the widest tile whose tables (nch x 16 entries x TW bytes) fit the LDS
@@ -644,7 +671,7 @@ int eval_wide(dcf_prg* p, const Cfg& c, Workspace* w, size_t n_bytes, uint64_t K
     }
     HIP_TRY(hipGetLastError());
     if (lam > 32) {
-      rc = run_tail(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus, cnt);
+      rc = run_tail(cws, cwv, np1, s0, nlev, lam, K, key, tvec, cnt, ys + off * lam, st, p->cus, cnt, party, w);
       if (rc) return rc;
     }
   }
@@ -711,7 +738,7 @@ int eval_wide_batch(dcf_prg* p, Workspace* w, size_t n_bytes, uint64_t K, uint64
 #undef DCF_WHB
     HIP_TRY(hipGetLastError());
     if (lam > 32) {
-      if (int rc = run_tail(cws, cwv, np1, s0p, nlev, lam, K, k0, tvec, cnt, yp, st, p->cus, ppk)) return rc;
+      if (int rc = run_tail(cws, cwv, np1, s0p, nlev, lam, K, k0, tvec, cnt, yp, st, p->cus, ppk, party, w)) return rc;
     }
   }
   return DCF_OK;
@@ -879,7 +906,7 @@ static void free_workspace(Workspace* w) {
   if (w->aux) (void)hipStreamSynchronize(w->aux);
   if (w->pending) (void)hipEventSynchronize(w->done);  // the last device call's kernels
   for (void* b : {(void*)w->d_ctr, (void*)w->d_ws, (void*)w->d_dig, (void*)w->d_kdig, (void*)w->d_pfx,
-                  (void*)w->d_mkey, (void*)w->d_stage})
+                  (void*)w->d_mkey, (void*)w->d_stage, (void*)w->d_tctr})
     if (b) (void)hipFree(b);
   if (w->h_stage) (void)hipHostFree(w->h_stage);
   if (w->h_tiny) (void)hipHostFree(w->h_tiny);
@@ -959,7 +986,7 @@ size_t dcf_prg_device_bytes(const dcf_prg* p) {
   for (const Workspace* w : p->all_ws) {
     if (w->d_ctr) b += kCtrBytes;
     b += (size_t)w->dig_levels * 65 + w->kdig_bytes + w->ws_bytes + w->pfx_bytes +
-         w->d_stage_bytes + w->mkey_bytes;
+         w->d_stage_bytes + w->mkey_bytes + w->tctr_bytes;
   }
   return b;
 }

@@ -310,24 +310,41 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail(const uint8_t* __rest
 // the index of chunk k: chunks 0 .. 2 R6 - 1 are 6 rows each from row 0, then 5-row chunks.
 // Rows past n + 1 are zero.  Kept in place in the head's 64-byte t-vector rows (first 32 B).
 // ------------------------------------------------------------------------
-template <int R6, int R5>
+// ROW0 = 1 ("party folded"): row 0's coefficient is t_0 = party (lib.rs:169), the same for every
+// point of the call, so its W row joins the constant (s0 ^ party W_0) and the chunks cover rows
+// 1 .. n only — at N = 16 that is 128 rows, which (R6, R5) = (9, 2) covers in 22 reads per 16 bytes
+// of y instead of (5, 7)'s 24, in exactly 160 KiB of LDS: the workgroup's block counter then lives
+// in global memory (GCTR).
+constexpr uint32_t kLdsMaxBytes = 160u * 1024u;
+#ifndef DCF_T2_CLAIM
+#define DCF_T2_CLAIM 4
+#endif
+constexpr uint32_t kT2ClaimBlocks = DCF_T2_CLAIM;  // 16-point blocks per global-counter claim (GCTR layouts; r05e A/B
+                                                   // on C4 with 128-B-line counters: 1 / 4 / 16 blocks 32.4-32.7 / 32.0 / 31.8 ms)
+#ifndef DCF_T2_CTR_STRIDE
+#define DCF_T2_CTR_STRIDE 1
+#endif
+constexpr uint32_t kT2CtrStride = DCF_T2_CTR_STRIDE;  // words between workgroups' counters (r05e A/B: packed 31.57 / 31.73 ms
+                                                     // vs one 128-B line each 32.01 / 32.00 on C4)
+template <int R6, int R5, int ROW0 = 0>
 struct Tail2Layout {
   static constexpr int R = R6 + R5, NC = 2 * R;
   static_assert(NC <= 32, "t-vector holds 32 chunk bytes");
   static constexpr uint32_t width(int k) { return k < 2 * R6 ? 6u : 5u; }
-  static constexpr uint32_t start(int k) { return k < 2 * R6 ? 6u * k : 12u * R6 + 5u * (k - 2 * R6); }
+  static constexpr uint32_t start(int k) { return (uint32_t)ROW0 + (k < 2 * R6 ? 6u * k : 12u * R6 + 5u * (k - 2 * R6)); }
   static constexpr uint32_t region(int m) { return m < R6 ? 16384u * m : 16384u * R6 + 8192u * (m - R6); }
-  static constexpr uint32_t rows() { return 12u * R6 + 10u * R5; }
-  static constexpr uint32_t lds_bytes() { return region(R) + 16u; }  // + the workgroup's block counter
+  static constexpr uint32_t rows() { return (uint32_t)ROW0 + 12u * R6 + 10u * R5; }  // rows 0 .. rows() - 1 covered
+  static constexpr bool GCTR = region(R) + 16u > kLdsMaxBytes;  // no LDS left for the block counter
+  static constexpr uint32_t lds_bytes() { return GCTR ? region(R) : region(R) + 16u; }
 };
 
 // Old nibble t-vector (row r at byte r >> 2, bit r & 3; words 0 .. nlev >> 4 valid) -> chunk
 // bytes of Tail2Layout<R6, R5>, in place (bytes [0, 32) of each 64-byte row).  One thread
 // per point: the row's first 16-byte pieces the layout's rows need read whole (unwritten
 // words hold rows past t_n, cleared below), 32 bytes written.
-template <int R6, int R5>
+template <int R6, int R5, int ROW0 = 0>
 __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, const uint64_t count) {
-  using L = Tail2Layout<R6, R5>;
+  using L = Tail2Layout<R6, R5, ROW0>;
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= count) return;
   uint32_t* row = tvec + p * kTWords;
@@ -367,7 +384,26 @@ __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, 
   o4[1] = make_uint4(out[4], out[5], out[6], out[7]);
 }
 
-template <int R6, int R5>
+// W row r (coefficient t_r) piece at byte offset off of key `key`, as the table build forms it:
+// cw_v[r] ^ (r + 1 even ? cw_s[r] : 0) for r < n, cw_np1 for r = n, bit 0 of byte LAMBDA - 1 per the
+// file header; zero for an offset outside [32, LAMBDA).
+__device__ __forceinline__ uint4 tail_w_row(const uint8_t* __restrict__ cw_s, const uint8_t* __restrict__ cw_v,
+                                            const uint8_t* __restrict__ cw_np1, uint32_t nlev, uint32_t lam,
+                                            uint64_t num_keys, uint64_t key, uint32_t r, uint32_t off) {
+  if (off < 32u || off >= lam) return make_uint4(0u, 0u, 0u, 0u);
+  if (r == nlev) return *reinterpret_cast<const uint4*>(cw_np1 + key * lam + off);
+  const uint64_t ro = ((uint64_t)r * num_keys + key) * lam + off;
+  const uint4 cv = *reinterpret_cast<const uint4*>(cw_v + ro), cs = *reinterpret_cast<const uint4*>(cw_s + ro);
+  const uint32_t l = r + 1u, even = (l & 1u) ? 0u : 0xFFFFFFFFu;
+  uint4 x = make_uint4(cv.x ^ (cs.x & even), cv.y ^ (cs.y & even), cv.z ^ (cs.z & even), cv.w ^ (cs.w & even));
+  if (off + 16 == lam) {  // bit 0 of byte LAMBDA-1: cw_s joins only at l == n
+    const uint32_t bit = (cv.w ^ ((l == nlev) ? cs.w : 0u)) & 0x01000000u;
+    x.w = (x.w & ~0x01000000u) | bit;
+  }
+  return x;
+}
+
+template <int R6, int R5, int ROW0 = 0>
 __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __restrict__ cw_s,
                                                              const uint8_t* __restrict__ cw_v,
                                                              const uint8_t* __restrict__ cw_np1,
@@ -376,8 +412,9 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
                                                              const uint64_t key0, const uint32_t* __restrict__ tvec,
                                                              const uint64_t count, const uint32_t pts_per_block,
                                                              uint8_t* __restrict__ ys, const uint64_t ppk,
-                                                             const uint32_t rpk) {
-  using L = Tail2Layout<R6, R5>;
+                                                             const uint32_t rpk, const uint32_t party,
+                                                             uint32_t* __restrict__ gctr) {
+  using L = Tail2Layout<R6, R5, ROW0>;
   constexpr int TW = 128, LP = 8;
   // Row blockIdx.y of the grid = range rr of key kk of the launch's keys (as k_eval_wide_tail)
   const uint32_t kk = blockIdx.y / rpk, rr = blockIdx.y % rpk;
@@ -396,7 +433,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
       if (it < items6) { k = it / (LP * 8); rest = it % (LP * 8); w = 6u; }
       else { k = 2 * R6 + (it - items6) / (LP * 4); rest = (it - items6) % (LP * 4); w = 5u; }
       const uint32_t q = rest % LP, g = rest / LP;
-      const uint32_t st = k < 2u * R6 ? 6u * k : 12u * R6 + 5u * (k - 2u * R6);
+      const uint32_t st = (uint32_t)ROW0 + (k < 2u * R6 ? 6u * k : 12u * R6 + 5u * (k - 2u * R6));
       const uint32_t off = byte0 + 16u * q;
       // W rows st .. st + 5 (row st + b used if b < w): all 12 loads issued before any is
       // used (w_row_piece's branches would serialise them), addresses clamped, then masked.
@@ -447,9 +484,14 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
       }
     }
   }
-  // the workgroup's block counter, past the tables
-  uint32_t* bctr = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(G) + L::region(L::R));
-  if (threadIdx.x == 0) *bctr = 0u;
+  // the workgroup's block counter: past the tables, or (GCTR: the tables fill the LDS) its own word
+  // of gctr, reset here (an atomic store at L2, where the claims' atomics run; the barrier orders it)
+  uint32_t* bctr = L::GCTR ? gctr + kT2CtrStride * ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x)
+                           : reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(G) + L::region(L::R));
+  if (threadIdx.x == 0) {
+    if (L::GCTR) __hip_atomic_store(bctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *bctr = 0u;
+  }
   __syncthreads();
   DCF_CLK(0, 0);
   const uint32_t q = threadIdx.x % LP;
@@ -460,6 +502,10 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   if (lane_live) {
     cst = *reinterpret_cast<const uint4*>(s0 + (uint64_t)kk * lam + off);
     if (off + 16 == lam) cst.w &= kMaskLast;
+    if (ROW0 && party) {  // row 0 (t_0 = party for every point) folded into the constant
+      const uint4 w0 = tail_w_row(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, 0u, off);
+      cst = make_uint4(cst.x ^ w0.x, cst.y ^ w0.y, cst.z ^ w0.z, cst.w ^ w0.w);
+    }
   }
   // lane constants (address byte 0 = slot, byte 2 = 64 KiB group): step i of a region reads
   // chunk 2m + (i ^ pi), whose entry sits in bytes [(i ^ pi) 128, +128) of the 256-B row
@@ -504,19 +550,24 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   const uint32_t nblk = p1 > p0 ? (uint32_t)((p1 - p0 + 15) / 16) : 0u;
   auto claim = [&]() -> uint32_t {
     uint32_t b = 0u;
-    if ((threadIdx.x & 63u) == 0) b = __hip_atomic_fetch_add(bctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if ((threadIdx.x & 63u) == 0)
+      b = L::GCTR ? __hip_atomic_fetch_add(bctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                  : __hip_atomic_fetch_add(bctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return __builtin_amdgcn_readfirstlane(b);
   };
   const uint32_t dead = 0x80000000u;
   const uint32_t kill = lane_live ? 0u : dead;
+  // GCTR: the counter is a global atomic, so a claim takes kT2ClaimBlocks consecutive blocks
+  constexpr uint32_t CB = L::GCTR ? kT2ClaimBlocks : 1u;
+  auto next_block = [&](uint32_t b) -> uint32_t { return ((b + 1u) % CB) ? b + 1u : claim() * CB; };
   uint4 ta[2], tb[2];
   uint32_t twa[NW], twb[NW];
-  uint32_t bc = claim();
+  uint32_t bc = claim() * CB;
   load_t(ta, p0 + 16u * bc + pin);
   load_t(tb, p0 + 16u * bc + 8u + pin);
   rotate(ta, twa);
   rotate(tb, twb);
-  uint32_t bn = claim();
+  uint32_t bn = next_block(bc);
   load_t(ta, p0 + 16u * bn + pin);
   load_t(tb, p0 + 16u * bn + 8u + pin);
   while (bc < nblk) {
@@ -560,7 +611,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
     bc = bn;
     rotate(ta, twa);
     rotate(tb, twb);
-    bn = claim();
+    bn = next_block(bc);
     load_t(ta, p0 + 16u * bn + pin);
     load_t(tb, p0 + 16u * bn + 8u + pin);
   }

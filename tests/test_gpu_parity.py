@@ -352,12 +352,14 @@ def test_small_pair_prefix_vs_oracle(dcf, nb, levels, m):
 @pytest.mark.parametrize("lam,nb,m", [(128, 1, 300), (256, 3, 200), (128, 4, 500), (384, 6, 300), (128, 8, 40000),
                                       (256, 12, 150), (128, 16, 33000), (256, 5, 100), (128, 9, 300),
                                       (256, 10, 200), (128, 11, 40000), (384, 13, 200), (128, 14, 300),
-                                      (256, 15, 500)])
+                                      (256, 15, 500), (128, 2, 300), (256, 7, 200), (128, 17, 200)])
 def test_wide_tail2_layouts_vs_oracle(dcf, lam, nb, m):
-    """The paired-slot tail (k_eval_wide_tail2, LAMBDA % 128 == 0) in each instantiated chunk
-    layout: N = 1 (1,0), 3 and 4 (2,1), 6 and 8 (3,3), 12..16 (5,7), plus N = 5 and 9..11, which
-    keep the 4-bit tail; 40000 / 33000 points cross the 32768-point workgroup ranges, and the
-    t-vector repack (k_tvec_chunks) runs in place on the head's rows."""
+    """The paired-slot tail (k_eval_wide_tail2, LAMBDA % 128 == 0) in every instantiated chunk
+    layout, row 0 (t_0 = party) folded into the constant (r05): N = 1 (0,1), 2 and 3 (2,0), 4
+    (1,2), 5 and 6 (4,0), 7 (3,2), 8 and 9 (6,0), 10 (5,2), 11 and 12 (8,0), 13 (7,2), 14 and 15
+    (10,0) and 16 (9,2) (both LDS-filling: global block counters), 17 (8,4); 40000 / 33000 points
+    cross the 32768-point workgroup ranges, and the t-vector repack (k_tvec_chunks) runs in place
+    on the head's rows.  Both parties: party 1 takes the folded row, party 0 not."""
     rng = np.random.default_rng(lam * 13 + nb)
     keys = [rng.bytes(32) for _ in range(18)]
     prg, P = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
