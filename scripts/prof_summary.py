@@ -90,6 +90,7 @@ def pmc_traffic(d, kernel_prefix="k_eval16<0>", suffix=""):
     if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
         out["read_bytes_corrected"] = 2 * out["FETCH_SIZE"]
         out["traffic_bytes"] = 2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]
+        out["traffic_bytes_x1"] = out["FETCH_SIZE"] + out["WRITE_SIZE"]
     return out
 
 
