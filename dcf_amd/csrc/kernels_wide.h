@@ -535,7 +535,8 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
     const uint32_t grp = (rb >> 16) << 16;  // compile-time per m: the 64 KiB group in address byte 2
     const int c = 2 * m + i;               // byte of the rotated chunk vector
     const uint32_t a = __builtin_amdgcn_perm(tw[c >> 2], (i ? lc1 : lc0) | grp, 0x0c020000u | ((4u + (c & 3)) << 8));
-    return lds_load16(a + (rb & 0xFFFFu));  // the rest of the region base rides in the offset field
+    // the rest of the region base rides in the offset field
+    return *(__attribute__((address_space(3))) const u32x4_t*)(size_t)(a + (rb & 0xFFFFu));
   };
   // Work: 16-point blocks of the workgroup's range, claimed per wave from the LDS counter (A = the
   // block's first 8 points, B = the next 8; a lane owns one 16-byte piece of one point of each).
@@ -560,6 +561,45 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   // GCTR: the counter is a global atomic, so a claim takes kT2ClaimBlocks consecutive blocks
   constexpr uint32_t CB = L::GCTR ? kT2ClaimBlocks : 1u;
   auto next_block = [&](uint32_t b) -> uint32_t { return ((b + 1u) % CB) ? b + 1u : claim() * CB; };
+  // BT regions (4 reads each) are issued before their XORs: the compiler otherwise waits after
+  // every two reads, ~3 reads in flight per wave.  All R regions into the accumulators.
+  auto regions = [&](const uint32_t (&twa)[NW], const uint32_t (&twb)[NW], uint32_t (&aa)[4], uint32_t (&ab)[4]) {
+    constexpr int BT = 2;
+#pragma unroll
+    for (int m0 = 0; m0 < L::R; m0 += BT) {
+      u32x4_t rb[BT][4];
+#pragma unroll
+      for (int k = 0; k < BT; ++k)
+        if (m0 + k < L::R) {
+          rb[k][0] = rd(twa, m0 + k, 0); rb[k][1] = rd(twa, m0 + k, 1);
+          rb[k][2] = rd(twb, m0 + k, 0); rb[k][3] = rd(twb, m0 + k, 1);
+        }
+      // the batch's reads are all issued before the first result is used: a memory clobber
+      // keeps them above, and one empty asm per read (issued in order) makes each XOR wait
+      // for its own read only (lgkmcnt counts down in order).  One 128-bit operand per read:
+      // four 32-bit operands let the allocator copy the tuple apart (a per-lane 64-bit row
+      // address in the loop then spilled ~120 VGPRs, r05j)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < BT; ++k)
+        if (m0 + k < L::R)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(rb[k][j]));
+#pragma unroll
+      for (int k = 0; k < BT; ++k)
+        if (m0 + k < L::R) {
+          const u32x4_t a0 = rb[k][0], a1 = rb[k][1], b0 = rb[k][2], b1 = rb[k][3];
+          aa[0] = xor3(aa[0], a0.x, a1.x); aa[1] = xor3(aa[1], a0.y, a1.y);
+          aa[2] = xor3(aa[2], a0.z, a1.z); aa[3] = xor3(aa[3], a0.w, a1.w);
+          ab[0] = xor3(ab[0], b0.x, b1.x); ab[1] = xor3(ab[1], b0.y, b1.y);
+          ab[2] = xor3(ab[2], b0.z, b1.z); ab[3] = xor3(ab[3], b0.w, b1.w);
+        }
+      // the accumulators are materialised here, before the next batch's reads (else the XORs
+      // may sink below them and every read result stays live: the r05j sorted tail spilled)
+      asm volatile("" : "+v"(aa[0]), "+v"(aa[1]), "+v"(aa[2]), "+v"(aa[3]), "+v"(ab[0]), "+v"(ab[1]), "+v"(ab[2]),
+                   "+v"(ab[3]));
+    }
+  };
   uint4 ta[2], tb[2];
   uint32_t twa[NW], twb[NW];
   uint32_t bc = claim() * CB;
@@ -572,38 +612,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   load_t(tb, p0 + 16u * bn + 8u + pin);
   while (bc < nblk) {
     uint32_t aa[4] = {cst.x, cst.y, cst.z, cst.w}, ab[4] = {cst.x, cst.y, cst.z, cst.w};
-    constexpr int BT = 2;
-    // BT regions (4 reads each) are issued before their XORs: the compiler
-    // otherwise waits after every two reads, ~3 reads in flight per wave
-#pragma unroll
-    for (int m0 = 0; m0 < L::R; m0 += BT) {
-      uint4 rb[BT][4];
-#pragma unroll
-      for (int k = 0; k < BT; ++k)
-        if (m0 + k < L::R) {
-          rb[k][0] = rd(twa, m0 + k, 0); rb[k][1] = rd(twa, m0 + k, 1);
-          rb[k][2] = rd(twb, m0 + k, 0); rb[k][3] = rd(twb, m0 + k, 1);
-        }
-      // the batch's reads are all issued before the first result is used: a memory clobber
-      // keeps them above, and one empty asm per read (issued in order) makes each XOR wait
-      // for its own read only (lgkmcnt counts down in order)
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int k = 0; k < BT; ++k)
-        if (m0 + k < L::R)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            asm volatile("" : "+v"(rb[k][j].x), "+v"(rb[k][j].y), "+v"(rb[k][j].z), "+v"(rb[k][j].w));
-#pragma unroll
-      for (int k = 0; k < BT; ++k)
-        if (m0 + k < L::R) {
-          const uint4 a0 = rb[k][0], a1 = rb[k][1], b0 = rb[k][2], b1 = rb[k][3];
-          aa[0] = xor3(aa[0], a0.x, a1.x); aa[1] = xor3(aa[1], a0.y, a1.y);
-          aa[2] = xor3(aa[2], a0.z, a1.z); aa[3] = xor3(aa[3], a0.w, a1.w);
-          ab[0] = xor3(ab[0], b0.x, b1.x); ab[1] = xor3(ab[1], b0.y, b1.y);
-          ab[2] = xor3(ab[2], b0.z, b1.z); ab[3] = xor3(ab[3], b0.w, b1.w);
-        }
-    }
+    regions(twa, twb, aa, ab);
     const uint64_t pw = p0 + 16u * bc, pa = pw + pin, pb = pa + 8u;
     tail_store<LP>(ys, pw, pin, lam, off, kill | (pa < p1 ? 0u : dead), make_uint4(aa[0], aa[1], aa[2], aa[3]));
     tail_store<LP>(ys, pw + 8u, pin, lam, off, kill | (pb < p1 ? 0u : dead), make_uint4(ab[0], ab[1], ab[2], ab[3]));
