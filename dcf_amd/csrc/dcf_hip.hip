@@ -1163,6 +1163,8 @@ static int gen_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, con
     HIP_TRY(hipMemsetAsync(w->d_ctr, 0, kCtrBytes, st));
     ctr = w->d_ctr;
   }
+  // Round keys in SGPRs (22 / 26 SGPR spills into VGPR lanes in the one-lane / quad instances):
+  // per-round keys from the device copy spill none but gen ran 1-1.5 % slower (C5 r05l).
 #define DCF_GEN16(LN)                                                                                           \
   hipLaunchKernelGGL(k_gen16<LN>, dim3((unsigned)grid_for(items, p->cus)), dim3(kBlock), 0, st, p->d_tab, p->rk[0], \
                      alpha, (const uint4*)beta, (const uint4*)s0_0, (const uint4*)s0_1, (uint32_t)bound,          \
@@ -1192,6 +1194,11 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
 // table / digest preparation), 2 at the end.
 static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party, const uint8_t* cwb,
                      const uint8_t* s0s, const uint8_t* xs, uint8_t* ys);
+
+#ifndef DCF_MK_NBC16
+#define DCF_MK_NBC16 1
+#endif
+constexpr bool kMkNbc16 = DCF_MK_NBC16;  // A/B knob: the N = 16 multi-key top-tree instance
 
 static int eval_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party,
                        const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys) {
@@ -1433,11 +1440,13 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
                      lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes, (uint64_t)kc, \
                      (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0)
       // multi-key: an instance for "per-key top trees present" (no root-seed start path: 48 -> 33
-      // SGPR spills; C5 r03c A/B 414.6 / 413.7 vs 408.5 / 408.1 M evals/s).  Single key, x in
+      // SGPR spills; C5 r03c A/B 414.6 / 413.7 vs 408.5 / 408.1 M evals/s), and of it one with the
+      // x width fixed at N = 16 (C5: 33 -> 18 SGPR spills, 121 -> 119 VGPRs, r05k).  Single key, x in
       // registers: N = 16 (C1 / C3) and N = 4 (C2) with the x width fixed at compile time (a
       // point's start loads x without width branches: C2 starts a point every ~13 AES slots).
       if (multi && lpf.levels) {
-        if (xreg) DCF_STREAM(true, true, true, 0);
+        if (xreg && n_bytes == 16 && kMkNbc16) DCF_STREAM(true, true, true, 16);
+        else if (xreg) DCF_STREAM(true, true, true, 0);
         else DCF_STREAM(false, true, true, 0);
       } else if (multi) {
         if (xreg) DCF_STREAM(true, true, false, 0);
