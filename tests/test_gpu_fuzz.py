@@ -4,7 +4,8 @@ that the hand-picked parity cases do not name, each checked bit for bit against 
 
 Every case runs gen through the C ABI and compares the CWB with the oracle's key
 (lib.rs:86-161), then evaluates both parties (lib.rs:163-204) on random points with x = alpha
-planted, and checks y0 ^ y1 against beta * [x < alpha] / [x > alpha] (lib.rs:114-125 and the
+planted (host-buffer entry point; batches of 64 or more also through the device-buffer one),
+and checks y0 ^ y1 against beta * [x < alpha] / [x > alpha] (lib.rs:114-125 and the
 reconstruction KATs, lib.rs:372-420).  The shapes come from a fixed seed, so a failure names a
 reproducible case id.
 """
@@ -18,7 +19,7 @@ pytestmark = pytest.mark.gpu
 LAMS = [16, 16, 16, 32, 48, 64, 80, 96, 112, 128, 144, 256, 272, 384, 512, 1024]
 
 
-def _cases(n=48, seed=0xF022):
+def _cases(n=128, seed=0xF022):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
@@ -32,7 +33,7 @@ def _cases(n=48, seed=0xF022):
     return out
 
 
-def _mk_cases(n=10, seed=0xF0A2):
+def _mk_cases(n=24, seed=0xF0A2):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
@@ -95,6 +96,12 @@ def test_fuzz_single_key_vs_oracle(dcf, case):
         got = d.eval(bool(b), dcf.Share([s], k.cws, k.cw_np1), xs)
         assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), f"party {b}"
         ys.append(np.asarray(got))
+    if m >= 64:  # the device-buffer entry point gives the same bytes
+        import torch
+        T = lambda v: torch.from_numpy(np.frombuffer(v, np.uint8).copy() if isinstance(v, bytes) else v).cuda()  # noqa: E731
+        yd = d.eval_device(True, T(dcf.share_to_cwb(k, nb, lam)), T(s1), T(xs))
+        torch.cuda.synchronize()
+        assert np.array_equal(yd.cpu().numpy(), ys[1]), "eval_device"
     if bound == 0:
         want = np.where(_lt(xs, a)[:, None], np.frombuffer(beta, np.uint8)[None, :], 0)
     else:  # GtBeta: beta where x > alpha
