@@ -122,11 +122,24 @@ struct Sel {
       ((T & 1) ? 1u : 0u) | ((4u + K) << 8) | (((T >> 1) ? 2u : 0x0cu) << 16) | (0x0cu << 24);
 };
 
-template <int T, int K>
+#ifndef DCF_T1_BITOP3
+#define DCF_T1_BITOP3 1
+#endif
+// B1: T1 at state byte 1 through the v_bitop3.  Same-box A/Bs, 3 alternating runs (r05s, r05t): C5
+// 317.2-317.8 vs 319.0-319.3 and 323.6-324.1 vs 325.3-325.5 ms, C3 492.8-494.5 vs 494.0-494.6 and
+// 502.7-504.4 vs 504.1-504.5, C2 3.446-3.452 vs 3.456-3.457 — kept; the λ ≥ 32 head (aes_tt_lka)
+// ran 31.21-31.23 vs 30.91-30.97 ms with it, so it keeps the v_perm.
+template <int T, int K, bool B1 = true>
 __device__ __forceinline__ uint32_t lk(const uint32_t* lds, uint32_t w, uint32_t lc) {
-  // (T1's address through one v_bitop3 instead of the v_perm measured the same: the rounds sit at
-  // the LDS-issue ceiling, AB_LOG ab_t1)
-  const uint32_t addr = __builtin_amdgcn_perm(w, lc, Sel<T, K>::v);
+  uint32_t addr;
+  if (DCF_T1_BITOP3 && B1 && T == 1 && K == 1) {
+    // T1 at state byte 1: the byte already sits at address bits 8..15, so one 2-cycle v_bitop3
+    // (w & 0xFF00) | slot builds the address instead of a 4-cycle v_perm (the slot byte is
+    // loop-invariant: hoisted once)
+    addr = __builtin_amdgcn_bitop3_b32(w, 0xFF00u, (lc >> 8) & 0xFFu, 0xEA);
+  } else {
+    addr = __builtin_amdgcn_perm(w, lc, Sel<T, K>::v);
+  }
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + addr);
 }
 
@@ -228,10 +241,10 @@ __device__ __forceinline__ void aes_tt_lka(uint32_t (&st)[NB][4], const uint32_t
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (r < NR) {
-          const uint32_t a = lk<0, 0>(lds, st[b][j], lc);
-          const uint32_t c = lk<1, 1>(lds, st[b][(j + 1) & 3], lc);
-          const uint32_t d = lk<2, 2>(lds, st[b][(j + 2) & 3], lc);
-          const uint32_t e = lk<3, 3>(lds, st[b][(j + 3) & 3], lc);
+          const uint32_t a = lk<0, 0, false>(lds, st[b][j], lc);
+          const uint32_t c = lk<1, 1, false>(lds, st[b][(j + 1) & 3], lc);
+          const uint32_t d = lk<2, 2, false>(lds, st[b][(j + 2) & 3], lc);
+          const uint32_t e = lk<3, 3, false>(lds, st[b][(j + 3) & 3], lc);
           o[b][j] = xor3(xor3(a, c, d), e, kw[j]);
         } else {  // final round: S(x) sits in byte r of T_{(r+2)&3}
           const uint32_t a = lk<2, 0>(lds, st[b][j], lc);
