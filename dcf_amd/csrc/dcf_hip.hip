@@ -1195,6 +1195,14 @@ int dcf_gen_batch_device(dcf_prg* p, size_t n_bytes, size_t num_keys, const uint
 static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party, const uint8_t* cwb,
                      const uint8_t* s0s, const uint8_t* xs, uint8_t* ys);
 
+#ifndef DCF_SK_PFX
+#define DCF_SK_PFX 1
+#endif
+// Single key below a shared-prefix table (C2 / C3 shapes): the instance whose starts all take the
+// table row (PFX), so the fresh-x-word path (4 selects per stream and step) is compiled out; 87 ->
+// 74 SGPRs.  r05v A/B (same box, 3 alternating runs): C3 491.3-491.7 vs 493.1-493.9 ms, C2
+// 3.354-3.360 vs 3.391-3.396 ms (round 2's attempt at this split lost to a register-allocation flip).
+constexpr bool kSkPfx = DCF_SK_PFX;
 #ifndef DCF_MK_NBC16
 #define DCF_MK_NBC16 1
 #endif
@@ -1451,8 +1459,12 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       } else if (multi) {
         if (xreg) DCF_STREAM(true, true, false, 0);
         else DCF_STREAM(false, true, false, 0);
+      } else if (xreg && n_bytes == 16 && lpf.levels && kSkPfx) {
+        DCF_STREAM(true, false, true, 16);  // every start below the shared prefix: no fresh-x-word path
       } else if (xreg && n_bytes == 16) {
         DCF_STREAM(true, false, false, 16);
+      } else if (xreg && n_bytes == 4 && lpf.levels && kSkPfx) {
+        DCF_STREAM(true, false, true, 4);
       } else if (xreg && n_bytes == 4) {
         DCF_STREAM(true, false, false, 4);
       } else if (xreg) {
