@@ -421,7 +421,8 @@ __device__ __forceinline__ void stream_run(
       L.ph[i] = adv ^ 1u;
       uint32_t nl = L.lev[i] + adv;
       L.cur[i] <<= adv;
-      if (adv && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+      // (x in one word, NBC <= 4: the only crossing ends the point, so no next word is taken)
+      if (!(NBC && NBC <= 4) && adv && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
       L.ci[i] += adv;
       {  // reuse: level nl with B known: its B half now, without an AES slot (branch-free)
         const uint32_t xb2 = L.cur[i] >> 31, t1 = L.t[i], tm1 = 0u - t1;
@@ -441,7 +442,7 @@ __device__ __forceinline__ void stream_run(
         nl += rr & 1u;
         L.cur[i] <<= (rr & 1u);
         L.ci[i] += rr & 1u;
-        if (rr && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+        if (!(NBC && NBC <= 4) && rr && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
       }
       L.lev[i] = nl;
     }
