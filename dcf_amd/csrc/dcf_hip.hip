@@ -301,13 +301,15 @@ uint32_t prefix_dfs_levels(uint32_t levels, uint32_t S) {
 // Shared-prefix depth for a single-key stream eval of `total` points (kernels_stream.h
 // PrefixTable): the top tree has 2^D nodes (33 B each, built with 2^(D+1) AES blocks)
 // and saves every point D levels.  Auto: D = log2(total) - 1 (table build < 1 block per
-// point; Hirose: log2(total)), at most kPrefixMax = 26 (a 2.2 GB table of 32-B rows inside 4.4 GB of build
-// buffers, 2 x 2^26 x 33 B), none below 8, always < 8N.  If the buffers cannot be
+// point; Hirose: log2(total)), at most kPrefixMax = 27 (a 4.3 GB table of 32-B rows beside 4.4 GB of build
+// buffers), none below 8, always < 8N.  If the buffers cannot be
 // allocated in auto mode, eval retries 2 levels shallower down to 8, then runs without a
 // table (identical bytes; see try_prefix).  Measured (r01i, C2: 2^24 points, N = 4):
 // D = 12 / 16 / 20 / 24 -> 2.00 / 2.29 / 2.62 / 2.83 G evals/s (1.44 without);
 // C3 (2^28, N = 16): D = 16 / 24 / 26 -> 450 / 477 / ~482 M (397 M without; r01q/r).
-constexpr uint32_t kPrefixMax = 26;       // auto (C3 r01q sweep: 24 519, 25 521, 26 524, 27 524 M evals/s)
+// auto cap.  C3 sweeps (2^28 points): r01q 24 519, 25 521, 26 524, 27 524 M evals/s; r05y (today's
+// walk, 2 runs, ms per step) 25 495.5 / 495.5, 26 491.6 / 492.0, 27 489.3 / 488.8, 28 488.9 / 488.8
+constexpr uint32_t kPrefixMax = 27;
 constexpr uint32_t kPrefixMaxForced = 28;  // dcf_prg_set_prefix_levels (2^28 x 33 B x 2 = 17.7 GB)
 // Device bytes of a shared-prefix table of depth d (table + build buffers, as build_prefix /
 // build_wide_prefix allocate them).

@@ -158,15 +158,15 @@ def test_config_c2(dcf):
 
 def test_config_c3(dcf):
     """C3: N = 16 (128-bit x), LAMBDA = 16, one key at 2^28 points on one GPU (the bench's
-    N = 1 shape), auto shared prefix D = 26; the sample holds both ends of every one of the
+    N = 1 shape), auto shared prefix D = 27; the sample holds both ends of every one of the
     2^20 256-point stream units (~2.1 M oracle evals per party, ~0.5 s on 16 threads)."""
-    _single_key_device(dcf, 16, 1 << 28, 26, 0xC3, 256)
+    _single_key_device(dcf, 16, 1 << 28, 27, 0xC3, 256)
 
 
 def test_config_c3_strong_slices(dcf):
     """C3 sharded over G = 8 GPUs (strong scaling, bench.py's default): each GPU evaluates
     a contiguous 2^25-point slice of the 2^28 points (dcf_point_slice), with its own auto
-    prefix depth (25 instead of 26).  The first and last slices, evaluated alone, must
+    prefix depth (25 instead of 27).  The first and last slices, evaluated alone, must
     equal the same rows of the whole-batch eval byte for byte."""
     import torch
     nb, lam = 16, 16

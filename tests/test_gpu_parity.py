@@ -176,7 +176,7 @@ def test_eval_prefix_table_vs_oracle(dcf, nb, levels):
     prg.set_prefix_levels(0)
     assert prg.eval_prefix_levels(nb, 1, m) == 0
     prg.set_prefix_levels(-1)
-    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 26  # auto: log2(points), capped
+    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 27  # auto: log2(points), capped
     assert prg.eval_prefix_levels(16, 1, 1 << 20) == 20
     assert prg.eval_prefix_levels(2, 1, 1 << 20) == 15   # < 8N
     assert prg.eval_prefix_levels(16, 2, 1 << 20) == 0   # one key only

@@ -188,7 +188,7 @@ def test_prefix_memory_cap_and_device_bytes(dcf):
     keys = [rng.bytes(32) for _ in range(2)]
     prg = dcf.Aes256HirosePrg(keys, 16)
     d = dcf.DcfImpl(16, 16, prg)
-    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 26
+    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 27
     prg.set_prefix_max_bytes(1 << 30)
     assert prg.eval_prefix_levels(16, 1, 1 << 28) == 23  # 2^23 x ~65 B fits 1 GiB, 2^24 does not
     prg.set_prefix_max_bytes(1000)
