@@ -1209,6 +1209,12 @@ constexpr bool kSkPfx = DCF_SK_PFX;
 #define DCF_MK_NBC16 1
 #endif
 constexpr bool kMkNbc16 = DCF_MK_NBC16;  // A/B knob: the N = 16 multi-key top-tree instance
+#ifndef DCF_MK_PK2
+#define DCF_MK_PK2 1
+#endif
+// ... and of it, for a power-of-two points per key (C5: 64), point -> key by a shift instead of
+// the division sequence (65 fewer VALU in the kernel)
+constexpr bool kMkPk2 = DCF_MK_PK2;
 
 static int eval_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party,
                        const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys) {
@@ -1445,8 +1451,10 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       uint8_t* lys = ys + c0 * lam;
       const uint8_t* ls0 = s0s + k0 * lam;
       const PrefixTable lpf = (multi && pf.levels) ? PrefixTable{pf.sv + 2 * (k0 << pf.levels), pf.levels} : pf;
-#define DCF_STREAM(XR, MK, PF, NBC)                                                                             \
-  hipLaunchKernelGGL((k_eval16_stream<NS, XR, MK, PF, NBC>), dim3((unsigned)blocks), block, 0, st, p->d_tab, p->rk[0], \
+#define DCF_STREAM(XR, MK, PF, NBC) DCF_STREAM6(XR, MK, PF, NBC, false)
+#define DCF_STREAM6(XR, MK, PF, NBC, PK2)                                                                       \
+  hipLaunchKernelGGL((k_eval16_stream<NS, XR, MK, PF, NBC, PK2>), dim3((unsigned)blocks), block, 0, st, p->d_tab,  \
+                     p->rk[0],                                                                                 \
                      lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes, (uint64_t)kc, \
                      (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0)
       // multi-key: an instance for "per-key top trees present" (no root-seed start path: 48 -> 33
@@ -1455,7 +1463,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       // registers: N = 16 (C1 / C3) and N = 4 (C2) with the x width fixed at compile time (a
       // point's start loads x without width branches: C2 starts a point every ~13 AES slots).
       if (multi && lpf.levels) {
-        if (xreg && n_bytes == 16 && kMkNbc16) DCF_STREAM(true, true, true, 16);
+        if (xreg && n_bytes == 16 && kMkNbc16 && kMkPk2 && (ppk & (ppk - 1)) == 0) DCF_STREAM6(true, true, true, 16, true);
+        else if (xreg && n_bytes == 16 && kMkNbc16) DCF_STREAM(true, true, true, 16);
         else if (xreg) DCF_STREAM(true, true, true, 0);
         else DCF_STREAM(false, true, true, 0);
       } else if (multi) {
@@ -1475,6 +1484,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
         DCF_STREAM(false, false, false, 0);
       }
 #undef DCF_STREAM
+#undef DCF_STREAM6
       HIP_TRY(hipGetLastError());
     }
   } else {  // lockstep T-table, 64-point units from the work counter

@@ -79,13 +79,14 @@ __device__ __forceinline__ void stream_load_x(StreamLane<NS, XREG, MULTI>& L, in
 }
 
 // XLOADED: the caller has already loaded the point's x words into L.xw[i] (stream_load_x).
-template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0, bool XLOADED = false>
+// PK2 (multi-key): points per key is a power of two (C5: 64), so point -> key is a shift.
+template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0, bool XLOADED = false, bool PK2 = false>
 __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int i, uint64_t p,
                                              const uint4* __restrict__ s0s, const uint4 s0v, uint32_t party,
                                              const uint8_t* __restrict__ xs, uint32_t nbytes_rt, uint64_t ppk,
                                              const PrefixTable& pf) {
   const uint32_t nbytes = NBC ? (uint32_t)NBC : nbytes_rt;  // NBC: x width fixed at compile time
-  const uint32_t k = MULTI ? (uint32_t)p / (uint32_t)ppk : 0u;
+  const uint32_t k = !MULTI ? 0u : PK2 ? (uint32_t)p >> __builtin_ctz((uint32_t)ppk) : (uint32_t)p / (uint32_t)ppk;
   const uint8_t* row = xs + p * nbytes;
   uint32_t w0;  // first 32 x bits, Msb0 (lib.rs:181)
   if (XREG) {
@@ -130,7 +131,7 @@ __device__ __forceinline__ void stream_start(StreamLane<NS, XREG, MULTI>& L, int
 
 // Give every lane whose stream i is free (`mine`) a new point, or retire the
 // stream when the counter is exhausted.  Called in wave-uniform control flow.
-template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit, bool PFX = false, int NBC = 0>
+template <int NS, bool XREG, bool MULTI, uint32_t UNIT = kStreamUnit, bool PFX = false, int NBC = 0, bool PK2 = false>
 __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, int i, bool mine, uint32_t& unext,
                                               uint32_t& uend, bool& exhausted, uint32_t* __restrict__ ctr,
                                               uint32_t nunits, uint32_t total, const uint4* __restrict__ s0s,
@@ -165,7 +166,7 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
       mine = mine && !take;
     }
     if (got) {
-      stream_start<NS, XREG, MULTI, PFX, NBC>(L, i, pnew, s0s, s0v, party, xs, nbytes, ppk, pf);
+      stream_start<NS, XREG, MULTI, PFX, NBC, false, PK2>(L, i, pnew, s0s, s0v, party, xs, nbytes, ppk, pf);
     } else if (mine) {  // nothing left: the stream retires
       L.alive[i] = false;
       L.ci[i] = 0;  // keep the idle stream's CW loads in bounds
@@ -193,7 +194,8 @@ __device__ __forceinline__ void stream_refill(StreamLane<NS, XREG, MULTI>& L, in
     }
     const uint32_t rank = lane_rank(need);
     const bool take = mine && rank < uend - unext;
-    if (take) stream_start<NS, XREG, MULTI, PFX, NBC>(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk, pf);
+    if (take)
+      stream_start<NS, XREG, MULTI, PFX, NBC, false, PK2>(L, i, unext + rank, s0s, s0v, party, xs, nbytes, ppk, pf);
     const uint64_t taken = __ballot(take);
     unext += (uint32_t)__popcll(taken);
     need &= ~taken;
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(kKmThreads) void k_cw_keymajor(const uint4* __restr
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
 // GK: round keys per round from the device copy rkg (aes256_tt_gk); otherwise from the kernel
 // argument (SGPRs).  PFX: every stream starts below the per-key top trees (multi-key).
-template <int NS, bool XREG, bool MULTI, uint32_t UNIT, bool GK, bool PFX = false, int NBC = 0>
+template <int NS, bool XREG, bool MULTI, uint32_t UNIT, bool GK, bool PFX = false, int NBC = 0, bool PK2 = false>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -304,8 +306,8 @@ __device__ __forceinline__ void stream_run(
   const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
 #pragma unroll
   for (int i = 0; i < NS; ++i)
-    stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, true, unext, uend, exhausted, ctr, nunits, total32, s0s,
-                                                  s0v, party, xs, nbytes, ppk, pf);
+    stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC, PK2>(L, i, true, unext, uend, exhausted, ctr, nunits, total32,
+                                                       s0s, s0v, party, xs, nbytes, ppk, pf);
 
   uint64_t nblk = 0;  // AES blocks this wave encrypts for live streams (wave-uniform)
   for (;;) {
@@ -453,14 +455,15 @@ __device__ __forceinline__ void stream_run(
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
       if (done) {
-        const uint4 np = MULTI ? cw_np1[L.pt[i] / (uint32_t)ppk] : np1v;
+        const uint32_t key = PK2 ? L.pt[i] >> __builtin_ctz((uint32_t)ppk) : L.pt[i] / (uint32_t)ppk;
+        const uint4 np = MULTI ? cw_np1[key] : np1v;
         const uint32_t tm = 0u - L.t[i];
         ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
                                  L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
       }
       if (__ballot(done))
-        stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC>(L, i, done, unext, uend, exhausted, ctr, nunits, total32, s0s,
-                                                  s0v, party, xs, nbytes, ppk, pf);
+        stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC, PK2>(L, i, done, unext, uend, exhausted, ctr, nunits, total32,
+                                                           s0s, s0v, party, xs, nbytes, ppk, pf);
     }
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
@@ -468,7 +471,7 @@ __device__ __forceinline__ void stream_run(
 }
 
 // One 1024-thread workgroup per CU (the replicated T-tables take 128 KiB of LDS).
-template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0>
+template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0, bool PK2 = false>
 __global__ __launch_bounds__(kBlock, 1) void k_eval16_stream(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -485,7 +488,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_stream(
   // registers it takes the device-copy keys (0 spills); with x loaded per word the key look-ahead
   // registers would spill 2 VGPRs to scratch instead, so it keeps SGPR keys (40 SGPR spills, to VGPR lanes).
   constexpr bool GK = !MULTI || (!PFX && XREG);
-  stream_run<NS, XREG, MULTI, kStreamUnit, GK, PFX, NBC>(lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs,
+  stream_run<NS, XREG, MULTI, kStreamUnit, GK, PFX, NBC, PK2>(lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs,
                                                        nbytes, num_keys, ppk, total, ctr, ys, pf);
   DCF_CLK(2, 1);
 }
