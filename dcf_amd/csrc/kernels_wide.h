@@ -564,7 +564,12 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   // BT regions (4 reads each) are issued before their XORs: the compiler otherwise waits after
   // every two reads, ~3 reads in flight per wave.  All R regions into the accumulators.
   auto regions = [&](const uint32_t (&twa)[NW], const uint32_t (&twb)[NW], uint32_t (&aa)[4], uint32_t (&ab)[4]) {
-    constexpr int BT = 2;
+#ifndef DCF_T2_BT
+#define DCF_T2_BT 2
+#endif
+    // regions per read batch (r05ad, C4 same box: 2 / 3 / 4 regions 32.22-32.63 / 32.17-32.45 /
+    // 32.12-32.42 ms, within noise)
+    constexpr int BT = DCF_T2_BT;
 #pragma unroll
     for (int m0 = 0; m0 < L::R; m0 += BT) {
       u32x4_t rb[BT][4];
