@@ -366,10 +366,22 @@ __device__ __forceinline__ void stream_run(
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[i][j] = GK ? xor3(L.s[i][j], inv, k0w[j]) : (L.s[i][j] ^ inv);
     }
+#ifndef DCF_STREAM_PRIO
+#define DCF_STREAM_PRIO 1
+#endif
+    // Wave priority: the AES rounds run at s_setprio 1, the level update / refill at 0, so the
+    // arbiter issues the LDS lookups of waves in their rounds ahead of other waves' update VALU
+    // and the LDS stays fed.  r05ae (same box, 3 alternating runs): C3 479.1-480.4 vs 497.9-499.8
+    // ms (-3.9 %), C2 3.325-3.391 vs 3.401-3.416, C5 319.2-319.8 vs 322.1-323.4; the update at
+    // priority 1 instead (knob 2) lost 2-5 %.
+    if (DCF_STREAM_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    if (DCF_STREAM_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     if (GK)
       aes256_tt_gk<NS, true>(st, rkl, lds, lc);
     else
       aes256_tt<NS>(st, rk, lds, lc);
+    if (DCF_STREAM_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if (DCF_STREAM_PRIO == 2) __builtin_amdgcn_s_setprio(1);
     // Pin the CW loads above the update: without this the compiler sinks the
     // cw_t load into the (divergent) level-done path and waits on it there.
 #pragma unroll
