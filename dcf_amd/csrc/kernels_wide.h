@@ -617,7 +617,12 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   load_t(tb, p0 + 16u * bn + 8u + pin);
   while (bc < nblk) {
     uint32_t aa[4] = {cst.x, cst.y, cst.z, cst.w}, ab[4] = {cst.x, cst.y, cst.z, cst.w};
+#ifndef DCF_TAIL_PRIO
+#define DCF_TAIL_PRIO 1
+#endif
+    if (DCF_TAIL_PRIO) __builtin_amdgcn_s_setprio(1);  // A/B knob: the table reads at priority 1
     regions(twa, twb, aa, ab);
+    if (DCF_TAIL_PRIO) __builtin_amdgcn_s_setprio(0);
     const uint64_t pw = p0 + 16u * bc, pa = pw + pin, pb = pa + 8u;
     tail_store<LP>(ys, pw, pin, lam, off, kill | (pa < p1 ? 0u : dead), make_uint4(aa[0], aa[1], aa[2], aa[3]));
     tail_store<LP>(ys, pw + 8u, pin, lam, off, kill | (pb < p1 ? 0u : dead), make_uint4(ab[0], ab[1], ab[2], ab[3]));

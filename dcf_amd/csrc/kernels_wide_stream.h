@@ -272,7 +272,12 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
         st[i][j] = xor3(sel[i][j], inv[i], k0w[j]);  // round key 0 folded in
       }
     }
+#ifndef DCF_HEAD_PRIO
+#define DCF_HEAD_PRIO 1
+#endif
+    if (DCF_HEAD_PRIO) __builtin_amdgcn_s_setprio(1);  // A/B knob: the AES rounds at priority 1
     aes_tt_lka<14, NS, true, KR>(st, ka, lds, lc, rkr, hmk);
+    if (DCF_HEAD_PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int i = 0; i < NS; ++i)
       asm volatile("" : "+v"(cs[i][0].x), "+v"(cs[i][0].y), "+v"(cs[i][0].z), "+v"(cs[i][0].w), "+v"(cs[i][1].x),
