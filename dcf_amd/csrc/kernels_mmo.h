@@ -11,6 +11,11 @@
 // going right: each lane reads the round keys of its side from LDS.
 #pragma once
 
+// A/B knob: the MMO AES rounds at wave priority 1.
+#ifndef DCF_MMO_PRIO
+#define DCF_MMO_PRIO 1
+#endif
+
 #include "aes_lds.h"
 #include "kernels16.h"
 
@@ -55,7 +60,9 @@ __device__ __forceinline__ uint4 mmo_eval_one(const uint32_t* lds, uint32_t lc, 
       uint32_t st[2][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[0][j] = st[1][j] = s[j];
+      if (DCF_MMO_PRIO) __builtin_amdgcn_s_setprio(1);
       aes128_tt<2>(st, rk, lds, lc);  // side's s and v blocks
+      if (DCF_MMO_PRIO) __builtin_amdgcn_s_setprio(0);
       const uint64_t ci = (uint64_t)lev * num_keys + key;
       const uint4 cs = cw_s[ci], cv = cw_v[ci];
       const uint32_t ct = cw_t[ci];
@@ -119,7 +126,9 @@ __device__ __forceinline__ void mmo_prg4(const uint32_t* lds, uint32_t lc, const
     uint32_t st[2][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) st[0][j] = st[1][j] = s[j];
+    if (DCF_MMO_PRIO) __builtin_amdgcn_s_setprio(1);
     aes128_tt<2>(st, rk, lds, lc);
+    if (DCF_MMO_PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       o[2 * h][j] = st[0][j];
