@@ -13,6 +13,10 @@
 #ifndef DCF_GEN_PRIO
 #define DCF_GEN_PRIO 0
 #endif
+// A/B knob: the pair walk's AES rounds (k_eval16_pair, k_eval16) at wave priority 1.
+#ifndef DCF_PAIR_PRIO
+#define DCF_PAIR_PRIO 1
+#endif
 
 namespace {
 
@@ -48,7 +52,9 @@ __device__ __forceinline__ uint4 tt_eval_one(const uint32_t* lds, uint32_t lc, c
         st[0][j] = s[j];
         st[1][j] = ~s[j];
       }
+      if (DCF_PAIR_PRIO) __builtin_amdgcn_s_setprio(1);
       aes256_tt<2>(st, rk, lds, lc);  // st[0] = A, st[1] = B
+      if (DCF_PAIR_PRIO) __builtin_amdgcn_s_setprio(0);
       const uint64_t ci = (uint64_t)lev * num_keys + key;
       const uint4 cs = cw_s[ci];
       const uint4 cv = cw_v[ci];
@@ -201,7 +207,9 @@ __device__ __forceinline__ uint4 tt_eval_pair(const uint32_t* lds, uint32_t lc, 
       uint32_t st[1][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[0][j] = s[j] ^ inv;
+      if (DCF_PAIR_PRIO) __builtin_amdgcn_s_setprio(1);
       aes256_tt_gk<1>(st, rkg, lds, lc);  // round keys per round from global memory (SGPR keys spill)
+      if (DCF_PAIR_PRIO) __builtin_amdgcn_s_setprio(0);
       uint32_t A[4], B[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
