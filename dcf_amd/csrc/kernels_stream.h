@@ -275,6 +275,10 @@ __global__ __launch_bounds__(kKmThreads) void k_cw_keymajor(const uint4* __restr
   }
 }
 
+// Wave priority knob (see the AES call in stream_run).
+#ifndef DCF_STREAM_PRIO
+#define DCF_STREAM_PRIO 1
+#endif
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
 // GK: round keys per round from the device copy rkg (aes256_tt_gk); otherwise from the kernel
 // argument (SGPRs).  PFX: every stream starts below the per-key top trees (multi-key).
@@ -366,14 +370,12 @@ __device__ __forceinline__ void stream_run(
 #pragma unroll
       for (int j = 0; j < 4; ++j) st[i][j] = GK ? xor3(L.s[i][j], inv, k0w[j]) : (L.s[i][j] ^ inv);
     }
-#ifndef DCF_STREAM_PRIO
-#define DCF_STREAM_PRIO 1
-#endif
     // Wave priority: the AES rounds run at s_setprio 1, the level update / refill at 0, so the
     // arbiter issues the LDS lookups of waves in their rounds ahead of other waves' update VALU
     // and the LDS stays fed.  r05ae (same box, 3 alternating runs): C3 479.1-480.4 vs 497.9-499.8
     // ms (-3.9 %), C2 3.325-3.391 vs 3.401-3.416, C5 319.2-319.8 vs 322.1-323.4; the update at
-    // priority 1 instead (knob 2) lost 2-5 %.
+    // priority 1 instead (knob 2) lost 2-5 %; widening the priority-1 span to the CW loads (noise)
+    // or to the stores and refill as well (C3 +2 %) did not help (r05aj).
     if (DCF_STREAM_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     if (DCF_STREAM_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     if (GK)
