@@ -56,13 +56,20 @@ PEAK_MMO_BLOCKS = CUS * CLK_HZ / (160 / 32 + 11 / 16)
 # Measured ceiling of the T-table AES-256 rounds alone on MI355X (scripts/micro/aes_rate.hip, r02):
 # 74-75 G blocks/s for 1-4 blocks per lane, = 0.85 of PEAK_TT_BLOCKS (ds_read_b32 alone: 0.863).
 MEASURED_TT_BLOCKS = 74.6e9
+# ds_read_b32 issue alone (same micro-benchmark): 0.863 of the nominal rate — the LDS wall itself.
+DS_READ_FRAC = 0.863
 
 
 def measured_ceiling(achieved_blocks_per_s: float) -> dict:
     """The T-table AES rounds' practical ceiling beside the nominal LDS peak."""
     return {"value": MEASURED_TT_BLOCKS / 1e9, "unit": "G AES-256 blocks/s",
             "frac": achieved_blocks_per_s / MEASURED_TT_BLOCKS,
-            "source": "scripts/micro/aes_rate.hip: T-table AES-256 rounds alone, 16 waves/CU (0.85 of peak)"}
+            "source": "scripts/micro/aes_rate.hip: T-table AES-256 rounds alone, 16 waves/CU (0.85 of peak)",
+            "ds_read_ceiling": DS_READ_FRAC * PEAK_TT_BLOCKS / 1e9,
+            "ds_read_frac": achieved_blocks_per_s / (DS_READ_FRAC * PEAK_TT_BLOCKS),
+            "note": "the rounds-only micro-benchmark keeps every wave in the same phase; the engines "
+                    "raise wave priority for their rounds (s_setprio, r05ae) and can exceed it — the "
+                    "ds_read_b32 issue rate alone (ds_read_ceiling) is the wall"}
 
 
 def engine_peak(engine: str) -> float:
