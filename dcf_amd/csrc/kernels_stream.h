@@ -275,6 +275,10 @@ __global__ __launch_bounds__(kKmThreads) void k_cw_keymajor(const uint4* __restr
   }
 }
 
+// B reuse over whole runs of right steps at t = 0 (A/B knob, see the reuse block in stream_run).
+#ifndef DCF_REUSE_RUN
+#define DCF_REUSE_RUN 0
+#endif
 // Wave priority knob (see the AES call in stream_run).
 #ifndef DCF_STREAM_PRIO
 #define DCF_STREAM_PRIO 1
@@ -459,6 +463,28 @@ __device__ __forceinline__ void stream_run(
         L.cur[i] <<= (rr & 1u);
         L.ci[i] += rr & 1u;
         if (!(NBC && NBC <= 4) && rr && (nl & 31u) == 0u) stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+        if (DCF_REUSE_RUN) {
+          // A reused right step that left t = 0 (t1 = 0) kept s, so the next level has the same
+          // B again: a run of k further right steps keeps s and t = 0 and XORs ~s & M into v k
+          // times (lib.rs:178-186 with t = 0: no CW enters); the left step that ends the run has
+          // its B half too (v ^= (B ^ ~s) & M), leaving A for the next slot.  The run stops at the
+          // x word's end (the next word's first step recomputes B).
+          const bool go = rr && t1 == 0u && (nl & 31u) != 0u && nl < nlev;
+          const uint32_t k = go ? min((uint32_t)__clz(~L.cur[i]), nlev - nl) : 0u;
+          const uint32_t ko = 0u - (k & 1u);
+          nl += k;
+          L.cur[i] <<= k;
+          L.ci[i] += k;
+          const uint32_t lm = 0u - (uint32_t)(go && nl < nlev && (nl & 31u) != 0u);  // the left step after the run
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t msk = (j == 3) ? kMaskLast : 0xFFFFFFFFu;
+            L.v[i][j] ^= ((ko & ~L.s[i][j]) ^ (lm & d[j])) & msk;
+          }
+          L.ph[i] = lm ? 1u : L.ph[i];
+          if (!(NBC && NBC <= 4) && go && k && (nl & 31u) == 0u && nl < nlev)
+            stream_next_word<NS, XREG, MULTI>(L, i, nl, nlev, nbytes);
+        }
       }
       L.lev[i] = nl;
     }

@@ -2,8 +2,9 @@
 in registers, no shared prefix) against the second oracle restatement (oracle/pyref.py,
 lib.rs:163-204): the per-step B / A slot schedule and B reuse after a right step at t = 0.
 Word-level transcription of the kernel's update (same masks and order), so a schedule bug shows
-up here as wrong bytes or a level past 8N — the GPU tests pin the kernel itself.  (The measured-
-and-dropped reuse chain, runs of free right steps, is in git history and profiles/AB_LOG.md.)"""
+up here as wrong bytes or a level past 8N — the GPU tests pin the kernel itself.  run=True
+transcribes the DCF_REUSE_RUN form: after a reused right step that left t = 0, a whole run of right
+steps (and the left step ending it) takes no AES slot."""
 import random
 
 import pytest
@@ -26,7 +27,7 @@ def _bswap(x):
     return int.from_bytes(x.to_bytes(4, "little"), "big")
 
 
-def stream_eval(aes, party, s0, cws, np1, x, counts):
+def stream_eval(aes, party, s0, cws, np1, x, counts, run=False):
     nb = len(x)
     nlev = 8 * nb
     raw = x + bytes((-nb) % 4) + bytes(16)
@@ -90,14 +91,28 @@ def stream_eval(aes, party, s0, cws, np1, x, counts):
         cur = (cur << (rr & 1)) & F
         if rr and (nl & 31) == 0:
             next_word()
+        if run:  # DCF_REUSE_RUN
+            go = bool(rr) and t1 == 0 and (nl & 31) != 0 and nl < nlev
+            k = min(32 - ((~cur) & F).bit_length(), nlev - nl) if go else 0
+            ko = F if k & 1 else 0
+            nl += k
+            cur = (cur << k) & F
+            lm = F if (go and nl < nlev and (nl & 31) != 0) else 0
+            for j in range(4):
+                v[j] ^= ((ko & ~s[j] & F) ^ (lm & d[j])) & msk[j]
+            if lm:
+                ph = 1
+            if go and k and (nl & 31) == 0 and nl < nlev:
+                next_word()
         assert nl <= nlev, (nl, nlev)
         lev = nl
     np_ = _w(np1)
     return _b([v[j] ^ s[j] ^ (np_[j] if t else 0) for j in range(4)])
 
 
-@pytest.mark.parametrize("nb", [1, 2, 4, 8, 16])
-def test_stream_schedule_matches_oracle(nb):
+@pytest.mark.parametrize("run", [False, True], ids=["reuse1", "reuse_run"])
+@pytest.mark.parametrize("nb", [1, 2, 3, 4, 5, 8, 16])
+def test_stream_schedule_matches_oracle(nb, run):
     rnd = random.Random(0x57E4 + nb)
     lam = 16
     keys = [rnd.randbytes(32) for _ in range(2)]
@@ -111,9 +126,10 @@ def test_stream_schedule_matches_oracle(nb):
     # all-ones / all-zeros, alpha
     xs = [rnd.randbytes(nb) for _ in range(m)] + [rnd.randbytes(nb - 1) + b"\xff" for _ in range(m)]
     xs += [b"\xff" * nb, bytes(nb), alpha, bytes(max(0, nb - 1)) + b"\x7f", b"\x0f" * nb]
+    xs += [bytes([0x80 | rnd.getrandbits(7)]) + b"\xff" * (nb - 1) for _ in range(8)]  # long right runs
     counts = [0]
     for party in (0, 1):
         ref = pyref.eval_(prg, bool(party), s0s[party], cws, np1, xs)
-        got = [stream_eval(aes, party, s0s[party], cws, np1, x, counts) for x in xs]
+        got = [stream_eval(aes, party, s0s[party], cws, np1, x, counts, run) for x in xs]
         assert got == ref
     assert counts[0] < 2 * len(xs) * 2 * 8 * nb
