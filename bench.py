@@ -97,8 +97,8 @@ def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels:
 
 
 def traffic_fields(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels: int, alg_bytes: float):
-    """(traffic, source): the PMC figure when profiles/ holds this launch shape, otherwise
-    the algorithmic bytes, labelled as such (never null)."""
+    """(traffic, source): the PMC figure when profiles/ holds this launch shape, otherwise None
+    (traffic is measured HBM bytes or nothing; the algorithmic bytes are in the line beside it)."""
     e = pmc_traffic(kernel, points, n_bytes, lam, prefix_levels)
     if e is not None and e.get("traffic_bytes") is not None:
         src = f"pmc: 2 x FETCH_SIZE + WRITE_SIZE per launch ({e.get('source', '?')}, via profiles/pmc_traffic.json)"
@@ -106,7 +106,8 @@ def traffic_fields(kernel: str, points: int, n_bytes: int, lam: int, prefix_leve
             src += (f"; 1 x FETCH_SIZE + WRITE_SIZE = {e['traffic_bytes_x1'] / 1e9:.2f} GB (the x2 correction is for "
                     f"wide streaming reads; 32-B row gathers are fetched as 64-B requests, so x1 may be the closer figure)")
         return e["traffic_bytes"], src
-    return alg_bytes, "algorithmic bytes (no PMC profile of this exact launch shape in profiles/pmc_traffic.json)"
+    return None, (f"null: no PMC profile of this exact launch shape in profiles/pmc_traffic.json "
+                  f"(algorithmic bytes {alg_bytes / 1e9:.2f} GB)")
 
 
 def blocks_per_eval(n_bytes: int, lam: int) -> int:
