@@ -5,14 +5,6 @@
 #include "aes_lds.h"
 #include "kernels_lat.h"
 
-// A/B knob: the full-domain / prefix-build AES rounds at wave priority 1 (fd_children, k_fd_level16).
-#ifndef DCF_FD_PRIO
-#define DCF_FD_PRIO 0
-#endif
-// A/B knob: k_gen16's AES rounds at wave priority 1.
-#ifndef DCF_GEN_PRIO
-#define DCF_GEN_PRIO 0
-#endif
 // A/B knob: the pair walk's AES rounds (k_eval16_pair, k_eval16) at wave priority 1.
 #ifndef DCF_PAIR_PRIO
 #define DCF_PAIR_PRIO 1
@@ -320,17 +312,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_gen16(
             st[2][j] = s[1][j];
             st[3][j] = ~s[1][j];
           }
-          if (DCF_GEN_PRIO) __builtin_amdgcn_s_setprio(1);
           aes256_tt<4>(st, rk, lds, lc);  // A0, B0, A1, B1
-          if (DCF_GEN_PRIO) __builtin_amdgcn_s_setprio(0);
         } else {
           uint32_t one[1][4];
           const uint32_t inv = 0u - (q & 1u);  // B blocks encrypt ~s
 #pragma unroll
           for (int j = 0; j < 4; ++j) one[0][j] = ((q >> 1) ? s[1][j] : s[0][j]) ^ inv;
-          if (DCF_GEN_PRIO) __builtin_amdgcn_s_setprio(1);
           aes256_tt<1>(one, rk, lds, lc);
-          if (DCF_GEN_PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {  // quad_perm broadcasts of lane b's block (b, b, b, b)
             st[0][j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)one[0][j], 0x00, 0xF, 0xF, true);
@@ -472,9 +460,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_fd_level16(
       st[0][k] = s[k];
       st[1][k] = ~s[k];
     }
-    if (DCF_FD_PRIO) __builtin_amdgcn_s_setprio(1);
     aes256_tt<2>(st, rk, lds, lc);  // A, B
-    if (DCF_FD_PRIO) __builtin_amdgcn_s_setprio(0);
     const uint32_t tm = 0u - t;
     uint32_t sl[4], vl[4], sr[4], vr[4];
 #pragma unroll
@@ -531,12 +517,10 @@ __device__ __forceinline__ void fd_children(const uint32_t* lds, uint32_t lc, co
     st[0][k] = s[k];
     st[1][k] = ~s[k];
   }
-  if (DCF_FD_PRIO) __builtin_amdgcn_s_setprio(1);  // A/B knob: the AES rounds at priority 1
   if (GKB)
     aes256_tt_gk<2>(st, rkg, lds, lc);  // A, B
   else
     aes256_tt<2>(st, rk, lds, lc);  // A, B
-  if (DCF_FD_PRIO) __builtin_amdgcn_s_setprio(0);
   const uint32_t tm = 0u - t;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {

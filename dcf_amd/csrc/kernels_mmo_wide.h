@@ -19,11 +19,6 @@
 // (the side's s and v), 2 * 8N * LAMBDA / 16 in all.
 #pragma once
 
-// A/B knob: the wide MMO AES rounds at wave priority 1.
-#ifndef DCF_MMOW_PRIO
-#define DCF_MMOW_PRIO 0
-#endif
-
 #include "aes_lds.h"
 #include "kernels_mmo.h"
 
@@ -77,9 +72,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mmo_wide_eval(
 #pragma unroll
       for (int k = 0; k < 4; ++k) st[0][k] = st[1][k] = s[k];
       const uint4* const rkp[2] = {rks, rkv};
-      if (DCF_MMOW_PRIO) __builtin_amdgcn_s_setprio(1);
       aes_tt_lk<10, 2, true>(st, rkp, lds, lc);
-      if (DCF_MMOW_PRIO) __builtin_amdgcn_s_setprio(0);
       const uint64_t ci = ((uint64_t)lev * num_keys + key) * lam + 16ull * j;
       const uint4 cs = *reinterpret_cast<const uint4*>(cw_s + ci), cv = *reinterpret_cast<const uint4*>(cw_v + ci);
       const uint32_t csw[4] = {cs.x, cs.y, cs.z, cs.w}, cvw[4] = {cv.x, cv.y, cv.z, cv.w};
@@ -166,9 +159,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_mmo_wide_gen(
           for (int q = 0; q < 4; ++q) st[0][q] = st[1][q] = s[p][q];
           const uint4* const rkp[2] = {rk + (uint64_t)((2u * h) * nb + j) * kMmoRk,
                                        rk + (uint64_t)((2u * h + 1u) * nb + j) * kMmoRk};
-          if (DCF_MMOW_PRIO) __builtin_amdgcn_s_setprio(1);
           aes_tt_lk<10, 2, true>(st, rkp, lds, lc);
-          if (DCF_MMOW_PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint32_t msk = (q == 3) ? mlast : 0xFFFFFFFFu;
@@ -262,9 +253,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_prg_mmo_wide(const uint32_t* __re
       for (int q = 0; q < 4; ++q) st[0][q] = st[1][q] = s[q];
       const uint4* const rkp[2] = {rk + (uint64_t)((2u * h) * nb + j) * kMmoRk,
                                    rk + (uint64_t)((2u * h + 1u) * nb + j) * kMmoRk};
-      if (DCF_MMOW_PRIO) __builtin_amdgcn_s_setprio(1);
       aes_tt_lk<10, 2, true>(st, rkp, lds, lc);
-      if (DCF_MMOW_PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         o[2 * h][q] = st[0][q] ^ s[q];

@@ -26,6 +26,11 @@
 
 #include "aes_lds.h"
 
+// Wave priority for the tail2 table reads (r05af: C4 -2.0 % with DCF_HEAD_PRIO).
+#ifndef DCF_TAIL_PRIO
+#define DCF_TAIL_PRIO 1
+#endif
+
 namespace {
 
 // Per-point t-vector (head -> tail), tw words (64 B for N <= 31): byte c holds rows 4c..4c+3
@@ -617,9 +622,6 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
   load_t(tb, p0 + 16u * bn + 8u + pin);
   while (bc < nblk) {
     uint32_t aa[4] = {cst.x, cst.y, cst.z, cst.w}, ab[4] = {cst.x, cst.y, cst.z, cst.w};
-#ifndef DCF_TAIL_PRIO
-#define DCF_TAIL_PRIO 1
-#endif
     if (DCF_TAIL_PRIO) __builtin_amdgcn_s_setprio(1);  // A/B knob: the table reads at priority 1
     regions(twa, twb, aa, ab);
     if (DCF_TAIL_PRIO) __builtin_amdgcn_s_setprio(0);

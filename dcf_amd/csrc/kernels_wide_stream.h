@@ -18,6 +18,11 @@
 #include "kernels_lat.h"     // dpp<>
 #include "kernels_stream.h"  // dequeue_unit
 
+// Wave priority for the head's AES rounds (r05af: C4 -2.0 % with DCF_TAIL_PRIO).
+#ifndef DCF_HEAD_PRIO
+#define DCF_HEAD_PRIO 1
+#endif
+
 namespace {
 
 __device__ __forceinline__ uint32_t xand(uint32_t a, uint32_t m, uint32_t c) {  // a ^ (m & c)
@@ -272,9 +277,6 @@ __global__ __launch_bounds__(WG, 1) void k_eval_wide_head_stream(
         st[i][j] = xor3(sel[i][j], inv[i], k0w[j]);  // round key 0 folded in
       }
     }
-#ifndef DCF_HEAD_PRIO
-#define DCF_HEAD_PRIO 1
-#endif
     if (DCF_HEAD_PRIO) __builtin_amdgcn_s_setprio(1);  // A/B knob: the AES rounds at priority 1
     aes_tt_lka<14, NS, true, KR>(st, ka, lds, lc, rkr, hmk);
     if (DCF_HEAD_PRIO) __builtin_amdgcn_s_setprio(0);
