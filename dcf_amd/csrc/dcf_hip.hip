@@ -1205,6 +1205,12 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
 // 74 SGPRs.  r05v A/B (same box, 3 alternating runs): C3 491.3-491.7 vs 493.1-493.9 ms, C2
 // 3.354-3.360 vs 3.391-3.396 ms (round 2's attempt at this split lost to a register-allocation flip).
 constexpr bool kSkPfx = DCF_SK_PFX;
+#ifndef DCF_STG
+#define DCF_STG 0
+#endif
+// N <= 4 single key below the table (C2): prefix rows staged two iterations ahead into LDS by DMA
+// (kernels_stream.h STG) instead of gathered at each point start.
+constexpr bool kStg = DCF_STG;
 #ifndef DCF_MK_NBC16
 #define DCF_MK_NBC16 1
 #endif
@@ -1451,9 +1457,10 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       uint8_t* lys = ys + c0 * lam;
       const uint8_t* ls0 = s0s + k0 * lam;
       const PrefixTable lpf = (multi && pf.levels) ? PrefixTable{pf.sv + 2 * (k0 << pf.levels), pf.levels} : pf;
-#define DCF_STREAM(XR, MK, PF, NBC) DCF_STREAM6(XR, MK, PF, NBC, false)
-#define DCF_STREAM6(XR, MK, PF, NBC, PK2)                                                                       \
-  hipLaunchKernelGGL((k_eval16_stream<NS, XR, MK, PF, NBC, PK2>), dim3((unsigned)blocks), block, 0, st, p->d_tab,  \
+#define DCF_STREAM(XR, MK, PF, NBC) DCF_STREAM7(XR, MK, PF, NBC, false, false)
+#define DCF_STREAM6(XR, MK, PF, NBC, PK2) DCF_STREAM7(XR, MK, PF, NBC, PK2, false)
+#define DCF_STREAM7(XR, MK, PF, NBC, PK2, STG)                                                                  \
+  hipLaunchKernelGGL((k_eval16_stream<NS, XR, MK, PF, NBC, PK2, STG>), dim3((unsigned)blocks), block, 0, st, p->d_tab, \
                      p->rk[0],                                                                                 \
                      lcs, cwv, lct, lnp1, (const uint4*)ls0, (uint32_t)party, lxs, (uint32_t)n_bytes, (uint64_t)kc, \
                      (uint64_t)ppk, (uint64_t)cnt, w->d_ctr, (uint4*)lys, lpf, p->d_rk0)
@@ -1474,6 +1481,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
         DCF_STREAM(true, false, true, 16);  // every start below the shared prefix: no fresh-x-word path
       } else if (xreg && n_bytes == 16) {
         DCF_STREAM(true, false, false, 16);
+      } else if (xreg && n_bytes == 4 && lpf.levels && kSkPfx && kStg) {
+        DCF_STREAM7(true, false, true, 4, false, true);  // rows staged two iterations ahead (C2)
       } else if (xreg && n_bytes == 4 && lpf.levels && kSkPfx) {
         DCF_STREAM(true, false, true, 4);
       } else if (xreg && n_bytes == 4) {
@@ -1485,6 +1494,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       }
 #undef DCF_STREAM
 #undef DCF_STREAM6
+#undef DCF_STREAM7
       HIP_TRY(hipGetLastError());
     }
   } else {  // lockstep T-table, 64-point units from the work counter

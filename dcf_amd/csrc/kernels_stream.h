@@ -279,6 +279,24 @@ __global__ __launch_bounds__(kKmThreads) void k_cw_keymajor(const uint4* __restr
 #ifndef DCF_REUSE_RUN
 #define DCF_REUSE_RUN 0
 #endif
+// STG (staged rows; single key, prefix table, x in one word — C2): a wave claims its points in
+// halves of kStgUnit and stages each half ahead of use: the x words by an ordinary load (end of
+// iteration k), the 32-B prefix rows by LDS DMA into the wave's 2 KiB area (end of k + 1, x in by
+// then: lanes 0-31 the s halves, 32-63 the v halves), read by the refills of k + 2 instead of a
+// gather from HBM with the wave waiting.  The DMA is inline asm, so hipcc adds no vmcnt(0) for
+// it, and it is the iteration's last memory operation: it retires in order before the next
+// iteration's CW loads, whose wait precedes every read of the staged rows, and no wait inside its
+// own iteration drains it.  The AES rounds take their keys from SGPRs here: a device-copy key load
+// waits, in order, for every load issued before it, staged ones included (AB_LOG r05m).
+constexpr uint32_t kStgUnit = 32;
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_dst)
+               : "memory");
+}
+
 // Wave priority knob (see the AES call in stream_run).
 #ifndef DCF_STREAM_PRIO
 #define DCF_STREAM_PRIO 1
@@ -286,13 +304,16 @@ __global__ __launch_bounds__(kKmThreads) void k_cw_keymajor(const uint4* __restr
 // The stream loop of one wave over the work counter's UNIT-point units (tables already in LDS).
 // GK: round keys per round from the device copy rkg (aes256_tt_gk); otherwise from the kernel
 // argument (SGPRs).  PFX: every stream starts below the per-key top trees (multi-key).
-template <int NS, bool XREG, bool MULTI, uint32_t UNIT, bool GK, bool PFX = false, int NBC = 0, bool PK2 = false>
+template <int NS, bool XREG, bool MULTI, uint32_t UNIT, bool GK, bool PFX = false, int NBC = 0, bool PK2 = false,
+          bool STG = false>
 __device__ __forceinline__ void stream_run(
     const uint32_t* lds, const uint4* rkl, const RoundKeys& rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
     const uint4* __restrict__ s0s, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes_rt,
     const uint64_t num_keys, const uint64_t ppk, const uint64_t total, uint32_t* __restrict__ ctr,
-    uint4* __restrict__ ys, const PrefixTable& pf) {
+    uint4* __restrict__ ys, const PrefixTable& pf, const uint32_t stg_lds = 0u) {
+  static_assert(!STG || (!MULTI && XREG && PFX && NBC > 0 && NBC <= 4),
+                "staged rows: single key, prefix table, x in one word");
   const uint32_t nbytes = NBC ? (uint32_t)NBC : nbytes_rt;
   const uint32_t lc = lane_const();
   const uint32_t nlev = 8u * nbytes;
@@ -312,6 +333,101 @@ __device__ __forceinline__ void stream_run(
     L.ph[i] = 0u;
   }
   const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
+  // STG: per half h (wave-uniform) its first point, size, stage (0 free, 1 x loading, 2 rows
+  // loading, 3 ready) and points handed out; xh[h]: lane r's raw x word of point base + (r & 31)
+  uint32_t hb[2] = {0u, 0u}, hn[2] = {0u, 0u}, hs[2] = {0u, 0u}, hu[2] = {0u, 0u}, xh[2] = {0u, 0u}, xr[2] = {0u, 0u};
+  const uint32_t lane = threadIdx.x & 63u;
+  auto claim = [&](int h) {  // the wave's next (up to) kStgUnit points into free half h, x loading
+    if (unext >= uend && !exhausted) {  // the same UNIT-point claims as the direct path
+      const uint32_t u = dequeue_unit(ctr);
+      if (u >= nunits) {
+        exhausted = true;
+      } else {
+        unext = u * UNIT;
+        uend = min(unext + UNIT, total32);
+      }
+    }
+    if (unext >= uend) return;
+    hb[h] = unext;
+    hn[h] = min(kStgUnit, uend - unext);
+    unext += hn[h];
+    hu[h] = 0u;
+    const uint32_t pp = hb[h] + min(lane & 31u, hn[h] - 1u);
+    xh[h] = *reinterpret_cast<const uint32_t*>(xs + (size_t)pp * nbytes);
+    hs[h] = 1u;
+  };
+  // At the end of an iteration (after its refills, so that no later wait in the iteration drains
+  // the DMA): rows of the halves claimed an iteration ago (their x in by now) into LDS, ready for
+  // the next iteration's refills; then new claims for free halves.  States: 0 free, 1 claimed now
+  // (x loading), 2 x in (DMA due), 3 ready.
+  auto stage = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)  // claims first: the counter atomic's wait would drain a DMA
+      if (hs[h] == 0u) claim(h);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (hs[h] == 2u) {  // xr[h]: copied by prep() this iteration
+        const uint32_t top = bswap32(xr[h]) >> (32u - pf.levels);
+        glds16(pf.sv + 2u * top + (lane >> 5), stg_lds + 1024u * h);
+        hs[h] = 3u;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (hs[h] == 1u) hs[h] = 2u;
+  };
+  // After the iteration's CW wait (which retired every load of the previous iteration): the x words
+  // of halves due for their DMA, copied into registers no later load targets, so neither the DMA's
+  // address nor the refills' ds_bpermute makes hipcc wait for the claims' fresh x loads.
+  auto prep = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (hs[h] == 2u) asm volatile("v_mov_b32 %0, %1" : "=v"(xr[h]) : "v"(xh[h]));
+  };
+  // Staged refill of the lanes whose stream i is free (`mine`) from the ready halves.
+  auto refill_stg = [&](int i, bool mine) {
+    uint64_t need = __ballot(mine);
+    asm volatile("" ::: "memory");  // staged-row reads stay below the CW wait that retired their DMA
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (need && hs[h] == 3u) {
+        const uint32_t rank = lane_rank(need);
+        const bool take = mine && rank < hn[h] - hu[h];
+        const uint32_t r = min(hu[h] + rank, hn[h] - 1u);
+        const uint32_t xw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(r << 2), (int)xr[h]);
+        const uint4 sv = lds_load16(stg_lds + 1024u * h + 16u * r);
+        const uint4 vv = lds_load16(stg_lds + 1024u * h + 512u + 16u * r);
+        if (take) {  // stream_start below the shared prefix, with the row and x in hand (prefix_row)
+          const uint32_t lev0 = pf.levels;
+          L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w & kMaskLast;
+          L.v[i][0] = vv.x; L.v[i][1] = vv.y; L.v[i][2] = vv.z; L.v[i][3] = vv.w;
+          L.t[i] = (sv.w >> 24) & 1u;
+          L.ph[i] = 0u;
+          L.lev[i] = lev0;
+          L.ci[i] = lev0;
+          L.pt[i] = hb[h] + r;
+          L.alive[i] = true;
+          L.cur[i] = bswap32(xw) << lev0;
+          L.xw[i][0] = 0u; L.xw[i][1] = 0u; L.xw[i][2] = 0u;
+          L.fresh[i] = false;
+        }
+        const uint64_t taken = __ballot(take);
+        hu[h] += (uint32_t)__popcll(taken);
+        need &= ~taken;
+        mine = mine && !take;
+        if (hu[h] == hn[h]) {  // used up: refill the half at once
+          hs[h] = 0u;
+          claim(h);
+        }
+      }
+    }
+    // the rest gathers directly (the direct path's claimed unit first); with the counter spent
+    // it parks the stream, which retries while staged points remain (`want` below)
+    if (need)
+      stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC, PK2>(L, i, mine, unext, uend, exhausted, ctr, nunits, total32,
+                                                         s0s, s0v, party, xs, nbytes, ppk, pf);
+  };
+  if (STG) stage();
 #pragma unroll
   for (int i = 0; i < NS; ++i)
     stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC, PK2>(L, i, true, unext, uend, exhausted, ctr, nunits, total32,
@@ -325,7 +441,8 @@ __device__ __forceinline__ void stream_run(
       any = any || L.alive[i];
       nblk += (uint64_t)__popcll(__ballot(L.alive[i]));
     }
-    if (!__ballot(any)) break;
+    const bool pend = STG && (hs[0] != 0u || hs[1] != 0u);  // staged points not handed out yet
+    if (!__ballot(any) && !pend) break;
     // Correction words of each stream's current level (vector loads, issued before the AES),
     // and of the next level for a stream whose step may end with B still valid (a right
     // step at t = 0 keeps s: see "B reuse" below).
@@ -491,6 +608,7 @@ __device__ __forceinline__ void stream_run(
     // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.  (vmcnt counts
     // stores too, so the refill's wait for its x word also waits for this store; issuing the
     // store after the refill's loads measured slower, AB_LOG r02.)
+    if (STG) prep();
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
@@ -501,17 +619,22 @@ __device__ __forceinline__ void stream_run(
         ys[L.pt[i]] = make_uint4(L.v[i][0] ^ L.s[i][0] ^ (tm & np.x), L.v[i][1] ^ L.s[i][1] ^ (tm & np.y),
                                  L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
       }
-      if (__ballot(done))
+      if (STG) {
+        const bool want = done || (!L.alive[i] && (hs[0] != 0u || hs[1] != 0u));
+        if (__ballot(want)) refill_stg(i, want);
+      } else if (__ballot(done)) {
         stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC, PK2>(L, i, done, unext, uend, exhausted, ctr, nunits, total32,
                                                            s0s, s0v, party, xs, nbytes, ppk, pf);
+      }
     }
+    if (STG) stage();
   }
   // ctr[2..3]: the launch's AES block count (dcf_prg_last_eval_blocks)
   if ((threadIdx.x & 63u) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + 1, (unsigned long long)nblk);
 }
 
 // One 1024-thread workgroup per CU (the replicated T-tables take 128 KiB of LDS).
-template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0, bool PK2 = false>
+template <int NS, bool XREG, bool MULTI, bool PFX = false, int NBC = 0, bool PK2 = false, bool STG = false>
 __global__ __launch_bounds__(kBlock, 1) void k_eval16_stream(
     const uint32_t* __restrict__ tab, const RoundKeys rk, const uint4* __restrict__ cw_s,
     const uint4* __restrict__ cw_v, const uint8_t* __restrict__ cw_t, const uint4* __restrict__ cw_np1,
@@ -527,9 +650,24 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_stream(
   // root-seed start path as well and spilled 45 SGPRs with SGPR keys (r04 resource usage): with x in
   // registers it takes the device-copy keys (0 spills); with x loaded per word the key look-ahead
   // registers would spill 2 VGPRs to scratch instead, so it keeps SGPR keys (40 SGPR spills, to VGPR lanes).
-  constexpr bool GK = !MULTI || (!PFX && XREG);
-  stream_run<NS, XREG, MULTI, kStreamUnit, GK, PFX, NBC, PK2>(lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs,
-                                                       nbytes, num_keys, ppk, total, ctr, ys, pf);
+#ifndef DCF_DIAG_SK
+#define DCF_DIAG_SK 0  // diagnostic: the C2 instance with SGPR round keys
+#endif
+#ifndef DCF_STG_GK
+#define DCF_STG_GK 0  // A/B: the staged instance with device-copy round keys
+#endif
+  constexpr bool C2I = !MULTI && PFX && NBC == 4;
+  constexpr bool GK = (!STG || DCF_STG_GK) && !(DCF_DIAG_SK && C2I) && (!MULTI || (!PFX && XREG));
+  if constexpr (STG) {  // 2 KiB of staged rows per wave beside the 128 KiB of tables (160 KiB in all)
+    __shared__ uint4 stg[kBlock / 64 * 128];
+    const uint32_t stg_lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(size_t)(__attribute__((address_space(3))) uint4*)stg + (threadIdx.x >> 6) * 2048u);
+    stream_run<NS, XREG, MULTI, kStreamUnit, GK, PFX, NBC, PK2, STG>(
+        lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party, xs, nbytes, num_keys, ppk, total, ctr, ys, pf, stg_lds);
+  } else {
+    stream_run<NS, XREG, MULTI, kStreamUnit, GK, PFX, NBC, PK2>(lds, rkg, rk, cw_s, cw_v, cw_t, cw_np1, s0s, party,
+                                                               xs, nbytes, num_keys, ppk, total, ctr, ys, pf);
+  }
   DCF_CLK(2, 1);
 }
 
