@@ -1206,7 +1206,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
 // 3.354-3.360 vs 3.391-3.396 ms (round 2's attempt at this split lost to a register-allocation flip).
 constexpr bool kSkPfx = DCF_SK_PFX;
 #ifndef DCF_STG
-#define DCF_STG 0
+#define DCF_STG 1
 #endif
 // N <= 4 single key below the table (C2): prefix rows staged two iterations ahead into LDS by DMA
 // (kernels_stream.h STG) instead of gathered at each point start.

@@ -280,14 +280,16 @@ __global__ __launch_bounds__(kKmThreads) void k_cw_keymajor(const uint4* __restr
 #define DCF_REUSE_RUN 0
 #endif
 // STG (staged rows; single key, prefix table, x in one word — C2): a wave claims its points in
-// halves of kStgUnit and stages each half ahead of use: the x words by an ordinary load (end of
-// iteration k), the 32-B prefix rows by LDS DMA into the wave's 2 KiB area (end of k + 1, x in by
-// then: lanes 0-31 the s halves, 32-63 the v halves), read by the refills of k + 2 instead of a
-// gather from HBM with the wave waiting.  The DMA is inline asm, so hipcc adds no vmcnt(0) for
-// it, and it is the iteration's last memory operation: it retires in order before the next
-// iteration's CW loads, whose wait precedes every read of the staged rows, and no wait inside its
-// own iteration drains it.  The AES rounds take their keys from SGPRs here: a device-copy key load
-// waits, in order, for every load issued before it, staged ones included (AB_LOG r05m).
+// halves of kStgUnit (from its own 256-point counter claims: 32-point atomics on the one counter ran
+// C2 2x slower) and stages each half ahead of use: the x words by an ordinary load (end of iteration
+// k), the 32-B prefix rows by LDS DMA into the wave's 2 KiB area (k + 1, right after the CW wait:
+// lanes 0-31 the s halves, 32-63 the v halves), read by the refills of k + 2 instead of a gather
+// from HBM at every point start.  The DMA is inline asm, so hipcc adds no vmcnt(0) for it; the
+// next iteration's CW wait retires it before any read of the staged rows, and the update and the
+// refills lie between it and the next round-key wait (in-order VM counter).  C2 r05as (same box, 4
+// alternating runs): 3.189-3.204 vs 3.237-3.258 ms with the DMA there and device-copy keys, 3.18-3.22
+// with SGPR keys (SGPR keys alone: +3.9 %), 3.18-3.23 with the DMA at the iteration's end; the
+// bound (rows from an L2-resident span, r05ar) is -6.8 %.
 constexpr uint32_t kStgUnit = 32;
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
   uint32_t keep;
@@ -297,6 +299,9 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
                : "memory");
 }
 
+#ifndef DCF_STG_EARLY
+#define DCF_STG_EARLY 1  // the staging DMA right after the CW wait (state 4 until the next one; 0: at the end)
+#endif
 // Wave priority knob (see the AES call in stream_run).
 #ifndef DCF_STREAM_PRIO
 #define DCF_STREAM_PRIO 1
@@ -366,7 +371,7 @@ __device__ __forceinline__ void stream_run(
       if (hs[h] == 0u) claim(h);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if (hs[h] == 2u) {  // xr[h]: copied by prep() this iteration
+      if (!DCF_STG_EARLY && hs[h] == 2u) {  // xr[h]: copied by prep() this iteration
         const uint32_t top = bswap32(xr[h]) >> (32u - pf.levels);
         glds16(pf.sv + 2u * top + (lane >> 5), stg_lds + 1024u * h);
         hs[h] = 3u;
@@ -381,8 +386,17 @@ __device__ __forceinline__ void stream_run(
   // address nor the refills' ds_bpermute makes hipcc wait for the claims' fresh x loads.
   auto prep = [&]() {
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      if (hs[h] == 2u) asm volatile("v_mov_b32 %0, %1" : "=v"(xr[h]) : "v"(xh[h]));
+    for (int h = 0; h < 2; ++h) {
+      if (DCF_STG_EARLY && hs[h] == 4u) hs[h] = 3u;  // its DMA retired with this iteration's CW wait
+      if (hs[h] == 2u) {
+        asm volatile("v_mov_b32 %0, %1" : "=v"(xr[h]) : "v"(xh[h]));
+        if (DCF_STG_EARLY) {  // the DMA here, an update and a refill ahead of the next key wait
+          const uint32_t top = bswap32(xr[h]) >> (32u - pf.levels);
+          glds16(pf.sv + 2u * top + (lane >> 5), stg_lds + 1024u * h);
+          hs[h] = 4u;
+        }
+      }
+    }
   };
   // Staged refill of the lanes whose stream i is free (`mine`) from the ready halves.
   auto refill_stg = [&](int i, bool mine) {
@@ -650,14 +664,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_stream(
   // root-seed start path as well and spilled 45 SGPRs with SGPR keys (r04 resource usage): with x in
   // registers it takes the device-copy keys (0 spills); with x loaded per word the key look-ahead
   // registers would spill 2 VGPRs to scratch instead, so it keeps SGPR keys (40 SGPR spills, to VGPR lanes).
-#ifndef DCF_DIAG_SK
-#define DCF_DIAG_SK 0  // diagnostic: the C2 instance with SGPR round keys
-#endif
 #ifndef DCF_STG_GK
-#define DCF_STG_GK 0  // A/B: the staged instance with device-copy round keys
+#define DCF_STG_GK 1  // the staged instance with device-copy round keys (0: SGPR keys, r05as)
 #endif
-  constexpr bool C2I = !MULTI && PFX && NBC == 4;
-  constexpr bool GK = (!STG || DCF_STG_GK) && !(DCF_DIAG_SK && C2I) && (!MULTI || (!PFX && XREG));
+  constexpr bool GK = (!STG || DCF_STG_GK) && (!MULTI || (!PFX && XREG));
   if constexpr (STG) {  // 2 KiB of staged rows per wave beside the 128 KiB of tables (160 KiB in all)
     __shared__ uint4 stg[kBlock / 64 * 128];
     const uint32_t stg_lds = __builtin_amdgcn_readfirstlane(
