@@ -290,7 +290,12 @@ __global__ __launch_bounds__(kKmThreads) void k_cw_keymajor(const uint4* __restr
 // alternating runs): 3.189-3.204 vs 3.237-3.258 ms with the DMA there and device-copy keys, 3.18-3.22
 // with SGPR keys (SGPR keys alone: +3.9 %), 3.18-3.23 with the DMA at the iteration's end; the
 // bound (rows from an L2-resident span, r05ar) is -6.8 %.
-constexpr uint32_t kStgUnit = 32;
+#ifndef DCF_STG_SLOTS
+#define DCF_STG_SLOTS 2  // A/B: staging slots per wave (2 KiB of LDS split evenly)
+#endif
+constexpr int kStgH = DCF_STG_SLOTS;
+constexpr uint32_t kStgUnit = 64 / kStgH;          // points per slot
+constexpr uint32_t kStgBytes = kStgUnit * 32u;     // LDS bytes per slot (s halves, then v halves)
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -340,7 +345,15 @@ __device__ __forceinline__ void stream_run(
   const uint4 np1v = cw_np1[0];  // single key: cw_np1 hoisted out of the loop
   // STG: per half h (wave-uniform) its first point, size, stage (0 free, 1 x loading, 2 rows
   // loading, 3 ready) and points handed out; xh[h]: lane r's raw x word of point base + (r & 31)
-  uint32_t hb[2] = {0u, 0u}, hn[2] = {0u, 0u}, hs[2] = {0u, 0u}, hu[2] = {0u, 0u}, xh[2] = {0u, 0u}, xr[2] = {0u, 0u};
+  uint32_t hb[kStgH], hn[kStgH], hs[kStgH], hu[kStgH], xh[kStgH], xr[kStgH];
+#pragma unroll
+  for (int h = 0; h < kStgH; ++h) hb[h] = hn[h] = hs[h] = hu[h] = xh[h] = xr[h] = 0u;
+  auto staged = [&]() {  // a slot holds points not handed out yet
+    bool any = false;
+#pragma unroll
+    for (int h = 0; h < kStgH; ++h) any = any || hs[h] != 0u;
+    return any;
+  };
   const uint32_t lane = threadIdx.x & 63u;
   auto claim = [&](int h) {  // the wave's next (up to) kStgUnit points into free half h, x loading
     if (unext >= uend && !exhausted) {  // the same UNIT-point claims as the direct path
@@ -357,7 +370,7 @@ __device__ __forceinline__ void stream_run(
     hn[h] = min(kStgUnit, uend - unext);
     unext += hn[h];
     hu[h] = 0u;
-    const uint32_t pp = hb[h] + min(lane & 31u, hn[h] - 1u);
+    const uint32_t pp = hb[h] + min(lane % kStgUnit, hn[h] - 1u);
     xh[h] = *reinterpret_cast<const uint32_t*>(xs + (size_t)pp * nbytes);
     hs[h] = 1u;
   };
@@ -367,18 +380,18 @@ __device__ __forceinline__ void stream_run(
   // (x loading), 2 x in (DMA due), 3 ready.
   auto stage = [&]() {
 #pragma unroll
-    for (int h = 0; h < 2; ++h)  // claims first: the counter atomic's wait would drain a DMA
+    for (int h = 0; h < kStgH; ++h)  // claims first: the counter atomic's wait would drain a DMA
       if (hs[h] == 0u) claim(h);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kStgH; ++h) {
       if (!DCF_STG_EARLY && hs[h] == 2u) {  // xr[h]: copied by prep() this iteration
         const uint32_t top = bswap32(xr[h]) >> (32u - pf.levels);
-        glds16(pf.sv + 2u * top + (lane >> 5), stg_lds + 1024u * h);
+        if (lane < 2u * kStgUnit) glds16(pf.sv + 2u * top + lane / kStgUnit, stg_lds + kStgBytes * h);
         hs[h] = 3u;
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < kStgH; ++h)
       if (hs[h] == 1u) hs[h] = 2u;
   };
   // After the iteration's CW wait (which retired every load of the previous iteration): the x words
@@ -386,13 +399,13 @@ __device__ __forceinline__ void stream_run(
   // address nor the refills' ds_bpermute makes hipcc wait for the claims' fresh x loads.
   auto prep = [&]() {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kStgH; ++h) {
       if (DCF_STG_EARLY && hs[h] == 4u) hs[h] = 3u;  // its DMA retired with this iteration's CW wait
       if (hs[h] == 2u) {
         asm volatile("v_mov_b32 %0, %1" : "=v"(xr[h]) : "v"(xh[h]));
         if (DCF_STG_EARLY) {  // the DMA here, an update and a refill ahead of the next key wait
           const uint32_t top = bswap32(xr[h]) >> (32u - pf.levels);
-          glds16(pf.sv + 2u * top + (lane >> 5), stg_lds + 1024u * h);
+          if (lane < 2u * kStgUnit) glds16(pf.sv + 2u * top + lane / kStgUnit, stg_lds + kStgBytes * h);
           hs[h] = 4u;
         }
       }
@@ -403,14 +416,14 @@ __device__ __forceinline__ void stream_run(
     uint64_t need = __ballot(mine);
     asm volatile("" ::: "memory");  // staged-row reads stay below the CW wait that retired their DMA
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kStgH; ++h) {
       if (need && hs[h] == 3u) {
         const uint32_t rank = lane_rank(need);
         const bool take = mine && rank < hn[h] - hu[h];
         const uint32_t r = min(hu[h] + rank, hn[h] - 1u);
         const uint32_t xw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(r << 2), (int)xr[h]);
-        const uint4 sv = lds_load16(stg_lds + 1024u * h + 16u * r);
-        const uint4 vv = lds_load16(stg_lds + 1024u * h + 512u + 16u * r);
+        const uint4 sv = lds_load16(stg_lds + kStgBytes * h + 16u * r);
+        const uint4 vv = lds_load16(stg_lds + kStgBytes * h + 16u * (kStgUnit + r));
         if (take) {  // stream_start below the shared prefix, with the row and x in hand (prefix_row)
           const uint32_t lev0 = pf.levels;
           L.s[i][0] = sv.x; L.s[i][1] = sv.y; L.s[i][2] = sv.z; L.s[i][3] = sv.w & kMaskLast;
@@ -455,7 +468,7 @@ __device__ __forceinline__ void stream_run(
       any = any || L.alive[i];
       nblk += (uint64_t)__popcll(__ballot(L.alive[i]));
     }
-    const bool pend = STG && (hs[0] != 0u || hs[1] != 0u);  // staged points not handed out yet
+    const bool pend = STG && staged();  // staged points not handed out yet
     if (!__ballot(any) && !pend) break;
     // Correction words of each stream's current level (vector loads, issued before the AES),
     // and of the next level for a stream whose step may end with B still valid (a right
@@ -634,7 +647,7 @@ __device__ __forceinline__ void stream_run(
                                  L.v[i][2] ^ L.s[i][2] ^ (tm & np.z), L.v[i][3] ^ L.s[i][3] ^ (tm & np.w));
       }
       if (STG) {
-        const bool want = done || (!L.alive[i] && (hs[0] != 0u || hs[1] != 0u));
+        const bool want = done || (!L.alive[i] && staged());
         if (__ballot(want)) refill_stg(i, want);
       } else if (__ballot(done)) {
         stream_refill<NS, XREG, MULTI, UNIT, PFX, NBC, PK2>(L, i, done, unext, uend, exhausted, ctr, nunits, total32,
