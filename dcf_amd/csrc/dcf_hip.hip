@@ -30,7 +30,7 @@
 
 #include "dcf_hip.h"
 
-#define DCF_VERSION "dcf_amd 0.1.0 (gfx950)"
+#define DCF_VERSION "dcf_amd 0.2.0 (gfx950)"
 
 #include "aes_lds.h"
 #include "kernels16.h"
@@ -311,6 +311,16 @@ uint32_t prefix_dfs_levels(uint32_t levels, uint32_t S) {
 // walk, 2 runs, ms per step) 25 495.5 / 495.5, 26 491.6 / 492.0, 27 489.3 / 488.8, 28 488.9 / 488.8
 constexpr uint32_t kPrefixMax = 27;
 constexpr uint32_t kPrefixMaxForced = 28;  // dcf_prg_set_prefix_levels (2^28 x 33 B x 2 = 17.7 GB)
+// Nodes per workgroup region of k_prefix_build16's two ping-pong buffers (log2): the widest
+// level a workgroup writes there.  With a depth-first tail of H levels the breadth-first part
+// stops at level D - H, so that is 2^(D-H-S) nodes (at D = 27: 553 MB of buffers beside the
+// 4.3 GB table, r06; it was 2^(D-1-S), 4.4 GB); without one the last level goes straight to
+// the table and the widest buffered level is D - 1.
+uint32_t prefix_region_log2(uint32_t d, uint32_t S) {
+  const uint32_t H = prefix_dfs_levels(d, S);
+  return d - std::max<uint32_t>(H, 1u) - S;
+}
+
 // Device bytes of a shared-prefix table of depth d (table + build buffers, as build_prefix /
 // build_wide_prefix allocate them).
 size_t prefix_table_bytes(const dcf_prg* p, uint32_t d) {
@@ -318,7 +328,8 @@ size_t prefix_table_bytes(const dcf_prg* p, uint32_t d) {
   const uint32_t S = prefix_split(d);
   if (p->lambda > 16) return (((size_t)80 << d) + 255) + 2 * ((size_t)80 << (d - 1u));
   if (p->kind == 1) return 2 * ((((size_t)33 << d) + 255) & ~(size_t)255) + 256;
-  return ((((size_t)32 << d) + 255) & ~(size_t)255) + 2 * ((size_t)1 << S) * ((((size_t)33 << (d - 1u - S)) + 255) & ~(size_t)255);
+  return ((((size_t)32 << d) + 255) & ~(size_t)255) +
+         2 * ((size_t)1 << S) * ((((size_t)33 << prefix_region_log2(d, S)) + 255) & ~(size_t)255);
 }
 
 // Auto depth under the dcf_prg_set_prefix_max_bytes cap: shallower until it fits (none below 8).
@@ -412,7 +423,7 @@ int build_prefix(dcf_prg* p, Workspace* w, size_t n_bytes, int party, const uint
   const size_t nodeb = 33, half = (maxnodes * nodeb + 255) & ~(size_t)255;
   // Hirose: [table 2^D x 32 B | 2 x 2^S regions of 2^(D-1-S) nodes]; MMO: two level buffers + counters
   const uint32_t S = prefix_split(levels);
-  const uint32_t R = 1u << (levels - 1u - S);
+  const uint32_t R = 1u << prefix_region_log2(levels, S);
   const size_t region = ((size_t)R * nodeb + 255) & ~(size_t)255;
   const size_t tab_bytes = (maxnodes * 32 + 255) & ~(size_t)255;
   const size_t need = p->kind == 0 ? tab_bytes + 2 * ((size_t)1 << S) * region : 2 * half + 64 * sizeof(uint32_t);

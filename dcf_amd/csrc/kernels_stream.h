@@ -294,6 +294,10 @@ __global__ __launch_bounds__(kKmThreads) void k_cw_keymajor(const uint4* __restr
 #define DCF_STG_SLOTS 2  // A/B: staging slots per wave (2 KiB of LDS split evenly)
 #endif
 constexpr int kStgH = DCF_STG_SLOTS;
+// A slot's s halves are DMA'd by lanes [0, kStgUnit) and its v halves by [kStgUnit, 2 kStgUnit), so
+// the wave covers both only if 2 kStgUnit <= 64 (kStgH >= 2); kStgUnit = 64 / kStgH must be exact
+// and at least 2 (one slot silently staged the s halves only).
+static_assert(kStgH >= 2 && kStgH <= 32 && 64 % kStgH == 0, "DCF_STG_SLOTS: 2, 4, 8, 16 or 32");
 constexpr uint32_t kStgUnit = 64 / kStgH;          // points per slot
 constexpr uint32_t kStgBytes = kStgUnit * 32u;     // LDS bytes per slot (s halves, then v halves)
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {

@@ -81,23 +81,31 @@ __device__ __forceinline__ void aes256_small(uint32_t (&w)[4], const uint32_t* r
   for (int j = 0; j < 4; ++j) w[j] = o[j];
 }
 
-// W row r (coefficient t_r), 16 bytes at byte offset `off` (>= 32), see file header.
+// The W-row formula (see file header), the one definition every user shares: row r < n is
+// cw_v[r] ^ (r + 1 even ? cw_s[r] : 0), except bit 0 of byte LAMBDA - 1 (bit 24 of the last word
+// of the last piece), where cw_s joins only at r + 1 == n; row n is cw_np1 (passed as cv).
+__device__ __forceinline__ uint4 w_row_form(const uint4 cv, const uint4 cs, uint32_t r, uint32_t nlev,
+                                            bool last_piece) {
+  if (r >= nlev) return cv;
+  const uint32_t l = r + 1u, even = (l & 1u) ? 0u : 0xFFFFFFFFu;
+  uint4 w = make_uint4(cv.x ^ (cs.x & even), cv.y ^ (cs.y & even), cv.z ^ (cs.z & even), cv.w ^ (cs.w & even));
+  if (last_piece) {
+    const uint32_t bit = (cv.w ^ ((l == nlev) ? cs.w : 0u)) & 0x01000000u;
+    w.w = (w.w & ~0x01000000u) | bit;
+  }
+  return w;
+}
+
+// W row r (coefficient t_r) of key `key`, 16 bytes at byte offset `off`; zero for an offset outside
+// [32, LAMBDA) or r > n.
 __device__ __forceinline__ uint4 w_row_piece(const uint8_t* __restrict__ cw_s, const uint8_t* __restrict__ cw_v,
                                              const uint8_t* __restrict__ cw_np1, uint32_t nlev, uint32_t lam,
                                              uint64_t num_keys, uint64_t key, uint32_t r, uint32_t off) {
   if (r > nlev || off >= lam || off < 32u) return make_uint4(0u, 0u, 0u, 0u);
   if (r == nlev) return *reinterpret_cast<const uint4*>(cw_np1 + key * lam + off);
-  const uint32_t l = r + 1;
   const uint64_t ro = ((uint64_t)r * num_keys + key) * lam + off;
-  const uint4 cv = *reinterpret_cast<const uint4*>(cw_v + ro);
-  const uint4 cs = *reinterpret_cast<const uint4*>(cw_s + ro);
-  const uint32_t even = (l & 1u) ? 0u : 0xFFFFFFFFu;
-  uint4 w = make_uint4(cv.x ^ (cs.x & even), cv.y ^ (cs.y & even), cv.z ^ (cs.z & even), cv.w ^ (cs.w & even));
-  if (off + 16 == lam) {  // bit 0 of byte LAMBDA-1 (bit 24 of the last word)
-    const uint32_t bit = (cv.w ^ ((l == nlev) ? cs.w : 0u)) & 0x01000000u;
-    w.w = (w.w & ~0x01000000u) | bit;
-  }
-  return w;
+  return w_row_form(*reinterpret_cast<const uint4*>(cw_v + ro), *reinterpret_cast<const uint4*>(cw_s + ro), r, nlev,
+                    off + 16 == lam);
 }
 
 
@@ -389,25 +397,6 @@ __global__ void k_tvec_chunks(uint32_t* __restrict__ tvec, const uint32_t nlev, 
   o4[1] = make_uint4(out[4], out[5], out[6], out[7]);
 }
 
-// W row r (coefficient t_r) piece at byte offset off of key `key`, as the table build forms it:
-// cw_v[r] ^ (r + 1 even ? cw_s[r] : 0) for r < n, cw_np1 for r = n, bit 0 of byte LAMBDA - 1 per the
-// file header; zero for an offset outside [32, LAMBDA).
-__device__ __forceinline__ uint4 tail_w_row(const uint8_t* __restrict__ cw_s, const uint8_t* __restrict__ cw_v,
-                                            const uint8_t* __restrict__ cw_np1, uint32_t nlev, uint32_t lam,
-                                            uint64_t num_keys, uint64_t key, uint32_t r, uint32_t off) {
-  if (off < 32u || off >= lam) return make_uint4(0u, 0u, 0u, 0u);
-  if (r == nlev) return *reinterpret_cast<const uint4*>(cw_np1 + key * lam + off);
-  const uint64_t ro = ((uint64_t)r * num_keys + key) * lam + off;
-  const uint4 cv = *reinterpret_cast<const uint4*>(cw_v + ro), cs = *reinterpret_cast<const uint4*>(cw_s + ro);
-  const uint32_t l = r + 1u, even = (l & 1u) ? 0u : 0xFFFFFFFFu;
-  uint4 x = make_uint4(cv.x ^ (cs.x & even), cv.y ^ (cs.y & even), cv.z ^ (cs.z & even), cv.w ^ (cs.w & even));
-  if (off + 16 == lam) {  // bit 0 of byte LAMBDA-1: cw_s joins only at l == n
-    const uint32_t bit = (cv.w ^ ((l == nlev) ? cs.w : 0u)) & 0x01000000u;
-    x.w = (x.w & ~0x01000000u) | bit;
-  }
-  return x;
-}
-
 template <int R6, int R5, int ROW0 = 0>
 __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __restrict__ cw_s,
                                                              const uint8_t* __restrict__ cw_v,
@@ -458,17 +447,11 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
         }
 #pragma unroll
         for (int b = 0; b < 6; ++b) {
-          const uint32_t r = st + b, l = r + 1;
+          const uint32_t r = st + b;
           const bool valid = offok && (uint32_t)b < w && r <= nlev;
           const uint32_t vm = valid ? 0xFFFFFFFFu : 0u;
-          const uint32_t even = (r < nlev && !(l & 1u)) ? vm : 0u;  // cw_s joins W_l on even l (row n: np1 only)
-          uint4 x = make_uint4((cv[b].x & vm) ^ (cs[b].x & even), (cv[b].y & vm) ^ (cs[b].y & even),
-                               (cv[b].z & vm) ^ (cs[b].z & even), (cv[b].w & vm) ^ (cs[b].w & even));
-          if (off + 16 == lam && r < nlev) {  // bit 0 of byte LAMBDA-1: cw_s joins only at l == n
-            const uint32_t bit = (cv[b].w ^ ((l == nlev) ? cs[b].w : 0u)) & 0x01000000u & vm;
-            x.w = (x.w & ~0x01000000u) | bit;
-          }
-          wr[b] = x;
+          const uint4 x = w_row_form(cv[b], cs[b], r, nlev, off + 16 == lam);
+          wr[b] = make_uint4(x.x & vm, x.y & vm, x.z & vm, x.w & vm);
         }
       }
       uint4 acc = make_uint4(0u, 0u, 0u, 0u);
@@ -508,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_wide_tail2(const uint8_t* __res
     cst = *reinterpret_cast<const uint4*>(s0 + (uint64_t)kk * lam + off);
     if (off + 16 == lam) cst.w &= kMaskLast;
     if (ROW0 && party) {  // row 0 (t_0 = party for every point) folded into the constant
-      const uint4 w0 = tail_w_row(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, 0u, off);
+      const uint4 w0 = w_row_piece(cw_s, cw_v, cw_np1, nlev, lam, num_keys, key, 0u, off);
       cst = make_uint4(cst.x ^ w0.x, cst.y ^ w0.y, cst.z ^ w0.z, cst.w ^ w0.w);
     }
   }

@@ -136,11 +136,20 @@ int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
  * as the full-domain eval does) and starts each point at level D from its node:
  * D fewer levels per point, identical output bytes.
  *   levels = -1: automatic (the default): D = log2(points) (Aes128MatyasMeyerOseasPrg:
- *                log2(points) - 1), at most 26 (LAMBDA >= 32: log2(points) - 1, at most
+ *                log2(points) - 1), at most 27 (LAMBDA >= 32: log2(points) - 1, at most
  *                22), none below 8 or (LAMBDA = 16) for small batches;
  *   levels =  0: off;  levels > 0: that depth (capped at 28 (LAMBDA >= 32: 30) and
  *                at 8N - 1).
- * The table lives on the prg (its size follows the largest D used).
+ * The table and its build buffers are one allocation of the call's workspace; they stay
+ * resident on the prg (sized by the largest D used) until dcf_prg_trim / dcf_prg_free, and
+ * dcf_prg_device_bytes counts them.  Bytes at depth D:
+ *   Hirose, LAMBDA = 16:  32 * 2^D (rows) + the one-launch build's two node buffers,
+ *                         2 * 33 * 2^(D-H) with H = min(4, D - 18) levels built depth-first
+ *                         (33 * 2^D when D <= 18) — 4.85e9 B at D = 27 (2^28 points, the auto
+ *                         cap), 2.42e9 at 26, 0.61e9 at 24 (C2);
+ *   MMO, LAMBDA = 16:     2 * 33 * 2^D (level-by-level build, rows packed into one half) —
+ *                         8.86e9 B at D = 27;
+ *   LAMBDA >= 32:         160 * 2^D (80-B rows + the build's two node buffers) — 0.34e9 at 21.
  * Multi-key stream eval (LAMBDA = 16, >= 32 points per key, 8N > 6 levels):
  * each key's own top tree of depth 5 (32 rows of 32 B per key, 36 PRG calls per key)
  * unless levels = 0; if its buffer cannot be allocated the points walk from the root. */
@@ -153,9 +162,10 @@ int dcf_eval_prefix_levels(const dcf_prg* prg, size_t n_bytes, size_t num_keys, 
  * as consecutive launches over whole keys.  Pure arithmetic (no device access). */
 size_t dcf_eval_keys_per_launch(size_t n_bytes, size_t points_per_key);
 /* Cap on the device memory the AUTOMATIC prefix depth may allocate (table + build
- * buffers, which stay resident on the prg until it is freed): the auto depth is lowered
- * until they fit, and no table is built below depth 8.  0 = no cap (the default: up to
- * ~4.4 GB at depth 26, LAMBDA = 16).  Forced depths ignore it.  Output bytes never change. */
+ * buffers, which stay resident on the prg until dcf_prg_trim / dcf_prg_free; sizes above):
+ * the auto depth is lowered until they fit, and no table is built below depth 8.  0 = no cap
+ * (the default: 4.85e9 B at the auto cap D = 27, Hirose LAMBDA = 16).  Forced depths ignore
+ * it.  Output bytes never change. */
 int dcf_prg_set_prefix_max_bytes(dcf_prg* prg, size_t max_bytes);
 /* Device memory this dcf_prg currently holds (tables, prefix tables, scratch, staging, over
  * all of its workspaces). */

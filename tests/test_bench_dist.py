@@ -135,3 +135,28 @@ def test_spawn_ranks_env_and_exit_status(capfd):
     t0 = time.perf_counter()
     assert bench.spawn_ranks(2, [sys.executable, "-c", code], env=env) == 3
     assert time.perf_counter() - t0 < 30
+
+
+@pytest.mark.gpu
+def test_bench_c4_two_ranks_check():
+    """C4's N > 1 path (north_star: 2^22 points PER GPU, weak scaling, LAMBDA = 16384): 2 ranks
+    (no launcher), each rank its own point range, rank 0 regenerates both ranks' points and
+    compares output digests, and the one-process multi-GPU ABI check runs at LAMBDA = 16384."""
+    pts = 4099
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c4", "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--points", str(pts), "--no-cpu", "--no-compare", "--dist-backend", "gloo", "--check"]
+    out = subprocess.run(cmd, cwd=ROOT, env=_no_launcher_env(), capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _one_line(out)
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
+    assert d["config"]["lambda"] == 16384 and d["config"]["points_per_gpu"] == pts
+    assert d["config"]["global_points"] == 2 * pts
+    assert d["slice_check"]["slices_match"], d["slice_check"]
+    pr = d["per_rank"]["ranks"]
+    assert [r["rank"] for r in pr] == [0, 1]
+    assert [r["start"] for r in pr] == [0, pts] and all(r["points"] == pts for r in pr)
+    for r in pr:
+        assert r["kernel_ms"] > 0 and r["walk_ms"] > 0
+    abi = d["multi_gpu_abi_check"]
+    assert abi["ok"], abi
+    assert len(abi["devices"]) >= 2 and abi["slices_match"] and abi["gather_matches"]

@@ -190,7 +190,8 @@ def test_prefix_memory_cap_and_device_bytes(dcf):
     d = dcf.DcfImpl(16, 16, prg)
     assert prg.eval_prefix_levels(16, 1, 1 << 28) == 27
     prg.set_prefix_max_bytes(1 << 30)
-    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 23  # 2^23 x ~65 B fits 1 GiB, 2^24 does not
+    # depth 24: 0.61e9 B fits 1 GiB, depth 25 (1.21e9 B) does not (include/dcf_hip.h sizes)
+    assert prg.eval_prefix_levels(16, 1, 1 << 28) == 24
     prg.set_prefix_max_bytes(1000)
     assert prg.eval_prefix_levels(16, 1, 1 << 28) == 0
     prg.set_prefix_levels(12)
@@ -208,3 +209,39 @@ def test_prefix_memory_cap_and_device_bytes(dcf):
     torch.cuda.synchronize()
     assert torch.equal(capped, free)
     assert prg.device_bytes() >= small + (1 << 20) * 32   # the 2^20-row table is resident
+
+
+def prefix_bytes_header(D: int) -> int:
+    """Resident bytes of a Hirose LAMBDA = 16 shared-prefix table of depth D as include/dcf_hip.h
+    states them: 32 * 2^D rows + the build's two node buffers 2 * 33 * 2^(D - H), H = min(4, D - 18)."""
+    H = min(4, D - 18) if D > 18 else 0
+    return 32 * 2 ** D + (2 * 33 * 2 ** (D - H) if H else 33 * 2 ** D)
+
+
+@pytest.mark.gpu
+def test_prefix_table_resident_bytes_c3(dcf):
+    """After one auto-depth eval of 2^28 points (C3, D = 27) the prg holds the table and its
+    build buffers (4.85e9 B, include/dcf_hip.h) plus small per-workspace scratch — no more —
+    and dcf_prg_trim releases them."""
+    import torch
+    rng = np.random.default_rng(78)
+    keys = [rng.bytes(32) for _ in range(2)]
+    prg = dcf.Aes256HirosePrg(keys, 16)
+    d = dcf.DcfImpl(16, 16, prg)
+    k = d.gen(dcf.CmpFn(rng.bytes(16), rng.bytes(16)), [rng.bytes(16), rng.bytes(16)], dcf.BoundState.LtBeta)
+    T = lambda b: torch.from_numpy(np.frombuffer(b, np.uint8).copy()).cuda()  # noqa: E731
+    cwb, s0 = T(dcf.share_to_cwb(k, 16, 16)), T(k.s0s[0])
+    base = prg.device_bytes()
+    m = 1 << 28
+    assert prg.eval_prefix_levels(16, 1, m) == 27
+    xs = torch.zeros((m, 16), dtype=torch.uint8, device="cuda")
+    ys = d.eval_device(False, cwb, s0, xs)
+    torch.cuda.synchronize()
+    held = prg.device_bytes() - base
+    want = prefix_bytes_header(27)
+    assert want == 4_848_615_424
+    assert want <= held <= want + (64 << 20), (held, want)
+    del xs, ys
+    assert prg.trim() >= 1
+    assert prg.device_bytes() <= base + (1 << 20)
+
