@@ -81,7 +81,7 @@ def engine_peak(engine: str) -> float:
 def pmc_traffic(kernel: str, points: int, n_bytes: int, lam: int, prefix_levels: int = 0):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json: one entry per profiled launch shape, written by
-    scripts/prof_summary.py from scripts/leases/gpu_profile.sh: 2 x FETCH_SIZE + WRITE_SIZE,
+    scripts/prof_summary.py from `scripts/gpu.sh TAG profile W`: 2 x FETCH_SIZE + WRITE_SIZE,
     MI355X_MICROARCH.md §HBM), only when a profile ran this exact launch shape; else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -134,6 +134,29 @@ def wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine):
             "note": "peak = 1 / (executed AES-256 blocks per eval / 87.8 G blocks/s (T-table LDS bound) + "
                     "LAMBDA bytes per eval / 8 TB/s HBM write): the head (AES walk over bytes [0,32)) and the tail "
                     "(GF(2) combination writing bytes [32, LAMBDA)) run back to back"}
+
+
+def lds_clock_bound(workload: str, kern_s: float):
+    """Counter-backed bound of the workload's eval kernels from a committed profile
+    (profiles/lds_clock_bound.json, scripts/lds_clock_bound.py): each kernel's LDS-array cycles per
+    CU at the clock that kernel ran at, summed; frac = that bound / this line's kernel time.  None
+    when no profile of the workload is committed."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "lds_clock_bound.json")) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for e in t:
+        if e.get("workload") == workload:
+            return {"bound_ms": e["bound_ms"], "frac": e["bound_ms"] / (kern_s * 1e3),
+                    "bound_ms_at_2p4ghz": e["bound_ms_at_2p4ghz"],
+                    "clocks_ghz": {r["kernel"].split("<")[0]: round(r["clock_ghz"], 3) for r in e["kernels"]
+                                   if "clock_ghz" in r},
+                    "source": e["source"] + " via profiles/lds_clock_bound.json",
+                    "note": "sum over the eval kernels of SQ_LDS_IDX_ACTIVE / 256 CUs / (the kernel's clock = "
+                            "GRBM_GUI_ACTIVE / 8 XCDs / its mean duration): the LDS array 100 % busy at the clock "
+                            "the chip held (DESIGN.md section 7, C4); bound_ms_at_2p4ghz: the same cycles at 2.4 GHz"}
+    return None
 
 
 def zero_bits(xs: torch.Tensor, skip_bits: int = 0) -> int:
@@ -537,6 +560,8 @@ def run_eval(args, world, rank):
     }
     if lam > 16 and engine != "mmo-wide":
         out["roofline"]["prefix_levels"] = pfx  # wide stream head below a shared-prefix table
+        if args.workload == "c4" and nb == 16 and m == 1 << 22:
+            out["roofline"]["lds_clock_bound"] = lds_clock_bound("C4", kern_s)
         out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic_fields(
             kernel, m, nb, lam, pfx, m * (nb + lam))
     if check is not None:

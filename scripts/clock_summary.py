@@ -1,4 +1,4 @@
-"""Per-kernel effective clock from scripts/leases/archive/pmc_clock.sh runs (rocpd sqlite): mean
+"""Per-kernel effective clock from GRBM_GUI_ACTIVE PMC runs (round-3 lease script pmc_clock.sh, in git history) (rocpd sqlite): mean
 GRBM_GUI_ACTIVE per dispatch / 8 XCDs / mean kernel duration of the same run.
 
   python scripts/clock_summary.py gpurun_out/<tag>

@@ -17,6 +17,7 @@
 #                                   dcf_amd/libdcf_hip_<VARIANT>.so from scripts/build_variant.sh),
 #                                   one summary line per run appended to ab.txt
 #   abtest  VARIANT... [-- pytest args]  parity of each variant build on the GPU suite subset
+#   pmc     W "COUNTERS" [bench args]    one extra PMC pass (mean per dispatch per kernel printed)
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; CMD=$2; shift 2
@@ -96,6 +97,26 @@ profile)
   fi
   rm -rf $O/trace_$W $O/pmc_fetch_$W $O/pmc_write_$W $O/pmc_sq_$W
   echo "profiled $W"; head -20 $O/prof_$W.md
+  ;;
+pmc)  # one extra PMC pass of one workload: pmc W "COUNTERS" [bench args] (<= 8 SQ_, 4 TCC_, 2 TA_ ... per pass)
+  W=$1; C=$2; shift 2
+  B="bench.py $(steps_of $W | sed -e 's/--steps [0-9]*/--steps 2/' -e 's/--warmup [0-9]*/--warmup 1/') --no-cpu --no-compare $*"
+  N=pmc_x_${W}_$(echo $C | md5sum | cut -c1-6)
+  timeout -s KILL 240 rocprofv3 --pmc $C -d $O/$N -o pmc -- python $B > $O/$N.log 2>&1 || { tail -5 $O/$N.log; exit 1; }
+  python - "$O/$N" <<'PY'
+import glob, sqlite3, sys
+from collections import defaultdict
+sys.path.insert(0, "scripts")
+from prof_summary import short
+agg = defaultdict(lambda: defaultdict(list))
+for db in glob.glob(sys.argv[1] + "/**/*.db", recursive=True):
+    for k, c, v in sqlite3.connect(db).execute("select kernel_name, counter_name, value from counters_collection"):
+        agg[short(k)][c].append(v)
+for k, cs in agg.items():
+    if k.startswith("k_"):
+        print(k, " ".join(f"{c}={sum(v) / len(v):.4g}" for c, v in sorted(cs.items())))
+PY
+  rm -rf $O/$N
   ;;
 ab)
   W=$1; REPS=$2; shift 2

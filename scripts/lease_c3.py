@@ -1,5 +1,5 @@
 """Same-lease C3 evidence: the driver's bench command and a rocprofv3 kernel trace of the same
-workload taken in one gpurun call (scripts/leases/gpu_r05f.sh), reduced to one summary:
+workload taken in one gpurun call (`bash scripts/gpu.sh TAG trace`), reduced to one summary:
 
   python scripts/lease_c3.py gpurun_out/<tag> > profiles/<tag>_prof_c3.md
 

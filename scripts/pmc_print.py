@@ -1,5 +1,5 @@
 """Print mean-per-dispatch PMC values of the eval kernels (PMC_KERNELS: comma-separated name
-filters, default k_eval) in gpurun_out/<tag>/*/ (scripts/leases/archive/pmc_engines.sh, pmc_stall.sh)."""
+filters, default k_eval) in gpurun_out/<tag>/*/ (round-2/3 lease scripts pmc_engines.sh / pmc_stall.sh, in git history)."""
 import glob
 import os
 import sqlite3

@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 (rocpd sqlite) outputs of scripts/leases/gpu_profile_w.sh.
+"""Summarise rocprofv3 (rocpd sqlite) outputs of `bash scripts/gpu.sh TAG profile W`.
 
   python scripts/prof_summary.py gpurun_out/r01 > profiles/r01_summary.md
 

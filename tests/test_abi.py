@@ -45,7 +45,7 @@ def test_library_is_gfx950_code_object(hip_lib):
 
 
 def test_version_and_layout_helpers(hip_lib):
-    assert b"gfx950" in hip_lib.dcf_version()
+    assert b"gfx950" in hip_lib.dcf_version() and b"0.2.0" in hip_lib.dcf_version()  # INTEGRATION.md "ABI version"
     for nb, lam, K in ((16, 16, 1), (4, 16, 7), (3, 32, 5), (2, 16384, 1)):
         n = 8 * nb
         off = hip_lib.dcf_cwb_np1_offset(nb, lam, K)
