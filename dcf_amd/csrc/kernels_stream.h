@@ -308,6 +308,11 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
                : "memory");
 }
 
+// s_waitcnt immediate (gfx9 encoding): vmcnt(0), expcnt and lgkmcnt at their maxima (no wait).
+constexpr int kVmcnt0 = (0x7 << 4) | (0xF << 8);
+#ifndef DCF_STG_PIN
+#define DCF_STG_PIN 1  // A/B knob: the stream state pinned before the staging DMA (see stream_run)
+#endif
 #ifndef DCF_STG_EARLY
 #define DCF_STG_EARLY 1  // the staging DMA right after the CW wait (state 4 until the next one; 0: at the end)
 #endif
@@ -402,9 +407,22 @@ __device__ __forceinline__ void stream_run(
   // of halves due for their DMA, copied into registers no later load targets, so neither the DMA's
   // address nor the refills' ds_bpermute makes hipcc wait for the claims' fresh x loads.
   auto prep = [&]() {
+    // Slots whose DMA (last iteration) is out: retired by now — every vmcnt wait since (this
+    // iteration's round keys and CWs, issued after it) drained it, as vmcnt counts in order.  hipcc
+    // does not see the asm DMA, so that is made explicit: one vmcnt(0) before the slots'
+    // rows may be read, free here (the CW wait has retired every load in flight), and before this
+    // call's own DMAs below, which it would otherwise drain.
+    if (DCF_STG_EARLY) {
+      bool out = false;
+#pragma unroll
+      for (int h = 0; h < kStgH; ++h) out = out || hs[h] == 4u;
+      if (out) __builtin_amdgcn_s_waitcnt(kVmcnt0);
+#pragma unroll
+      for (int h = 0; h < kStgH; ++h)
+        if (hs[h] == 4u) hs[h] = 3u;
+    }
 #pragma unroll
     for (int h = 0; h < kStgH; ++h) {
-      if (DCF_STG_EARLY && hs[h] == 4u) hs[h] = 3u;  // its DMA retired with this iteration's CW wait
       if (hs[h] == 2u) {
         asm volatile("v_mov_b32 %0, %1" : "=v"(xr[h]) : "v"(xh[h]));
         if (DCF_STG_EARLY) {  // the DMA here, an update and a refill ahead of the next key wait
@@ -639,7 +657,16 @@ __device__ __forceinline__ void stream_run(
     // Finished points: y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), then refill.  (vmcnt counts
     // stores too, so the refill's wait for its x word also waits for this store; issuing the
     // store after the refill's loads measured slower, AB_LOG r02.)
-    if (STG) prep();
+    if (STG) {
+      // The level update (and so the AES's last round-key wait) before the staging DMA: else hipcc
+      // sinks the last round's key XOR below the DMA and its vmcnt(0) drains the DMA at once.
+      if (DCF_STG_PIN)
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+          asm volatile("" : "+v"(L.s[i][0]), "+v"(L.s[i][1]), "+v"(L.s[i][2]), "+v"(L.s[i][3]), "+v"(L.v[i][0]),
+                       "+v"(L.v[i][1]), "+v"(L.v[i][2]), "+v"(L.v[i][3]), "+v"(L.t[i]));
+      prep();
+    }
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const bool done = L.alive[i] && L.lev[i] == nlev;
