@@ -153,9 +153,10 @@ def lds_clock_bound(workload: str, kern_s: float):
                     "clocks_ghz": {r["kernel"].split("<")[0]: round(r["clock_ghz"], 3) for r in e["kernels"]
                                    if "clock_ghz" in r},
                     "source": e["source"] + " via profiles/lds_clock_bound.json",
-                    "note": "sum over the eval kernels of SQ_LDS_IDX_ACTIVE / 256 CUs / (the kernel's clock = "
+                    "note": "sum over the step's kernels of SQ_LDS_IDX_ACTIVE / 256 CUs / (the kernel's clock = "
                             "GRBM_GUI_ACTIVE / 8 XCDs / its mean duration): the LDS array 100 % busy at the clock "
-                            "the chip held (DESIGN.md section 7, C4); bound_ms_at_2p4ghz: the same cycles at 2.4 GHz"}
+                            "the chip held (DESIGN.md section 7); bound_ms_at_2p4ghz: the same cycles at 2.4 GHz; "
+                            "from a committed profile of this launch shape, not this run"}
     return None
 
 
@@ -562,6 +563,9 @@ def run_eval(args, world, rank):
         out["roofline"]["prefix_levels"] = pfx  # wide stream head below a shared-prefix table
         if args.workload == "c4" and nb == 16 and m == 1 << 22:
             out["roofline"]["lds_clock_bound"] = lds_clock_bound("C4", kern_s)
+    elif args.prg == "hirose" and (args.workload, nb, m) in (("c1", 16, 100_000), ("c2", 4, 1 << 24), ("c3", 16, 1 << 28)):
+        # the default launch shapes the committed profiles ran (per-party kernel time)
+        out["roofline"]["lds_clock_bound"] = lds_clock_bound(args.workload.upper(), kern_s)
         out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic_fields(
             kernel, m, nb, lam, pfx, m * (nb + lam))
     if check is not None:
@@ -785,6 +789,7 @@ def run_c5(args, world, rank):
                                       "measured_ceiling": measured_ceiling(eval_blocks / eval_s)},
                         "gen_only": {"achieved": gen_blocks / phase[0] / 1e9, "frac": gen_blocks / phase[0] / peak},
                         "traffic": traffic, "traffic_source": traffic_src, "algorithmic_bytes": alg_bytes,
+                        "lds_clock_bound": lds_clock_bound("C5", step_s) if (K, nb) == (1 << 20, 16) else None,
                         "kernel_ms": step_s * 1e3, "hbm_GBps": alg_bytes / step_s / 1e9,
                         "executed_blocks_per_step": gen_blocks + eval_blocks,
                         "note": "gen: 4 AES-256 blocks per level per key (k_gen16); eval: blocks the multi-key "

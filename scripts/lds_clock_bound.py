@@ -1,6 +1,7 @@
 """Counter-backed LDS bound of a workload's kernels at the clock the chip held.
 
-  python scripts/lds_clock_bound.py profiles/r06/r06c_prof_c4.md C4 > profiles/lds_clock_bound.json
+  python scripts/lds_clock_bound.py profiles/r06/r06c_prof_c4.md C4 profiles/r05/r05ap_prof_c3.md C3 ... \\
+      > profiles/lds_clock_bound.json
 
 Reads one `scripts/gpu.sh TAG profile W` summary (prof_summary.py markdown: the kernel trace's mean
 duration per kernel and the SQ pass's SQ_LDS_IDX_ACTIVE / GRBM_GUI_ACTIVE means per dispatch) and,
@@ -33,11 +34,12 @@ def parse(md):
     return avg, pmc
 
 
-def bound(md, workload, kernels=("k_eval", "k_wpfx", "k_tvec", "k_prefix", "k_cw", "k_mk", "k_gen")):
+def bound(md, workload, kernels=("k_eval", "k_wpfx", "k_tvec", "k_prefix", "k_cw", "k_mk", "k_gen16<")):
     avg, pmc = parse(md)
     rows, total_ms, meas_ms = [], 0.0, 0.0
     for k, ms in avg.items():
-        if not k.startswith(kernels) or k.startswith("k_gen"):  # gen runs once, outside the timed eval
+        # the key's gen runs once outside the timed step (C1-C4); C5's batched gen is part of its step
+        if not k.startswith(kernels) or (k.startswith("k_gen") and workload != "C5"):
             continue
         c = pmc.get(k, {})
         meas_ms += ms
@@ -62,4 +64,6 @@ def bound(md, workload, kernels=("k_eval", "k_wpfx", "k_tvec", "k_prefix", "k_cw
 
 
 if __name__ == "__main__":
-    print(json.dumps([bound(sys.argv[1], sys.argv[2])], indent=1))
+    # pairs of (profile summary, workload): python scripts/lds_clock_bound.py A.md C4 B.md C3 ...
+    a = sys.argv[1:]
+    print(json.dumps([bound(a[i], a[i + 1]) for i in range(0, len(a), 2)], indent=1))

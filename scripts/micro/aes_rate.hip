@@ -188,6 +188,34 @@ void run(const char* name, int cus, const uint32_t* dtab, const RoundKeys& rk, c
   }
 }
 
+// Occupancy sweep (C1's ceiling): one workgroup of `waves` waves per CU, one AES block per lane,
+// round keys per round from global memory as the pair walk (k_eval16_pair) reads them; blocks / s
+// per CU against the waves the CU holds (C1: 100k points x 2 lanes = 13 waves on 241 CUs).
+void occupancy(int cus, const uint32_t* dtab, const RoundKeys& rk, const uint4* rkg, uint32_t* out) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  // NB = 1 at 4 .. 16 waves; NB = 2 at half the waves (the same blocks in flight, twice the ILP)
+  for (int cfg = 0; cfg < 9; ++cfg) {
+    const int nb = cfg < 6 ? 1 : 2;
+    const int waves = cfg < 6 ? (int[]){4, 8, 12, 13, 14, 16}[cfg] : (int[]){6, 7, 8}[cfg - 6];
+    for (int rep = 0; rep < 2; ++rep) {
+      hipEventRecord(e0);
+      if (nb == 1) hipLaunchKernelGGL((k_aes<1, 1>), dim3(cus), dim3(64 * waves), 0, 0, dtab, rk, rkg, out);
+      else hipLaunchKernelGGL((k_aes<2, 1>), dim3(cus), dim3(64 * waves), 0, 0, dtab, rk, rkg, out);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (rep == 1) {
+        const double blocks = (double)cus * 64 * waves * kIters * nb;
+        printf("occupancy %2d waves/CU, %d block(s)/lane, global keys: %8.3f ms  %6.2f G blocks/s  (%.3f of the 87.8 "
+               "LDS bound)\n", waves, nb, ms, blocks / (ms * 1e-3) / 1e9, blocks / (ms * 1e-3) / 87.77e9);
+      }
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -204,6 +232,10 @@ int main(int argc, char** argv) {
   hipMemcpy(dtab, g_tab, sizeof(g_tab), hipMemcpyHostToDevice);
   hipMemcpy(rkg, rk.w, 240, hipMemcpyHostToDevice);
   printf("CUs %d\n", cus);
+  if (argc > 1 && !strcmp(argv[1], "occ")) {
+    occupancy(cus, dtab, rk, rkg, out);
+    return 0;
+  }
   if (argc > 1 && !strcmp(argv[1], "mix")) {
     // LDS + vector-L1 split of the lookups, and the outputs against the all-LDS rounds
     for (int w : {4, 16}) {
