@@ -137,10 +137,10 @@ def wide_roofline(m, nb, lam, kern_s, exec_bpe, bpe, kernel, engine):
 
 
 def lds_clock_bound(workload: str, kern_s: float):
-    """Counter-backed bound of the workload's eval kernels from a committed profile
+    """Counter-backed bound of the workload's kernels from a committed profile
     (profiles/lds_clock_bound.json, scripts/lds_clock_bound.py): each kernel's LDS-array cycles per
-    CU at the clock that kernel ran at, summed; frac = that bound / this line's kernel time.  None
-    when no profile of the workload is committed."""
+    CU at the clock that kernel ran at, summed over one dispatch of each; frac = that bound / the
+    same kernels' traced time in the profiled run.  None when no profile of the workload is committed."""
     try:
         with open(os.path.join(ROOT, "profiles", "lds_clock_bound.json")) as f:
             t = json.load(f)
@@ -148,14 +148,18 @@ def lds_clock_bound(workload: str, kern_s: float):
         return None
     for e in t:
         if e.get("workload") == workload:
-            return {"bound_ms": e["bound_ms"], "frac": e["bound_ms"] / (kern_s * 1e3),
+            # frac within the profiled run (its clocks and its kernel times): a bound at one run's clocks
+            # against another run's time would mix boxes
+            return {"bound_ms": e["bound_ms"], "frac": e["frac_of_kernels"], "profiled_kernels_ms": e["kernels_ms"],
+                    "this_run_kernel_ms": kern_s * 1e3,
                     "bound_ms_at_2p4ghz": e["bound_ms_at_2p4ghz"],
                     "clocks_ghz": {r["kernel"].split("<")[0]: round(r["clock_ghz"], 3) for r in e["kernels"]
                                    if "clock_ghz" in r},
                     "source": e["source"] + " via profiles/lds_clock_bound.json",
                     "note": "sum over the step's kernels of SQ_LDS_IDX_ACTIVE / 256 CUs / (the kernel's clock = "
                             "GRBM_GUI_ACTIVE / 8 XCDs / its mean duration): the LDS array 100 % busy at the clock "
-                            "the chip held (DESIGN.md section 7); bound_ms_at_2p4ghz: the same cycles at 2.4 GHz; "
+                            "the chip held (DESIGN.md section 7), against the same kernels' traced time in that run (one dispatch "
+                            "each: C5's step runs the eval kernels twice); bound_ms_at_2p4ghz: the same cycles at 2.4 GHz; "
                             "from a committed profile of this launch shape, not this run"}
     return None
 
