@@ -1,6 +1,7 @@
 """Per-call time of device-resident single-key evals around DCF_EVAL_ROW_MAX (k_eval16_row vs
-k_eval16_oct) and of batched gens around DCF_GEN_ROW_MAX (k_gen16_row vs k_gen16_col):
-DCF_HIP_LIB=... python scripts/row_threshold.py [gen] -> one JSON line {m: us}."""
+k_eval16_oct), around DCF_EVAL_ROW2_MAX (`small`: k_eval16_row2 vs k_eval16_row) and of batched gens
+around DCF_GEN_ROW_MAX (k_gen16_row vs k_gen16_col):
+DCF_HIP_LIB=... python scripts/row_threshold.py [gen|small] -> one JSON line {m: us}."""
 import json
 import os
 import sys
@@ -35,7 +36,10 @@ def main():
             out[K] = (time.perf_counter() - t0) / 200 * 1e6
         print(json.dumps({"lib": os.environ.get("DCF_HIP_LIB", "default"), "gen_us": out}), flush=True)
         return
-    for m in (4096, 8192, 12000, 16384, 24576, 32768):
+    sizes = (4096, 8192, 12000, 16384, 24576, 32768)
+    if len(sys.argv) > 1 and sys.argv[1] == "small":  # around DCF_EVAL_ROW2_MAX (k_eval16_row2 vs k_eval16_row)
+        sizes = (1, 4, 16, 64, 128, 256, 512, 1024, 2048, 4096)
+    for m in sizes:
         xs = torch.randint(0, 256, (m, 16), dtype=torch.uint8, device="cuda")
         ys = torch.empty((m, 16), dtype=torch.uint8, device="cuda")
         for _ in range(20):
