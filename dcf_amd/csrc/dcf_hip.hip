@@ -1096,6 +1096,12 @@ int dcf_prg_trim(dcf_prg* p) {
 constexpr uint64_t kEvalOctMax = 32768;  // points (one key) up to which auto-mode eval runs k_eval16_oct
                                          // (r03a, us per device call: 32768 oct 187 vs pair 273; 100k 623 vs 485)
 constexpr uint64_t kEvalRowMax = 8192;   // points up to which auto-mode eval runs k_eval16_row (32 lanes per point)
+#ifndef DCF_EVAL_ROW2_MAX
+#define DCF_EVAL_ROW2_MAX 2048
+#endif
+constexpr uint64_t kEvalRow2Max = DCF_EVAL_ROW2_MAX;  // ... k_eval16_row2 (64 lanes per point, two levels per
+// chain on right steps) up to this many points (r06i, us per device call, row2 vs row: 1 point 75.7 vs
+// 97.6, 256 81.9 vs 108.1, 2048 87.4 vs 97.7, 4096 105.1 vs 100.3)
 constexpr uint64_t kGenRowMax = 2048;    // keys up to which gen runs k_gen16_row (one wave per key; pipelined, r03t3:
                                          // 2048 keys 110 vs 148 us col, 4096 keys 149 vs 147, 8192 277 vs 165)
 constexpr uint64_t kGenColMax = 16384;   // keys up to which gen runs k_gen16_col (r03a: 4096 keys 232 vs 562 us quads)
@@ -1310,6 +1316,16 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
     return DCF_OK;
   }
   int mode = c.mode;
+  if (oct_eval(p, c, n_bytes, num_keys, total) && total <= kEvalRow2Max) {
+    // The very smallest batches: one wave per point, two levels per AES chain on right steps
+    // (k_eval16_row2: rows 2 / 3 encrypt the right successor's blocks alongside the level's own).
+    phase_mark(p, L, 1);
+    const uint32_t ppw = per_wg(total, p->cus, kBlock / 64);
+    hipLaunchKernelGGL(k_eval16_row2, dim3((unsigned)((total + ppw - 1) / ppw)), dim3(kBlock), 0, st, p->d_tab,
+                       p->rk[0], cwb, s0s, (uint32_t)party, xs, (uint32_t)n_bytes, ppw, (uint64_t)total, ys, w->d_ctr);
+    HIP_TRY(hipGetLastError());
+    return DCF_OK;
+  }
   if (oct_eval(p, c, n_bytes, num_keys, total) && total <= kEvalRowMax) {
     // The smallest batches: 32 lanes per point, one table lookup per lane and AES round
     // (k_eval16_row: a lone point's level is one 16-lane AES chain).
@@ -1359,6 +1375,8 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
   hipLaunchKernelGGL(k_eval16_pair<MODE>, g2, b2, 0, st, p->d_tab, p->rk[0], cws, cwv, cwt, np1,                  \
                      (const uint4*)s0s, (uint32_t)party, xs, (uint32_t)n_bytes, (uint64_t)num_keys, (uint64_t)ppk,  \
                      (uint4*)ys, p->d_rk0, MODE == 0 ? spf : PrefixTable{nullptr, 0u})
+    // (r06i: a per-lane block schedule for one key, k_eval16_pair2 — ~100 instead of 128 AES passes
+    // per wave by simulation — ran 31 % slower on C1 and was removed; AB_LOG round 6)
     if (num_keys == 1) DCF_SMALL(0);
     else if (ppk % 64 == 0) DCF_SMALL(1);
     else DCF_SMALL(2);

@@ -372,6 +372,94 @@ __global__ __launch_bounds__(kBlock, 1) void k_eval16_row(
   DCF_CLK(3, 1);
 }
 
+// Dcf::eval (lib.rs:163-204) of one key at m points, one wave (64 lanes) per point, two levels per
+// AES chain whenever x goes right.  Rows 0 / 1 encrypt A = AES(s) and B = AES(~s) of level l as in
+// k_eval16_row; rows 2 / 3 encrypt the same two blocks of the seed level l + 1 has if x goes right
+// at l, s_R = s & M ^ t cw_s[l] (lib.rs:177-178: no AES needed to know it).  Going right, level l
+// needs only B (t_R = lsb(B ^ ~s), lib.rs:180), so level l + 1 completes in the same pass from rows 2
+// / 3; going left, rows 2 / 3 were speculation.  A lone point takes ~8N / 1.5 chains (~85 at N = 16)
+// instead of 8N.  The walk is wave-uniform (one point per wave), so the two-level step is a plain
+// branch; `ppw` points per workgroup (<= 16), spread over the CUs like k_eval16_row.
+__global__ __launch_bounds__(kBlock, 1) void k_eval16_row2(
+    const uint32_t* __restrict__ tab, const RoundKeys rk, const uint8_t* __restrict__ cwb,
+    const uint8_t* __restrict__ s0, const uint32_t party, const uint8_t* __restrict__ xs, const uint32_t nbytes,
+    const uint32_t ppw, const uint64_t m, uint8_t* __restrict__ ys, uint32_t* __restrict__ ctr) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint4 key[2 * kColMaxLevels + kColMaxLevels / 16 + 2];  // cw_s | cw_v | cw_t | cw_np1
+  __shared__ uint8_t xsh[(kBlock / 64) * (kColMaxLevels / 8)];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint4*>(ctr) = make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t n = 8u * nbytes;
+  const uint64_t p0 = (uint64_t)blockIdx.x * ppw;
+  const uint32_t np = (uint32_t)min<uint64_t>(ppw, m - p0);
+  const uint32_t np1_off = (2u * n * 16u + n + 15u) & ~15u;
+  const uint32_t kq = np1_off / 16u + 1u;
+  // every load first, then every LDS store (k_eval16_oct's prologue)
+  uint32_t tv[kFillPer];
+  lds_fill_load(tv, tab);
+  const bool kl = threadIdx.x < kq, xl = threadIdx.x < np * nbytes;
+  const uint4 kv = kl ? reinterpret_cast<const uint4*>(cwb)[threadIdx.x] : make_uint4(0u, 0u, 0u, 0u);
+  const uint8_t xv = xl ? xs[p0 * nbytes + threadIdx.x] : (uint8_t)0;
+  lds_fill_store(lds, tv);
+  if (kl) key[threadIdx.x] = kv;
+  if (xl) xsh[threadIdx.x] = xv;
+  for (uint32_t i = threadIdx.x + blockDim.x; i < kq; i += blockDim.x) key[i] = reinterpret_cast<const uint4*>(cwb)[i];
+  __syncthreads();
+  const uint32_t lc = lane_const();
+  const uint32_t pt = threadIdx.x >> 6, p = threadIdx.x & 15u, a = p & 3u, bq = p >> 2;
+  if (pt >= np) return;  // whole waves (whole points) leave together, after the only barrier
+  const uint32_t q = (threadIdx.x >> 4) & 3u;  // row: 0 A(s), 1 B(~s), 2 A(s_R), 3 B(~s_R)
+  uint32_t rkA[15], rkB[15];
+#pragma unroll
+  for (int r = 0; r < 15; ++r) {
+    const uint32_t w0 = rk.w[4 * r], w1 = rk.w[4 * r + 1], w2 = rk.w[4 * r + 2], w3 = rk.w[4 * r + 3];
+    rkA[r] = (a & 2u) ? ((a & 1u) ? w3 : w2) : ((a & 1u) ? w1 : w0);
+    rkB[r] = (bq & 2u) ? ((bq & 1u) ? w3 : w2) : ((bq & 1u) ? w1 : w0);
+  }
+  const uint32_t kA = (a - bq) & 3u, kB = (bq - a) & 3u;
+  const uint32_t selA = col16_sel(kA, kA), selB = col16_sel(kB, kB), selF = col16_sel(kB, (kB + 2u) & 3u);
+  const uint32_t fmask = 0xFFu << (8u * kB);
+  const uint32_t* kcs = reinterpret_cast<const uint32_t*>(key);             // cw_s[l] word a: kcs[4l + a]
+  const uint32_t* kcv = kcs + 4u * n;                                        // cw_v
+  const uint8_t* kct = reinterpret_cast<const uint8_t*>(key) + 32u * n;     // cw_t[l]
+  const uint32_t np1 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(key) + np1_off)[a];
+  // bit l of x, Msb0 (lib.rs:181), from the staged row (wave-uniform: the point is the wave's); read
+  // well ahead of its use after the AES chain
+  const uint8_t* x = xsh + pt * nbytes;
+  auto xbit = [&](uint32_t l) { return ((uint32_t)x[l >> 3] >> (7u - (l & 7u))) & 1u; };
+  const uint32_t inv = 0u - (q & 1u);                               // odd rows encrypt ~seed (B)
+  const bool spec = (q >> 1) != 0u;                                 // rows 2 / 3: the right successor
+  const uint32_t msk = (a == 3u) ? kMaskLast : 0xFFFFFFFFu;         // clear bit 0 of byte 15 (prg.rs:65-68)
+  uint32_t s = reinterpret_cast<const uint32_t*>(s0)[a];            // k.s0s[0] (lib.rs:168)
+  uint32_t v = 0u, t = party;
+  // one level's update from its blocks A, B (column a in every lane): lib.rs:174-189
+  auto level = [&](uint32_t lv, uint32_t A, uint32_t B) {
+    const uint32_t xb = xbit(lv), cs = kcs[4u * lv + a], cv = kcv[4u * lv + a], ct = kct[lv];
+    const uint32_t keepA = xb - 1u, tm = 0u - t;
+    const uint32_t tl = (A ^ s) & 1u, tr = (B ^ ~s) & 1u;            // t' = lsb(side)[0] ^ t & cw.t(side)
+    const uint32_t tn = dpp<kQpBcast0>((xb ? tr : tl) ^ (t & (ct >> xb) & 1u));
+    v ^= ((~s ^ (B & keepA)) & msk) ^ (tm & cv);                     // lib.rs:182/186
+    s = ((s ^ (A & keepA)) & msk) ^ (tm & cs);                       // lib.rs:177-178
+    t = tn;
+  };
+  for (uint32_t lev = 0; lev < n;) {
+    const uint32_t sR = (s & msk) ^ ((0u - t) & kcs[4u * lev + a]);  // level lev + 1's seed going right
+    const uint32_t mine = aes256_col16((spec ? sR : s) ^ inv, rkA, rkB, lds, lc, selA, selB, selF, fmask);
+    // rows (0,1) and (2,3) trade, then the wave halves: column a of A, B, A_R, B_R in every lane
+    const auto h = __builtin_amdgcn_permlane16_swap(mine, mine, false, false);
+    const auto e0 = __builtin_amdgcn_permlane32_swap(h[0], h[0], false, false);  // {A, A_R}
+    const auto e1 = __builtin_amdgcn_permlane32_swap(h[1], h[1], false, false);  // {B, B_R}
+    const bool right = xbit(lev) != 0u;
+    level(lev, e0[0], e1[0]);
+    ++lev;
+    if (right && lev < n) {  // wave-uniform: s is now s_R, whose blocks rows 2 / 3 encrypted
+      level(lev, e0[1], e1[1]);
+      ++lev;
+    }
+  }
+  if (q == 0u && p < 4u)  // y = v ^ s_n ^ t_n*cw_np1 (lib.rs:192), column a of point p0 + pt
+    reinterpret_cast<uint32_t*>(ys)[(p0 + pt) * 4u + a] = v ^ s ^ ((0u - t) & np1);
+}
+
 // Dcf::gen (lib.rs:86-161) of num_keys keys, 16 lanes per key: `kpw` keys per workgroup of
 // kBlock threads (spread over the CUs as k_eval16_oct spreads points).  Inputs and the CWB
 // output may be host-mapped.
