@@ -21,7 +21,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "libdcf_oracle.so")
+# DCF_ORACLE_LIB: another build of the same source (scripts/host_sanitize.sh: ASan + UBSan)
+_LIB_PATH = os.environ.get("DCF_ORACLE_LIB") or os.path.join(_HERE, "build", "libdcf_oracle.so")
 _lib = None
 
 LT_BETA = 0

@@ -78,3 +78,45 @@ def test_json_forms(hip_lib):
                           .replace("True", "true").replace("False", "false"),
                           str(list(k.cw_np1)).replace(" ", ""))
     assert wire.share_from_json(seq, 16, 16) == k
+
+
+@pytest.mark.parametrize("nb,lam", [(16, 16), (1, 32)])
+def test_bincode_decode_mutation_fuzz(hip_lib, nb, lam):
+    """dcf_share_from_bincode on corrupted input (seeded mutations of a valid key: byte flips,
+    truncations, appended bytes and arbitrary u64 length fields): every call either fails with a
+    DcfError or returns a Share whose encoding is exactly the input (the decoder accepts only
+    canonical bincode).  Run under a host sanitizer by scripts/host_sanitize.sh."""
+    keys = REF_KEYS if lam == 16 else [bytes([i]) * 32 for i in range(18)]
+    good = wire.share_to_bincode(_oracle_share(nb, lam, keys), nb, lam)
+    rng = np.random.default_rng(11 + lam)
+    # offsets of the u64 length fields: vec len, 2 seeds, cws len, 2 per cw, cw_np1
+    lens = [0, 8, 16 + lam, 24 + 2 * lam]
+    o = 32 + 2 * lam
+    for _ in range(8 * nb):
+        lens += [o, o + 8 + lam]
+        o += 2 * (8 + lam) + 2
+    lens.append(o)
+    assert o + 8 + lam == len(good)
+    accepted = 0
+    for i in range(1500):
+        b = bytearray(good)
+        kind = i % 4
+        if kind == 0:  # flip 1-3 bytes anywhere
+            for p in rng.integers(0, len(b), rng.integers(1, 4)):
+                b[p] ^= int(rng.integers(1, 256))
+        elif kind == 1:  # truncate
+            b = b[:int(rng.integers(0, len(b)))]
+        elif kind == 2:  # extend
+            b += rng.bytes(int(rng.integers(1, 64)))
+        else:  # a length field set to a small, boundary or huge value
+            p = lens[int(rng.integers(0, len(lens)))]
+            vals = [0, 1, lam - 1, lam + 1, 8 * nb + 1, 2**31, 2**63, 2**64 - 1]
+            v = vals[int(rng.integers(0, len(vals)))]
+            b[p:p + 8] = struct.pack("<Q", v)
+        try:
+            k = wire.share_from_bincode(bytes(b), nb, lam)
+        except dcf_amd.DcfError:
+            continue
+        accepted += 1
+        assert wire.share_to_bincode(k, nb, lam) == bytes(b)
+    assert accepted < 1500 // 4  # most corruptions are rejected; byte flips inside payloads are not
