@@ -1024,10 +1024,11 @@ def run_latency(args, world, rank):
             "cpu_baseline": {"gen_us": cpu_gen_us, "eval_us": cpu_eval_us, "cores": 1, "kind": "port",
                              "sample": f"{iters} calls each, the C restatement with AES-NI, 1 thread",
                              "matches_gpu": match},
-            "note": "latency-bound: a tiny call is ONE launch of a latency kernel (kernels_lat.h: one AES column "
-                    "per lane; k_eval16_oct / k_gen16_col) that reads the key and points from, and writes its "
-                    "outputs to, a mapped pinned buffer, plus one stream sync; a lone point's 8N levels run back "
-                    "to back (~0.75 us per level at 2.4 GHz); batch the points (C1) for throughput"}
+            "note": "latency-bound: a tiny call is ONE launch of a latency kernel (kernels_lat.h: the AES of a "
+                    "block on a 16-lane row; k_eval16_row2 — two levels per AES chain on right steps — / "
+                    "k_gen16_row) that reads the key and points from, and writes its outputs to, a mapped pinned "
+                    "buffer, plus one stream sync; a lone point's 8N levels run back to back (~0.5 us per level); "
+                    "batch the points (C1) for throughput"}
 
 
 def json_stdout():
