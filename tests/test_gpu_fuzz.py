@@ -9,6 +9,8 @@ and checks y0 ^ y1 against beta * [x < alpha] / [x > alpha] (lib.rs:114-125 and 
 reconstruction KATs, lib.rs:372-420).  The shapes come from a fixed seed, so a failure names a
 reproducible case id.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -19,8 +21,15 @@ pytestmark = pytest.mark.gpu
 LAMS = [16, 16, 16, 32, 48, 64, 80, 96, 112, 128, 144, 256, 272, 384, 512, 1024]
 
 
-def _cases(n=128, seed=0xF022):
+# Extended sweeps (one-off GPU runs; the default is the suite's fixed list): DCF_FUZZ_CASES /
+# DCF_FUZZ_MK_CASES cases from DCF_FUZZ_SEED / DCF_FUZZ_MK_SEED, and with DCF_FUZZ_BIG=1 also
+# λ = 16 batches on the pair-walk (40000 points) and stream (600000) engines.
+_ENV = os.environ.get
+
+
+def _cases(n=int(_ENV("DCF_FUZZ_CASES", "128")), seed=int(_ENV("DCF_FUZZ_SEED", "0xF022"), 0)):
     rng = np.random.default_rng(seed)
+    big = _ENV("DCF_FUZZ_BIG") == "1"
     out = []
     for i in range(n):
         lam = int(rng.choice(LAMS))
@@ -29,11 +38,13 @@ def _cases(n=128, seed=0xF022):
         m = int(rng.choice([1, 2, 17, 64, 65, 300, 1000, 2049, 4097]))
         if lam >= 512:
             m = min(m, 300)
+        if big and lam == 16 and rng.random() < 0.3:
+            m = int(rng.choice([40000, 600000]))
         out.append((i, lam, nb, mmo, int(rng.integers(0, 2)), m))
     return out
 
 
-def _mk_cases(n=24, seed=0xF0A2):
+def _mk_cases(n=int(_ENV("DCF_FUZZ_MK_CASES", "24")), seed=int(_ENV("DCF_FUZZ_MK_SEED", "0xF0A2"), 0)):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
