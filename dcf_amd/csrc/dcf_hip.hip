@@ -301,8 +301,8 @@ uint32_t prefix_dfs_levels(uint32_t levels, uint32_t S) {
 // Shared-prefix depth for a single-key stream eval of `total` points (kernels_stream.h
 // PrefixTable): the top tree has 2^D nodes (33 B each, built with 2^(D+1) AES blocks)
 // and saves every point D levels.  Auto: D = log2(total) - 1 (table build < 1 block per
-// point; Hirose: log2(total)), at most kPrefixMax = 27 (a 4.3 GB table of 32-B rows beside 4.4 GB of build
-// buffers), none below 8, always < 8N.  If the buffers cannot be
+// point; Hirose: log2(total)), at most kPrefixMax = 27 (a 4.3 GB table of 32-B rows beside 0.55 GB of build
+// buffers since r06; prefix_table_bytes), none below 8, always < 8N.  If the buffers cannot be
 // allocated in auto mode, eval retries 2 levels shallower down to 8, then runs without a
 // table (identical bytes; see try_prefix).  Measured (r01i, C2: 2^24 points, N = 4):
 // D = 12 / 16 / 20 / 24 -> 2.00 / 2.29 / 2.62 / 2.83 G evals/s (1.44 without);
@@ -310,7 +310,7 @@ uint32_t prefix_dfs_levels(uint32_t levels, uint32_t S) {
 // auto cap.  C3 sweeps (2^28 points): r01q 24 519, 25 521, 26 524, 27 524 M evals/s; r05y (today's
 // walk, 2 runs, ms per step) 25 495.5 / 495.5, 26 491.6 / 492.0, 27 489.3 / 488.8, 28 488.9 / 488.8
 constexpr uint32_t kPrefixMax = 27;
-constexpr uint32_t kPrefixMaxForced = 28;  // dcf_prg_set_prefix_levels (2^28 x 33 B x 2 = 17.7 GB)
+constexpr uint32_t kPrefixMaxForced = 28;  // dcf_prg_set_prefix_levels (Hirose 9.7 GB, MMO 2^28 x 33 B x 2 = 17.7 GB)
 // Nodes per workgroup region of k_prefix_build16's two ping-pong buffers (log2): the widest
 // level a workgroup writes there.  With a depth-first tail of H levels the breadth-first part
 // stops at level D - H, so that is 2^(D-H-S) nodes (at D = 27: 553 MB of buffers beside the
