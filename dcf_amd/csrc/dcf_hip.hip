@@ -1238,6 +1238,10 @@ constexpr bool kMkNbc16 = DCF_MK_NBC16;  // A/B knob: the N = 16 multi-key top-t
 // ... and of it, for a power-of-two points per key (C5: 64), point -> key by a shift instead of
 // the division sequence (65 fewer VALU in the kernel)
 constexpr bool kMkPk2 = DCF_MK_PK2;
+#ifndef DCF_MK_NBC4
+#define DCF_MK_NBC4 1
+#endif
+constexpr bool kMkNbc4 = DCF_MK_NBC4;  // A/B knob: the N = 4 multi-key top-tree instance (C5 at N = 4)
 
 static int eval_launch(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size_t ppk, int party,
                        const uint8_t* cwb, const uint8_t* s0s, const uint8_t* xs, uint8_t* ys) {
@@ -1504,6 +1508,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
       if (multi && lpf.levels) {
         if (xreg && n_bytes == 16 && kMkNbc16 && kMkPk2 && (ppk & (ppk - 1)) == 0) DCF_STREAM6(true, true, true, 16, true);
         else if (xreg && n_bytes == 16 && kMkNbc16) DCF_STREAM(true, true, true, 16);
+        else if (xreg && n_bytes == 4 && kMkNbc4 && (ppk & (ppk - 1)) == 0) DCF_STREAM6(true, true, true, 4, true);
         else if (xreg) DCF_STREAM(true, true, true, 0);
         else DCF_STREAM(false, true, true, 0);
       } else if (multi) {

@@ -216,14 +216,15 @@ def test_config_c4(dcf):
     check_reconstruction(xs, T(alpha), T(beta), y0, y1, chunk=1 << 15)
 
 
-def test_config_c5(dcf):
-    """C5: 2^20 independent keys x 64 points, N = 16, LAMBDA = 16: batched gen (one launch),
-    then multi-key eval of both parties.  Sample: the CWB of 130 keys (first, last, random)
-    against the oracle's gen and all 64 points of each (8320 evals per party);
-    reconstruction on all 2^26 points with each key's alpha / beta."""
+@pytest.mark.parametrize("nb", [16, 4])
+def test_config_c5(dcf, nb):
+    """C5: 2^20 independent keys x 64 points, N = 16 (and N = 4), LAMBDA = 16:
+    batched gen (one launch), then multi-key eval of both parties.  Sample: the CWB of 130 keys
+    (first, last, random) against the oracle's gen and all 64 points of each (8320 evals per
+    party); reconstruction on all 2^26 points with each key's alpha / beta."""
     import torch
-    nb, lam, K, Pk = 16, 16, 1 << 20, 64
-    rng = np.random.default_rng(0xC5)
+    lam, K, Pk = 16, 1 << 20, 64
+    rng = np.random.default_rng(0xC5 + nb)
     keys = [rng.bytes(32) for _ in range(2)]
     prg, Po = dcf.Aes256HirosePrg(keys, lam), O.OraclePrg(keys, lam)
     d = dcf.DcfImpl(nb, lam, prg)

@@ -231,7 +231,8 @@ def test_eval_device_large_sample_and_reconstruction(dcf, nb, m, mode):
     assert not rec[~lt].any()
 
 
-@pytest.mark.parametrize("nb,K,P", [(1, 70, 64), (3, 130, 40), (5, 65, 33), (16, 200, 32), (17, 40, 48), (32, 70, 40)])
+@pytest.mark.parametrize("nb,K,P", [(1, 70, 64), (3, 130, 40), (4, 70, 64), (4, 130, 32), (4, 65, 48), (5, 65, 33),
+                                     (16, 200, 32), (17, 40, 48), (32, 70, 40)])
 def test_multikey_stream_widths_vs_oracle(dcf, nb, K, P):
     """Multi-key stream eval (per-key top trees, key-major CW digest) at 8N levels that are not a
     multiple of the digest's 16-level tiles and key counts that are not a multiple of 64."""
