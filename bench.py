@@ -469,8 +469,9 @@ def run_eval(args, world, rank):
         w0, k0 = timed_loop(step, args.steps, args.warmup, world)
         np_blocks = prg.last_eval_blocks()
         prg.set_prefix_levels(args.prefix)
+        small_path = args.eval_mode == 0 and lam == 16 and m < CUS * 1024 * 2  # the pair walk: A and B every level
         no_prefix = {"value": global_points * args.steps * parties / w0, "kernel_ms": k0 / parties * 1e3,
-                     "executed_blocks_per_eval": 16 * nb if args.prg == "mmo" else (
+                     "executed_blocks_per_eval": 16 * nb if args.prg == "mmo" else 2 * 8 * nb if small_path else (
                          np_blocks / m if np_blocks else 8 * nb + zero_bits(xs) / m),
                      "speedup": w0 / wall}
     total_evals = global_points * args.steps * parties
@@ -500,7 +501,7 @@ def run_eval(args, world, rank):
         walk = dev_blocks / m if dev_blocks else (8 * nb - pfx) + zero_bits(xs, pfx) / m
         exec_bpe = walk + (2 ** (pfx + 1) - 2) / m
     elif engine == "mmo" or (engine == "ttable-small" and pfx):
-        # lockstep walks (A and B every level) below a forced shared prefix
+        # lockstep walks (A and B every level) below a shared prefix (auto on the small path since r06)
         exec_bpe = 2 * (8 * nb - pfx) + (2 ** (pfx + 1) - 2) / m
     else:
         exec_bpe = bpe

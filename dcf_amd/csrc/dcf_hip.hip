@@ -356,14 +356,38 @@ uint32_t prefix_depth(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t n
   return std::min<uint32_t>(d, (uint32_t)(8 * n_bytes - 1));
 }
 
-// Shared-prefix depth for the small-batch pair path (k_eval16_pair, auto mode, fewer points than
-// two per lane of the GPU): only a forced depth (dcf_prg_set_prefix_levels).  In auto mode a
-// C1-size batch walks without a table: C1 A/B (same box, 300 steps, M evals/s) no table
-// 226.3-226.4, D = 14 / 15 / 16 (log2(points) - 1..3) 221.1-221.5 / 221.2-221.5 / 221.8-222.1 —
-// the build's D sequential levels on few workgroups cost what the walk saves.
-uint32_t small_prefix_depth(const dcf_prg* p, const Cfg& c, size_t n_bytes) {
-  if (p->lambda != 16 || p->kind != 0 || c.prefix_levels <= 0) return 0;
-  return std::min<uint32_t>(std::min((uint32_t)c.prefix_levels, kPrefixMaxForced), (uint32_t)(8 * n_bytes - 1));
+// Tiny batches run the latency kernels of kernels_lat.h (thresholds below and at kEvalRowMax).
+#ifndef DCF_EVAL_OCT_MAX
+#define DCF_EVAL_OCT_MAX 32768
+#endif
+constexpr uint64_t kEvalOctMax = DCF_EVAL_OCT_MAX;  // points (one key) up to which auto-mode eval runs k_eval16_oct
+                                         // (r03a, us per device call: 32768 oct 187 vs pair 273; 100k 623 vs 485)
+bool oct_eval(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t num_keys, uint64_t total) {
+  return p->kind == 0 && p->lambda == 16 && num_keys == 1 && total <= kEvalOctMax && 8 * n_bytes <= kColMaxLevels &&
+         c.prefix_levels <= 0 && c.mode == DCF_EVAL_AUTO;
+}
+
+// Shared-prefix depth for the small-batch pair path (k_eval16_pair: one key, fewer points than
+// two per lane of the GPU, more than the latency kernels take).  Forced: dcf_prg_set_prefix_levels.
+// Auto: 18 below 2^18 points, 19 from there (at most 8N - 1; none below 8 or up to kEvalOctMax
+// points) — the build is one
+// launch of k_prefix_build16 (row-AES root path, depth-first tail) whose blocks cost far less than
+// the walk's latency-bound levels they save.  r06 sweep (one key, both parties, ms per step;
+// `scripts/c1_prefix_sweep.sh`, profiles/r06/r06v_*): N = 16 100k points 0.895 without a table,
+// 0.851 / 0.850 / 0.860 at D = 17 / 18 / 19; 250k 1.878 vs 1.704 at 18; 500k 3.736 vs 3.299 at 19;
+// N = 4 100k 0.249 vs 0.200 at 18, 400k 0.966 vs 0.530 at 19; N = 8 100k 0.464 vs 0.413 at 18.
+// (Round 3 measured no gain at D = 14-16 on C1, before the build's row-AES root path and
+// depth-first tail.)
+uint32_t small_prefix_depth(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t total) {
+  if (p->lambda != 16 || p->kind != 0 || c.prefix_levels == 0) return 0;
+  const uint32_t cap = (uint32_t)(8 * n_bytes - 1);
+  if (c.prefix_levels > 0) return std::min<uint32_t>(std::min((uint32_t)c.prefix_levels, kPrefixMaxForced), cap);
+  // none up to kEvalOctMax points: the latency kernels walk from the root there, and at N > 32 (the
+  // pair walk) a table's fixed build latency would cost more than a few thousand points save
+  if (total <= kEvalOctMax) return 0;
+  const uint32_t lg = 63u - (uint32_t)__builtin_clzll(total | 1u);
+  const uint32_t d = capped_depth(p, c, std::min<uint32_t>(lg < 18u ? 18u : 19u, cap));
+  return d >= 8u ? d : 0u;
 }
 
 // Shared-prefix depth for the LAMBDA >= 32 stream head over m points of one key
@@ -977,7 +1001,7 @@ int dcf_eval_prefix_levels(const dcf_prg* p, size_t n_bytes, size_t num_keys, si
   if (p->kind == 1) return small && c.prefix_levels < 0 ? 0 : (int)prefix_depth(p, c, n_bytes, num_keys, total);
   if (p->lambda > 16)  // batched keys (eval_wide_batch) build no table; per-key passes do
     return wide_batched(p, c, num_keys, points_per_key) ? 0 : (int)wide_prefix_depth(p, c, n_bytes, points_per_key);
-  if (c.mode == DCF_EVAL_AUTO && small) return num_keys == 1 ? (int)small_prefix_depth(p, c, n_bytes) : 0;
+  if (c.mode == DCF_EVAL_AUTO && small) return num_keys == 1 ? (int)small_prefix_depth(p, c, n_bytes, total) : 0;
   if (c.mode != DCF_EVAL_AUTO && c.mode != DCF_EVAL_STREAM) return 0;
   return (int)prefix_depth(p, c, n_bytes, num_keys, total);
 }
@@ -1093,8 +1117,6 @@ int dcf_prg_trim(dcf_prg* p) {
 
 // Tiny batches run the latency kernels of kernels_lat.h (one AES column per lane).  Thresholds:
 // scripts/lat_sweep.py / row_threshold.py (DESIGN.md §4 "Latency kernels", profiles/AB_LOG.md).
-constexpr uint64_t kEvalOctMax = 32768;  // points (one key) up to which auto-mode eval runs k_eval16_oct
-                                         // (r03a, us per device call: 32768 oct 187 vs pair 273; 100k 623 vs 485)
 constexpr uint64_t kEvalRowMax = 8192;   // points up to which auto-mode eval runs k_eval16_row (32 lanes per point)
 #ifndef DCF_EVAL_ROW2_MAX
 #define DCF_EVAL_ROW2_MAX 2048
@@ -1110,10 +1132,6 @@ constexpr uint64_t kGenColMax = 16384;   // keys up to which gen runs k_gen16_co
 static uint32_t per_wg(uint64_t items, int cus, uint32_t cap) {
   const uint64_t per = (items + (uint64_t)cus - 1) / (uint64_t)cus;
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, per));
-}
-static bool oct_eval(const dcf_prg* p, const Cfg& c, size_t n_bytes, uint64_t num_keys, uint64_t total) {
-  return p->kind == 0 && p->lambda == 16 && num_keys == 1 && total <= kEvalOctMax && 8 * n_bytes <= kColMaxLevels &&
-         c.prefix_levels <= 0 && c.mode == DCF_EVAL_AUTO;
 }
 static bool col_gen(const dcf_prg* p, size_t n_bytes, uint64_t num_keys) {
   return p->kind == 0 && p->lambda == 16 && num_keys <= kGenColMax && 8 * n_bytes <= kColMaxLevels;
@@ -1360,7 +1378,7 @@ static int eval_body(dcf_prg* p, Lease& L, size_t n_bytes, size_t num_keys, size
   if (mode == DCF_EVAL_AUTO && total < (uint64_t)p->cus * kBlock * 2) {
     PrefixTable spf{nullptr, 0u};
     if (num_keys == 1) {
-      const uint32_t d = small_prefix_depth(p, c, n_bytes);
+      const uint32_t d = small_prefix_depth(p, c, n_bytes, total);
       if (d) {
         int rc = try_prefix(p, c, w, n_bytes, party, cws, cwv, cwt, np1, s0s, d, &spf, st);
         if (rc) return rc;

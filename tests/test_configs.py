@@ -113,7 +113,7 @@ def test_config_c1(dcf):
     import torch
     nb, lam, m = 16, 16, 100_000
     rng, prg, P, d, k, ok, (alpha, beta, s0, s1), T = single_key_setup(dcf, nb, lam, 2, 0xC1)
-    assert prg.eval_prefix_levels(nb, 1, m) == 0  # small batch: no table in auto mode
+    assert prg.eval_prefix_levels(nb, 1, m) == 18  # small batch, auto: a depth-18 table below the pair walk (r06)
     xs = rng.integers(0, 256, (m, nb), dtype=np.uint8)
     xs[0] = np.frombuffer(alpha, np.uint8)
     ys_h = []

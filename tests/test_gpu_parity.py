@@ -323,17 +323,29 @@ def test_wide_eval_random_vs_oracle(dcf, lam, nb, m, mode):
             assert np.array_equal(got, O.eval_(P, b, ok, s, xs, nthreads=8)), (lam, nb, b, bound)
 
 
+def _small_auto_depth(nb, m):
+    """Auto depth on the small-batch path (dcf_hip.hip small_prefix_depth): none up to 32768
+    points (the latency kernels' sizes; at N > 32 the pair walk without a table), else 18 below
+    2^18 points and 19 from there, at most 8N - 1, none below 8."""
+    if m <= 32768:
+        return 0
+    d = min(18 if m < (1 << 18) else 19, 8 * nb - 1)
+    return d if d >= 8 else 0
+
+
 @pytest.mark.parametrize("nb,levels,m", [(16, 9, 3000), (16, 15, 20000), (16, 31, 5000), (4, 12, 4000), (3, 23, 2000),
-                                         (1, 5, 700), (5, 33, 1500), (16, -1, 20000), (2, -1, 40000)])
+                                         (1, 5, 700), (5, 33, 1500), (16, -1, 20000), (2, -1, 40000),
+                                         (16, -1, 100000), (4, -1, 300000), (1, -1, 50000), (33, -1, 3000)])
 def test_small_pair_prefix_vs_oracle(dcf, nb, levels, m):
     """Small batches (auto engine: the two-lanes-per-point path, k_eval16_pair) below a
-    shared-prefix table: forced depths (D = 5 .. 31, x-word boundary at N = 3, 5); auto (-1)
-    builds none there (measured slower at C1); both parties and bounds, vs the oracle."""
+    shared-prefix table: forced depths (D = 5 .. 31, x-word boundary at N = 3, 5) and the auto
+    depth (-1: 18 / 19, capped at 8N - 1; none on the latency kernels' sizes, nor at N = 1);
+    both parties and bounds, vs the oracle."""
     rng = np.random.default_rng(4000 + 37 * nb + levels)
     keys = [rng.bytes(32) for _ in range(2)]
     prg, P = dcf.Aes256HirosePrg(keys, 16), O.OraclePrg(keys, 16)
     prg.set_prefix_levels(levels)
-    want_d = min(levels, 28, 8 * nb - 1) if levels > 0 else 0  # auto: no table on the small path
+    want_d = min(levels, 28, 8 * nb - 1) if levels > 0 else _small_auto_depth(nb, m)
     assert prg.eval_prefix_levels(nb, 1, m) == want_d
     d = dcf.DcfImpl(nb, 16, prg)
     for bound in (0, 1):
