@@ -127,7 +127,7 @@ size_t dcf_prg_lambda(const dcf_prg* prg);
 int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
 
 /* Shared prefix for single-key eval at LAMBDA = 16 (Hirose PRG: stream engine, and the
- * automatic engine's small-batch path at forced depths; Aes128MatyasMeyerOseasPrg: every
+ * automatic engine's small-batch path; Aes128MatyasMeyerOseasPrg: every
  * engine setting) and, per key, for the LAMBDA >= 32
  * stream head (bytes [0,32) of the walk and the t-vector rows, 80 B per node).
  * Every point's walk (lib.rs:174-189) passes through the node of the key's GGM
@@ -137,7 +137,9 @@ int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
  * D fewer levels per point, identical output bytes.
  *   levels = -1: automatic (the default): D = log2(points) (Aes128MatyasMeyerOseasPrg:
  *                log2(points) - 1), at most 27 (LAMBDA >= 32: log2(points) - 1, at most
- *                22), none below 8 or (LAMBDA = 16) for small batches;
+ *                22), none below 8; Hirose small batches (32768 < points < 2^19 on the
+ *                pair walk): 18 below 2^18 points, 19 above (8.7e6 / 17.3e6 B of rows), at most
+ *                8N - 1; none for Aes128MatyasMeyerOseasPrg small batches or up to 32768 points;
  *   levels =  0: off;  levels > 0: that depth (capped at 28 (LAMBDA >= 32: 30) and
  *                at 8N - 1).
  * The table and its build buffers are one allocation of the call's workspace; they stay
