@@ -138,7 +138,7 @@ int dcf_prg_set_eval_mode(dcf_prg* prg, int mode);
  *   levels = -1: automatic (the default): D = log2(points) (Aes128MatyasMeyerOseasPrg:
  *                log2(points) - 1), at most 27 (LAMBDA >= 32: log2(points) - 1, at most
  *                22), none below 8; Hirose small batches (32768 < points < 2^19 on the
- *                pair walk): 18 below 2^18 points, 19 above (8.7e6 / 17.3e6 B of rows), at most
+ *                pair walk): 18 below 2^18 points, 19 above (1.7e7 / 3.4e7 B with the build buffers), at most
  *                8N - 1; none for Aes128MatyasMeyerOseasPrg small batches or up to 32768 points;
  *   levels =  0: off;  levels > 0: that depth (capped at 28 (LAMBDA >= 32: 30) and
  *                at 8N - 1).
